@@ -1,0 +1,118 @@
+"""ctypes mirror of include/mgx.h (the library's C-ABI) and model packing.
+
+``pack_model(model)`` turns a compiled :class:`~.mjcf.Model` into an ``mgx_model_desc``
+whose pointers reference numpy arrays kept alive by the returned holder.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .mjcf import Model
+
+P_I32 = C.POINTER(C.c_int32)
+P_U32 = C.POINTER(C.c_uint32)
+P_F64 = C.POINTER(C.c_double)
+
+# (field, kind) in declaration order of mgx_model_desc
+_INT_SIZES = ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "npair", "nM", "nmaskword",
+              "solver", "integrator", "cone", "iterations", "pad0"]
+_REAL_SCALARS = ["timestep", "tolerance", "impratio", "meaninertia"]
+_ARRAYS = [
+    ("body_parentid", "i"), ("body_rootid", "i"), ("body_weldid", "i"), ("body_jntnum", "i"),
+    ("body_jntadr", "i"), ("body_dofnum", "i"), ("body_dofadr", "i"), ("body_geomnum", "i"),
+    ("body_geomadr", "i"), ("body_subtree_end", "i"), ("body_dofmask", "u"),
+    ("body_pos", "d"), ("body_quat", "d"), ("body_ipos", "d"), ("body_iquat", "d"),
+    ("body_mass", "d"), ("body_inertia", "d"), ("body_invweight0", "d"),
+    ("jnt_type", "i"), ("jnt_bodyid", "i"), ("jnt_qposadr", "i"), ("jnt_dofadr", "i"),
+    ("jnt_limited", "i"),
+    ("jnt_pos", "d"), ("jnt_axis", "d"), ("jnt_range", "d"), ("jnt_stiffness", "d"),
+    ("jnt_margin", "d"), ("jnt_solref", "d"), ("jnt_solimp", "d"),
+    ("dof_bodyid", "i"), ("dof_jntid", "i"), ("dof_parentid", "i"), ("dof_Madr", "i"),
+    ("dof_armature", "d"), ("dof_damping", "d"), ("dof_frictionloss", "d"), ("dof_invweight0", "d"),
+    ("geom_type", "i"), ("geom_bodyid", "i"),
+    ("geom_size", "d"), ("geom_pos", "d"), ("geom_quat", "d"), ("geom_rbound", "d"),
+    ("pair_geom", "i"), ("pair_condim", "i"),
+    ("pair_friction", "d"), ("pair_margin", "d"), ("pair_gap", "d"),
+    ("pair_solref", "d"), ("pair_solimp", "d"),
+    ("actuator_trnid", "i"), ("actuator_ctrllimited", "i"), ("actuator_forcelimited", "i"),
+    ("actuator_gear", "d"), ("actuator_ctrlrange", "d"), ("actuator_forcerange", "d"),
+    ("actuator_gainprm", "d"), ("actuator_biasprm", "d"),
+    ("qpos0", "d"), ("qpos_spring", "d"),
+]
+_PTR = {"i": P_I32, "u": P_U32, "d": P_F64}
+_NP = {"i": np.int32, "u": np.uint32, "d": np.float64}
+
+
+class MgxModelDesc(C.Structure):
+    _fields_ = ([(n, C.c_int32) for n in _INT_SIZES] +
+                [(n, C.c_double) for n in _REAL_SCALARS] +
+                [("gravity", C.c_double * 3)] +
+                [(n, _PTR[k]) for n, k in _ARRAYS])
+
+
+class MgxModelInfo(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in
+                ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "npair", "max_nv", "max_nbody",
+                 "max_ncon", "max_nefc", "max_njnt", "precision", "lds_bytes_per_env"]]
+
+
+class MgxState(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("qacc_warmstart", C.c_void_p),
+                ("ctrl", C.c_void_p), ("qfrc_applied", C.c_void_p), ("xfrc_applied", C.c_void_p),
+                ("time", C.c_void_p), ("warning", C.c_void_p)]
+
+
+class MgxFrames(C.Structure):
+    _fields_ = [("xpos", C.c_void_p), ("xquat", C.c_void_p), ("subtree_com", C.c_void_p),
+                ("ncon", C.c_void_p), ("nefc", C.c_void_p), ("niter", C.c_void_p)]
+
+
+class MgxSoccerEnv(C.Structure):
+    _fields_ = [("prev_ball_pos", C.c_void_p), ("prev_robot_pos", C.c_void_p), ("wind", C.c_void_p),
+                ("step", C.c_void_p), ("goal_scored", C.c_void_p), ("stats", C.c_void_p)]
+
+
+class MgxSoccerIds(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in
+                ["torso", "ball", "goalkeeper", "ball_geom", "right_foot", "left_foot", "field_geom",
+                 "ball_qposadr", "ball_dofadr", "gk_qposadr", "gk_dofadr", "max_episode_steps"]] + \
+               [("obs_jnt_qposadr", C.c_int32 * 25), ("obs_jnt_dofadr", C.c_int32 * 25),
+                ("obs_jnt_range", C.c_double * 50),
+                ("robot_geom_mask_lo", C.c_uint64), ("robot_geom_mask_hi", C.c_uint64)]
+
+
+class PackedModel:
+    """Holds an ``MgxModelDesc`` plus the contiguous numpy arrays it points to."""
+
+    def __init__(self, model: Model):
+        self.model = model
+        self.arrays = {}
+        d = MgxModelDesc()
+        A = model.arrays
+        nmask = A["body_dofmask"].shape[1] if A["body_dofmask"].ndim == 2 else 1
+        sizes = dict(nq=model.nq, nv=model.nv, nu=model.nu, nbody=model.nbody, njnt=model.njnt,
+                     ngeom=model.ngeom, npair=int(A["pair_geom"].shape[0]), nM=model.nM,
+                     nmaskword=nmask, solver=model.solver, integrator=model.integrator,
+                     cone=model.cone, iterations=model.iterations, pad0=0)
+        for k, v in sizes.items():
+            setattr(d, k, int(v))
+        d.timestep, d.tolerance = model.timestep, model.tolerance
+        d.impratio, d.meaninertia = model.impratio, model.meaninertia
+        for i in range(3):
+            d.gravity[i] = float(model.gravity[i])
+        for name, kind in _ARRAYS:
+            arr = np.ascontiguousarray(A[name], dtype=_NP[kind]).reshape(-1)
+            if arr.size == 0:
+                arr = np.zeros(1, dtype=_NP[kind])
+            self.arrays[name] = arr
+            setattr(d, name, arr.ctypes.data_as(_PTR[kind]))
+        self.desc = d
+
+    def ref(self):
+        return C.byref(self.desc)
+
+
+def pack_model(model: Model) -> PackedModel:
+    return PackedModel(model)

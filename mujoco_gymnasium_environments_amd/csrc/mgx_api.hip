@@ -1,0 +1,550 @@
+// mgx_api.hip — kernels and the C-ABI of libmgx.so (declared in include/mgx.h).
+//
+// Launch geometry: one 64-thread workgroup (= one wavefront) per environment, dynamic LDS
+// sized from the model (Layout). Kernels never allocate; all state is caller-owned.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mgx.h"
+#include "mgx_soccer.h"
+
+using namespace mgx;
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                  \
+  do {                                                                             \
+    hipError_t _e = (x);                                                           \
+    if (_e != hipSuccess) return fail(MGX_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+}  // namespace
+
+struct mgx_model {
+  int precision;
+  int device;
+  void* dbuf = nullptr;
+  size_t dbytes = 0;
+  DevModel<float> mf;
+  DevModel<double> md;
+  Layout L;
+  bool soccer_ok = false;
+  SoccerIds<float> sf;
+  SoccerIds<double> sd;
+  int npair;
+};
+
+// ------------------------------------------------------------------------- kernels
+template <typename T>
+__global__ void __launch_bounds__(64) k_step(DevModel<T> m, mgx_state s, mgx_frames fr, int n_env, int nsub,
+                                             const uint8_t* mask) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int env = blockIdx.x;
+  if (env >= n_env) return;
+  if (mask && !mask[env]) return;
+  Env<T> e;
+  env_bind(m, e, smem);
+  T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
+  T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
+  load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  int warn = 0;
+  for (int k = 0; k < nsub; k++) warn += mj_step_env(m, e);
+  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  int l = lane_id();
+  if (l == 0 && s.warning) s.warning[env] += warn;
+  if (fr.xpos) for (int k = l; k < 3 * m.nbody; k += 64) ((T*)fr.xpos)[(size_t)env * 3 * m.nbody + k] = e.xpos[k];
+  if (fr.xquat) for (int k = l; k < 4 * m.nbody; k += 64) ((T*)fr.xquat)[(size_t)env * 4 * m.nbody + k] = e.xquat[k];
+  if (fr.subtree_com)
+    for (int k = l; k < 3 * m.nbody; k += 64) ((T*)fr.subtree_com)[(size_t)env * 3 * m.nbody + k] = e.subtree_com[k];
+  if (l == 0) {
+    if (fr.ncon) fr.ncon[env] = e.ncon;
+    if (fr.nefc) fr.nefc[env] = e.nefc;
+    if (fr.niter) fr.niter[env] = e.niter;
+  }
+}
+
+template <typename T>
+__global__ void k_reset(DevModel<T> m, mgx_state s, int n_env, const uint8_t* mask) {
+  int env = blockIdx.x;
+  if (env >= n_env || (mask && !mask[env])) return;
+  int l = threadIdx.x;
+  for (int k = l; k < m.nq; k += 64) ((T*)s.qpos)[(size_t)env * m.nq + k] = m.qpos0[k];
+  for (int k = l; k < m.nv; k += 64) {
+    ((T*)s.qvel)[(size_t)env * m.nv + k] = 0;
+    ((T*)s.qacc_warmstart)[(size_t)env * m.nv + k] = 0;
+    ((T*)s.qfrc_applied)[(size_t)env * m.nv + k] = 0;
+  }
+  for (int k = l; k < m.nu; k += 64) ((T*)s.ctrl)[(size_t)env * m.nu + k] = 0;
+  for (int k = l; k < 6 * m.nbody; k += 64) ((T*)s.xfrc_applied)[(size_t)env * 6 * m.nbody + k] = 0;
+  if (l == 0) ((T*)s.time)[env] = 0;
+}
+
+// Debug dump of one forward pass (stage outputs), offsets from mgx_debug_layout.
+struct DbgOff {
+  int xpos, xquat, xipos, subtree_com, cinert, cdof, qM, qLD, geom_xpos, geom_xmat, ncon, con_dist, con_pos,
+      con_frame, con_geom, nefc, efc_type, efc_id, efc_pos, efc_margin, efc_R, efc_aref, Bmat, cvel, cdof_dot,
+      qfrc_smooth, qacc_smooth, efc_force, qacc, qfrc_constraint, niter, total;
+};
+
+static DbgOff dbg_offsets(int nb, int nv, int nM, int ng, int C, int E) {
+  DbgOff o;
+  int p = 0;
+  auto take = [&](int n) { int r = p; p += n; return r; };
+  o.xpos = take(3 * nb); o.xquat = take(4 * nb); o.xipos = take(3 * nb); o.subtree_com = take(3 * nb);
+  o.cinert = take(10 * nb); o.cdof = take(6 * nv); o.qM = take(nM); o.qLD = take(nM);
+  o.geom_xpos = take(3 * ng); o.geom_xmat = take(9 * ng); o.ncon = take(1); o.con_dist = take(C);
+  o.con_pos = take(3 * C); o.con_frame = take(9 * C); o.con_geom = take(2 * C); o.nefc = take(1);
+  o.efc_type = take(E); o.efc_id = take(E); o.efc_pos = take(E); o.efc_margin = take(E); o.efc_R = take(E);
+  o.efc_aref = take(E); o.Bmat = take(E * nv); o.cvel = take(6 * nb); o.cdof_dot = take(6 * nv);
+  o.qfrc_smooth = take(nv); o.qacc_smooth = take(nv); o.efc_force = take(E); o.qacc = take(nv);
+  o.qfrc_constraint = take(nv); o.niter = take(1); o.total = p;
+  return o;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s, int n_env, T* dbg, DbgOff o) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int env = blockIdx.x;
+  if (env >= n_env) return;
+  Env<T> e;
+  env_bind(m, e, smem);
+  load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied,
+             (T*)s.xfrc_applied, (T*)s.time, env);
+  T* D = dbg + (size_t)env * o.total;
+  int l = lane_id();
+  kinematics(m, e);
+  com_crb(m, e);
+  for (int k = l; k < m.nM; k += 64) D[o.qM + k] = e.qLD[k];
+  wsync();
+  e.diaginv = factor_ld(m, e.qLD);
+  for (int k = l; k < m.nM; k += 64) D[o.qLD + k] = e.qLD[k];
+  collision(m, e);
+  make_constraint(m, e);
+  if (l < m.nv) e.vec0[l] = sqrt(e.diaginv);
+  wsync();
+  transform_rows(m, e);
+  velocity(m, e);
+  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
+  pgs(m, e);
+  wsync();
+  for (int k = l; k < 3 * m.nbody; k += 64) { D[o.xpos + k] = e.xpos[k]; D[o.xipos + k] = e.xipos[k]; D[o.subtree_com + k] = e.subtree_com[k]; }
+  for (int k = l; k < 4 * m.nbody; k += 64) D[o.xquat + k] = e.xquat[k];
+  for (int k = l; k < 10 * m.nbody; k += 64) D[o.cinert + k] = e.cinert[k];
+  for (int k = l; k < 6 * m.nv; k += 64) { D[o.cdof + k] = e.cdof[k]; D[o.cdof_dot + k] = e.cdof_dot[k]; }
+  for (int k = l; k < 6 * m.nbody; k += 64) D[o.cvel + k] = e.cvel[k];
+  for (int k = l; k < 3 * m.ngeom; k += 64) D[o.geom_xpos + k] = e.geom_xpos[k];
+  for (int k = l; k < 9 * m.ngeom; k += 64) D[o.geom_xmat + k] = e.geom_xmat[k];
+  if (l == 0) { D[o.ncon] = (T)e.ncon; D[o.nefc] = (T)e.nefc; D[o.niter] = (T)e.niter; }
+  for (int c = l; c < e.ncon; c += 64) {
+    D[o.con_dist + c] = e.con_dist[c];
+    for (int k = 0; k < 3; k++) D[o.con_pos + 3 * c + k] = e.con_pos[3 * c + k];
+    for (int k = 0; k < 9; k++) D[o.con_frame + 9 * c + k] = e.con_frame[9 * c + k];
+    D[o.con_geom + 2 * c] = (T)e.con_geom[2 * c];
+    D[o.con_geom + 2 * c + 1] = (T)e.con_geom[2 * c + 1];
+  }
+  for (int r = l; r < e.nefc; r += 64) {
+    D[o.efc_type + r] = (T)e.efc_type[r]; D[o.efc_id + r] = (T)e.efc_id[r]; D[o.efc_pos + r] = e.efc_pos[r];
+    D[o.efc_margin + r] = e.efc_margin[r]; D[o.efc_R + r] = e.efc_R[r]; D[o.efc_aref + r] = e.efc_aref[r];
+    D[o.efc_force + r] = e.efc_f[r];
+    for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];
+  }
+  if (l < m.nv) {
+    D[o.qfrc_smooth + l] = e.qfrc_smooth; D[o.qacc_smooth + l] = e.qacc_smooth; D[o.qacc + l] = e.qacc;
+    D[o.qfrc_constraint + l] = e.qfrc_constraint;
+  }
+}
+
+// soccer: mode 0 = step, 1 = reset
+template <typename T, int MODE>
+__global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
+                                               const float* action, const T* draws, float* obs, double* reward,
+                                               uint8_t* terminated, uint8_t* truncated, int n_env,
+                                               const uint8_t* mask) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int env = blockIdx.x;
+  if (env >= n_env) return;
+  if (mask && !mask[env]) return;
+  Env<T> e;
+  env_bind(m, e, smem);
+  T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
+  T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
+  load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  T* prev_ball = (T*)ev.prev_ball_pos + 3 * (size_t)env;
+  T* prev_robot = (T*)ev.prev_robot_pos + 3 * (size_t)env;
+  T* wind = (T*)ev.wind + 3 * (size_t)env;
+  T* stats = (T*)ev.stats + 5 * (size_t)env;
+  int l = lane_id();
+  int warn = 0;
+  if (MODE == 0) {
+    const float* a = action + (size_t)env * m.nu;
+    soccer_pre(m, e, ids, a, prev_ball, wind);
+    warn += mj_step_env(m, e);
+    store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+    soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball, prev_robot, stats,
+                obs + (size_t)env * 80, reward + env, terminated + env, truncated + env);
+  } else {
+    soccer_apply_reset(m, e, ids, draws + (size_t)env * 36, wind);
+    for (int k = 0; k < 10; k++) warn += mj_step_env(m, e);
+    store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+    soccer_obs(m, e, ids, 0, obs + (size_t)env * 80);
+    wsync();
+    if (l < 3) { prev_ball[l] = e.xpos[3 * ids.ball + l]; prev_robot[l] = e.xpos[3 * ids.torso + l]; }
+    if (l < 5) stats[l] = 0;
+    if (l == 0) { ev.step[env] = 0; ev.goal_scored[env] = 0; }
+  }
+  if (l == 0 && s.warning) s.warning[env] += warn;
+}
+
+// ------------------------------------------------------------------------- host side
+namespace {
+
+int align_up(int x, int a) { return (x + a - 1) / a * a; }
+
+Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active) {
+  Layout L{};
+  int p = 0;
+  int al = 16 / real_bytes;  // 16-byte alignment in elements
+  auto take = [&](int n) { int r = p; p = align_up(p + (n > 0 ? n : 1), al); return r; };
+  int nb = d->nbody, nv = d->nv, nj = d->njnt, ng = d->ngeom;
+  L.max_ncon = max_ncon; L.max_nefc = max_nefc; L.max_active = max_active;
+  L.qpos = take(d->nq); L.qvel = take(nv); L.ctrl = take(d->nu); L.xfrc = take(6 * nb);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.ximat = take(9 * nb); L.subtree_com = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb);
+  L.cvel = take(6 * nb); L.cfrc = take(6 * nb); L.xaxis = take(3 * nj); L.xanchor = take(3 * nj);
+  L.cdof = take(6 * nv); L.cdof_dot = take(6 * nv); L.qLD = take(d->nM); L.qMH = take(d->nM);
+  L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
+  L.act_force = take(d->nu); L.con_dist = take(max_ncon); L.con_pos = take(3 * max_ncon);
+  L.con_frame = take(9 * max_ncon); L.efc_pos = take(max_nefc); L.efc_margin = take(max_nefc);
+  L.efc_diag = take(max_nefc); L.efc_K = take(max_nefc); L.efc_B = take(max_nefc); L.efc_imp = take(max_nefc);
+  L.efc_R = take(max_nefc); L.efc_aref = take(max_nefc); L.efc_b = take(max_nefc); L.efc_f = take(max_nefc);
+  L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
+  L.Bmat = take(max_nefc * L.Bstride);
+  L.reals = p;
+  int q = 0;
+  auto takei = [&](int n) { int r = q; q = align_up(q + (n > 0 ? n : 1), 4); return r; };
+  L.con_geom = takei(2 * max_ncon); L.con_pair = takei(max_ncon); L.act_list = takei(max_active);
+  L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
+  L.ints = q;
+  L.bytes = L.reals * real_bytes + L.ints * 4;
+  return L;
+}
+
+template <typename T>
+struct Builder {
+  std::vector<char> host;
+  std::vector<std::pair<size_t, const void**>> fix;  // (offset, pointer slot)
+  size_t add(const void* src, size_t bytes, const void** slot) {
+    size_t off = (host.size() + 15) / 16 * 16;
+    host.resize(off + (bytes ? bytes : 16));
+    if (bytes) memcpy(host.data() + off, src, bytes);
+    fix.push_back({off, slot});
+    return off;
+  }
+  template <typename S>
+  void ints(const S* src, size_t n, const int** slot) {
+    std::vector<int> v(n ? n : 1, 0);
+    for (size_t i = 0; i < n; i++) v[i] = (int)src[i];
+    add(v.data(), v.size() * 4, (const void**)slot);
+  }
+  void reals(const double* src, size_t n, const T** slot) {
+    std::vector<T> v(n ? n : 1, (T)0);
+    for (size_t i = 0; i < n; i++) v[i] = (T)src[i];
+    add(v.data(), v.size() * sizeof(T), (const void**)slot);
+  }
+};
+
+template <typename T>
+int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>& M) {
+  Builder<T> B;
+  int nb = d->nbody, nv = d->nv, nj = d->njnt, ng = d->ngeom, np = d->npair, nu = d->nu;
+  M.nq = d->nq; M.nv = nv; M.nu = nu; M.nbody = nb; M.njnt = nj; M.ngeom = ng; M.npair = np; M.nM = d->nM;
+  M.nmaskword = d->nmaskword; M.solver = d->solver; M.integrator = d->integrator; M.cone = d->cone;
+  M.iterations = d->iterations;
+  M.timestep = (T)d->timestep; M.tolerance = (T)d->tolerance; M.impratio = (T)d->impratio;
+  M.meaninertia = (T)d->meaninertia;
+  for (int k = 0; k < 3; k++) M.gravity[k] = (T)d->gravity[k];
+  // derived tables: body chains, dof ancestors
+  std::vector<int> chain(nb * MGX_MAX_DEPTH, 0), depth(nb, 0);
+  for (int b = 1; b < nb; b++) {
+    std::vector<int> path;
+    for (int i = b; i > 0; i = d->body_parentid[i]) path.push_back(i);
+    if ((int)path.size() > MGX_MAX_DEPTH) return fail(MGX_E_CAPACITY, "body tree deeper than MGX_MAX_DEPTH");
+    depth[b] = (int)path.size();
+    for (int c = 0; c < depth[b]; c++) chain[b * MGX_MAX_DEPTH + c] = path[depth[b] - 1 - c];
+  }
+  std::vector<int> chainlen(nv), anc(nv * MGX_MAX_DEPTH, -1);
+  std::vector<uint64_t> ancmask(nv, 0);
+  for (int k = 0; k < nv; k++) {
+    int t = 0;
+    for (int j = k; j >= 0; j = d->dof_parentid[j], t++) {
+      if (t >= MGX_MAX_DEPTH) return fail(MGX_E_CAPACITY, "dof chain longer than MGX_MAX_DEPTH");
+      anc[k * MGX_MAX_DEPTH + t] = j;
+      if (j != k) ancmask[k] |= 1ull << j;
+    }
+    chainlen[k] = t;
+  }
+  B.ints(d->body_parentid, nb, &M.body_parentid); B.ints(d->body_rootid, nb, &M.body_rootid);
+  B.ints(d->body_jntnum, nb, &M.body_jntnum); B.ints(d->body_jntadr, nb, &M.body_jntadr);
+  B.ints(d->body_dofnum, nb, &M.body_dofnum); B.ints(d->body_dofadr, nb, &M.body_dofadr);
+  B.ints(d->body_subtree_end, nb, &M.body_subtree_end); B.ints(chain.data(), chain.size(), &M.body_chain);
+  B.ints(depth.data(), nb, &M.body_depth);
+  B.add(d->body_dofmask, sizeof(uint32_t) * nb * d->nmaskword, (const void**)&M.body_dofmask);
+  B.reals(d->body_pos, 3 * nb, &M.body_pos); B.reals(d->body_quat, 4 * nb, &M.body_quat);
+  B.reals(d->body_ipos, 3 * nb, &M.body_ipos); B.reals(d->body_iquat, 4 * nb, &M.body_iquat);
+  B.reals(d->body_mass, nb, &M.body_mass); B.reals(d->body_inertia, 3 * nb, &M.body_inertia);
+  B.reals(d->body_invweight0, 2 * nb, &M.body_invweight0);
+  B.ints(d->jnt_type, nj, &M.jnt_type); B.ints(d->jnt_bodyid, nj, &M.jnt_bodyid);
+  B.ints(d->jnt_qposadr, nj, &M.jnt_qposadr); B.ints(d->jnt_dofadr, nj, &M.jnt_dofadr);
+  B.ints(d->jnt_limited, nj, &M.jnt_limited);
+  B.reals(d->jnt_pos, 3 * nj, &M.jnt_pos); B.reals(d->jnt_axis, 3 * nj, &M.jnt_axis);
+  B.reals(d->jnt_range, 2 * nj, &M.jnt_range); B.reals(d->jnt_stiffness, nj, &M.jnt_stiffness);
+  B.reals(d->jnt_margin, nj, &M.jnt_margin); B.reals(d->jnt_solref, 2 * nj, &M.jnt_solref);
+  B.reals(d->jnt_solimp, 5 * nj, &M.jnt_solimp);
+  B.ints(d->dof_bodyid, nv, &M.dof_bodyid); B.ints(d->dof_jntid, nv, &M.dof_jntid);
+  B.ints(d->dof_parentid, nv, &M.dof_parentid); B.ints(d->dof_Madr, nv, &M.dof_Madr);
+  B.ints(chainlen.data(), nv, &M.dof_chainlen); B.ints(anc.data(), anc.size(), &M.dof_anc);
+  B.add(ancmask.data(), 8 * ancmask.size(), (const void**)&M.dof_ancmask);
+  B.reals(d->dof_armature, nv, &M.dof_armature); B.reals(d->dof_damping, nv, &M.dof_damping);
+  B.reals(d->dof_invweight0, nv, &M.dof_invweight0);
+  B.ints(d->geom_type, ng, &M.geom_type); B.ints(d->geom_bodyid, ng, &M.geom_bodyid);
+  B.reals(d->geom_size, 3 * ng, &M.geom_size); B.reals(d->geom_pos, 3 * ng, &M.geom_pos);
+  B.reals(d->geom_quat, 4 * ng, &M.geom_quat); B.reals(d->geom_rbound, ng, &M.geom_rbound);
+  B.ints(d->pair_geom, 2 * np, &M.pair_geom); B.ints(d->pair_condim, np, &M.pair_condim);
+  B.reals(d->pair_friction, 5 * np, &M.pair_friction); B.reals(d->pair_margin, np, &M.pair_margin);
+  B.reals(d->pair_gap, np, &M.pair_gap); B.reals(d->pair_solref, 2 * np, &M.pair_solref);
+  B.reals(d->pair_solimp, 5 * np, &M.pair_solimp);
+  B.ints(d->actuator_trnid, nu, &M.actuator_trnid); B.ints(d->actuator_ctrllimited, nu, &M.actuator_ctrllimited);
+  B.ints(d->actuator_forcelimited, nu, &M.actuator_forcelimited);
+  B.reals(d->actuator_gear, nu, &M.actuator_gear); B.reals(d->actuator_ctrlrange, 2 * nu, &M.actuator_ctrlrange);
+  B.reals(d->actuator_forcerange, 2 * nu, &M.actuator_forcerange);
+  B.reals(d->actuator_gainprm, 3 * nu, &M.actuator_gainprm); B.reals(d->actuator_biasprm, 3 * nu, &M.actuator_biasprm);
+  B.reals(d->qpos0, d->nq, &M.qpos0); B.reals(d->qpos_spring, d->nq, &M.qpos_spring);
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(&out->dbuf, B.host.size()));
+  HIPCHK(hipMemcpy(out->dbuf, B.host.data(), B.host.size(), hipMemcpyHostToDevice));
+  out->dbytes = B.host.size();
+  for (auto& f : B.fix) *f.second = (char*)out->dbuf + f.first;
+  return MGX_OK;
+}
+
+template <typename KernelT>
+int set_lds(KernelT k, int bytes) {
+  if (bytes > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  return MGX_OK;
+}
+
+int check_state(const mgx_state* s) {
+  if (!s || !s->qpos || !s->qvel || !s->qacc_warmstart || !s->ctrl || !s->qfrc_applied || !s->xfrc_applied || !s->time)
+    return fail(MGX_E_ARG, "null state buffer");
+  return MGX_OK;
+}
+
+}  // namespace
+
+template <typename T>
+static void fill_ids(SoccerIds<T>& o, const mgx_soccer_ids* ids, const DevModel<T>& M, const mgx_model_desc* unused) {
+  (void)unused;
+  o.torso = ids->torso; o.ball = ids->ball; o.goalkeeper = ids->goalkeeper; o.ball_geom = ids->ball_geom;
+  o.right_foot = ids->right_foot; o.left_foot = ids->left_foot; o.field_geom = ids->field_geom;
+  o.ball_qposadr = ids->ball_qposadr; o.ball_dofadr = ids->ball_dofadr; o.gk_qposadr = ids->gk_qposadr;
+  o.gk_qfrc_index = ids->gk_dofadr; o.max_episode_steps = ids->max_episode_steps;
+  for (int i = 0; i < 25; i++) {
+    o.obs_qposadr[i] = ids->obs_jnt_qposadr[i];
+    o.obs_dofadr[i] = ids->obs_jnt_dofadr[i];
+    o.obs_lo[i] = (T)ids->obs_jnt_range[2 * i];
+    o.obs_hi[i] = (T)ids->obs_jnt_range[2 * i + 1];
+  }
+  o.robot_mask_lo = ids->robot_geom_mask_lo;
+  o.robot_mask_hi = ids->robot_geom_mask_hi;
+}
+
+extern "C" {
+
+const char* mgx_last_error(void) { return g_err.c_str(); }
+
+int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_model** out) {
+  if (!d || !out) return fail(MGX_E_ARG, "null argument");
+  if (precision != MGX_F32 && precision != MGX_F64) return fail(MGX_E_ARG, "precision must be MGX_F32 or MGX_F64");
+  if (d->nv > MGX_MAX_NV) return fail(MGX_E_CAPACITY, "nv > 64 not supported by the wave-per-env kernel");
+  if (d->nbody > 4096 || d->solver != 0 || d->integrator != 0)
+    return fail(MGX_E_UNSUPPORTED, "this build implements PGS + Euler (solver=PGS, integrator=Euler)");
+  for (int p = 0; p < d->npair; p++)
+    if (d->pair_condim[p] != 1 && d->pair_condim[p] != 3) return fail(MGX_E_UNSUPPORTED, "condim must be 1 or 3");
+  mgx_model* m = new mgx_model();
+  m->precision = precision;
+  m->device = device;
+  m->npair = d->npair;
+  const char* env_nefc = getenv("MGX_MAX_NEFC");
+  const char* env_ncon = getenv("MGX_MAX_NCON");
+  int max_nefc = env_nefc ? atoi(env_nefc) : 192;
+  int max_ncon = env_ncon ? atoi(env_ncon) : 64;
+  if (max_nefc > 64 * MGX_EFC_SLOTS) max_nefc = 64 * MGX_EFC_SLOTS;
+  int rb = precision == MGX_F32 ? 4 : 8;
+  m->L = make_layout(d, rb, max_ncon, max_nefc, 128);
+  int rc;
+  if (precision == MGX_F32) { rc = build_model<float>(d, device, m, m->mf); m->mf.L = m->L; }
+  else { rc = build_model<double>(d, device, m, m->md); m->md.L = m->L; }
+  if (rc != MGX_OK) { delete m; return rc; }
+  if (m->L.bytes > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "per-env LDS exceeds 160 KiB"); }
+  int r2 = precision == MGX_F32
+               ? (set_lds(k_step<float>, m->L.bytes) | set_lds(k_debug_forward<float>, m->L.bytes) |
+                  set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes))
+               : (set_lds(k_step<double>, m->L.bytes) | set_lds(k_debug_forward<double>, m->L.bytes) |
+                  set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes));
+  if (r2 != MGX_OK) { delete m; return r2; }
+  *out = m;
+  return MGX_OK;
+}
+
+int mgx_model_destroy(mgx_model* m) {
+  if (!m) return MGX_OK;
+  if (m->dbuf) (void)hipFree(m->dbuf);
+  delete m;
+  return MGX_OK;
+}
+
+int mgx_model_get_info(const mgx_model* m, mgx_model_info* o) {
+  if (!m || !o) return fail(MGX_E_ARG, "null argument");
+  int nq, nv, nu, nb, nj, ng;
+  if (m->precision == MGX_F32) { nq = m->mf.nq; nv = m->mf.nv; nu = m->mf.nu; nb = m->mf.nbody; nj = m->mf.njnt; ng = m->mf.ngeom; }
+  else { nq = m->md.nq; nv = m->md.nv; nu = m->md.nu; nb = m->md.nbody; nj = m->md.njnt; ng = m->md.ngeom; }
+  o->nq = nq; o->nv = nv; o->nu = nu; o->nbody = nb; o->njnt = nj; o->ngeom = ng; o->npair = m->npair;
+  o->max_nv = MGX_MAX_NV; o->max_nbody = 4096; o->max_ncon = m->L.max_ncon; o->max_nefc = m->L.max_nefc;
+  o->max_njnt = 1 << 20; o->precision = m->precision; o->lds_bytes_per_env = m->L.bytes;
+  return MGX_OK;
+}
+
+int mgx_step(const mgx_model* m, const mgx_state* s, mgx_frames* frames, int n_env, int nsub, const uint8_t* mask,
+             void* stream) {
+  if (!m || n_env < 0 || nsub < 0) return fail(MGX_E_ARG, "bad argument");
+  int rc = check_state(s);
+  if (rc) return rc;
+  if (n_env == 0 || nsub == 0) return MGX_OK;
+  mgx_frames fr{};
+  if (frames) fr = *frames;
+  hipStream_t st = (hipStream_t)stream;
+  if (m->precision == MGX_F32)
+    hipLaunchKernelGGL(k_step<float>, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, fr, n_env, nsub, mask);
+  else
+    hipLaunchKernelGGL(k_step<double>, dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, fr, n_env, nsub, mask);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+int mgx_reset_data(const mgx_model* m, const mgx_state* s, int n_env, const uint8_t* mask, void* stream) {
+  if (!m || n_env < 0) return fail(MGX_E_ARG, "bad argument");
+  int rc = check_state(s);
+  if (rc) return rc;
+  if (n_env == 0) return MGX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (m->precision == MGX_F32) hipLaunchKernelGGL(k_reset<float>, dim3(n_env), dim3(64), 0, st, m->mf, *s, n_env, mask);
+  else hipLaunchKernelGGL(k_reset<double>, dim3(n_env), dim3(64), 0, st, m->md, *s, n_env, mask);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+int mgx_debug_layout(const mgx_model* m, int32_t* offsets, int32_t n) {
+  if (!m || !offsets) return fail(MGX_E_ARG, "null argument");
+  int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
+  int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
+  int nM = m->precision == MGX_F32 ? m->mf.nM : m->md.nM;
+  int ng = m->precision == MGX_F32 ? m->mf.ngeom : m->md.ngeom;
+  DbgOff o = dbg_offsets(nb, nv, nM, ng, m->L.max_ncon, m->L.max_nefc);
+  const int* src = (const int*)&o;
+  int cnt = (int)(sizeof(DbgOff) / sizeof(int));
+  for (int i = 0; i < n && i < cnt; i++) offsets[i] = src[i];
+  return cnt;
+}
+
+int mgx_debug_forward(const mgx_model* m, const mgx_state* s, int n_env, void* dbg, void* stream) {
+  if (!m || !dbg) return fail(MGX_E_ARG, "null argument");
+  int rc = check_state(s);
+  if (rc) return rc;
+  if (n_env <= 0) return MGX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (m->precision == MGX_F32) {
+    DbgOff o = dbg_offsets(m->mf.nbody, m->mf.nv, m->mf.nM, m->mf.ngeom, m->L.max_ncon, m->L.max_nefc);
+    hipLaunchKernelGGL(k_debug_forward<float>, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, n_env, (float*)dbg, o);
+  } else {
+    DbgOff o = dbg_offsets(m->md.nbody, m->md.nv, m->md.nM, m->md.ngeom, m->L.max_ncon, m->L.max_nefc);
+    hipLaunchKernelGGL(k_debug_forward<double>, dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, n_env, (double*)dbg, o);
+  }
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+int mgx_soccer_configure(mgx_model* m, const mgx_soccer_ids* ids) {
+  if (!m || !ids) return fail(MGX_E_ARG, "null argument");
+  if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
+  if (m->precision == MGX_F32) fill_ids(m->sf, ids, m->mf, nullptr);
+  else fill_ids(m->sd, ids, m->md, nullptr);
+  m->soccer_ok = true;
+  return MGX_OK;
+}
+
+// Reset-specific tables (noise joints) ride in the same ids struct; set via this helper.
+int mgx_soccer_configure_reset(mgx_model* m, int root_qposadr, int n_noise, const int32_t* noise_qposadr,
+                               const double* noise_range) {
+  if (!m || n_noise < 0 || n_noise > 29 || (n_noise && (!noise_qposadr || !noise_range)))
+    return fail(MGX_E_ARG, "bad reset table");
+  auto fill = [&](auto& o) {
+    o.root_qposadr = root_qposadr;
+    o.n_noise = n_noise;
+    for (int i = 0; i < n_noise; i++) {
+      o.noise_qposadr[i] = noise_qposadr[i];
+      o.noise_lo[i] = noise_range[2 * i];
+      o.noise_hi[i] = noise_range[2 * i + 1];
+    }
+  };
+  if (m->precision == MGX_F32) fill(m->sf); else fill(m->sd);
+  return MGX_OK;
+}
+
+int mgx_soccer_step(const mgx_model* m, const mgx_state* s, const mgx_soccer_env* e, const float* action, float* obs,
+                    double* reward, uint8_t* terminated, uint8_t* truncated, int n_env, const uint8_t* mask,
+                    void* stream) {
+  if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (!m->soccer_ok) return fail(MGX_E_ARG, "mgx_soccer_configure not called");
+  int rc = check_state(s);
+  if (rc) return rc;
+  if (n_env <= 0) return MGX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (m->precision == MGX_F32)
+    hipLaunchKernelGGL((k_soccer<float, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e, action,
+                       (const float*)nullptr, obs, reward, terminated, truncated, n_env, mask);
+  else
+    hipLaunchKernelGGL((k_soccer<double, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e, action,
+                       (const double*)nullptr, obs, reward, terminated, truncated, n_env, mask);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+int mgx_soccer_reset(const mgx_model* m, const mgx_state* s, const mgx_soccer_env* e, const void* draws, float* obs,
+                     int n_env, const uint8_t* mask, void* stream) {
+  if (!m || !e || !draws || !obs) return fail(MGX_E_ARG, "null argument");
+  if (!m->soccer_ok) return fail(MGX_E_ARG, "mgx_soccer_configure not called");
+  int rc = check_state(s);
+  if (rc) return rc;
+  if (n_env <= 0) return MGX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (m->precision == MGX_F32)
+    hipLaunchKernelGGL((k_soccer<float, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e,
+                       (const float*)nullptr, (const float*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
+                       (uint8_t*)nullptr, n_env, mask);
+  else
+    hipLaunchKernelGGL((k_soccer<double, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e,
+                       (const float*)nullptr, (const double*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
+                       (uint8_t*)nullptr, n_env, mask);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+}  // extern "C"

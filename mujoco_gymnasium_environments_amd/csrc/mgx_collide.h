@@ -1,0 +1,333 @@
+// mgx_collide.h — narrowphase primitives, one candidate pair per lane.
+//
+// Semantics follow MuJoCo's mjc_* collision functions [ext] (reached from mj_collision in
+// mj_step, humanoid_soccer_env/soccer_env.py:414): geom types ordered type1 <= type2, contact
+// normal points from geom1 to geom2, `dist` is the signed surface distance (negative =
+// penetration), `pos` is the midpoint between the two surfaces, and a contact exists when
+// dist <= margin. Box-box uses separating axes + reference/incident face clipping (<= 8
+// contacts); capsule-box uses the endpoint spheres plus the deepest interior point. The CPU
+// oracle (oracle/mjref.c) restates the same algorithms in fp64.
+#pragma once
+#include "mgx_common.h"
+
+namespace mgx {
+
+template <typename T>
+struct Con { T dist, pos[3], n[3]; };
+
+template <typename T>
+__device__ __forceinline__ int sph_sph(const T* c1, T r1, const T* c2, T r2, T margin, Con<T>* out) {
+  T dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  T L = normalize3(dv);
+  T dist = L - r1 - r2;
+  if (dist > margin) return 0;
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = dv[k]; out->pos[k] = c1[k] + dv[k] * (r1 + (T)0.5 * dist); }
+  return 1;
+}
+
+template <typename T>
+__device__ __forceinline__ void seg_ends(const T* pos, const T* mat, T hl, T* a, T* b) {
+  for (int k = 0; k < 3; k++) { a[k] = pos[k] - hl * mat[3 * k + 2]; b[k] = pos[k] + hl * mat[3 * k + 2]; }
+}
+
+template <typename T>
+__device__ void seg_seg(const T* p1, const T* q1, const T* p2, const T* q2, T* s, T* t) {
+  T d1[3], d2[3], r[3];
+  for (int k = 0; k < 3; k++) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+  T a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  if (a <= minval<T>() && e <= minval<T>()) { *s = *t = 0; return; }
+  if (a <= minval<T>()) { *s = 0; *t = clampv(f / e, (T)0, (T)1); return; }
+  T c = dot3(d1, r);
+  if (e <= minval<T>()) { *t = 0; *s = clampv(-c / a, (T)0, (T)1); return; }
+  T b = dot3(d1, d2), den = a * e - b * b;
+  T ss = den > (T)1e-12 * a * e ? clampv((b * f - c * e) / den, (T)0, (T)1) : (T)0;
+  T tt = (b * ss + f) / e;
+  if (tt < 0) { tt = 0; ss = clampv(-c / a, (T)0, (T)1); }
+  else if (tt > 1) { tt = 1; ss = clampv((b - c) / a, (T)0, (T)1); }
+  *s = ss; *t = tt;
+}
+
+template <typename T>
+__device__ __forceinline__ T box_sd(const T* p, const T* h, T* e) {
+  bool outside = false;
+  T dv[3];
+  for (int k = 0; k < 3; k++) {
+    T q = clampv(p[k], -h[k], h[k]);
+    dv[k] = p[k] - q;
+    if (dv[k] != 0) outside = true;
+  }
+  if (outside) {
+    T L = normalize3(dv);
+    e[0] = dv[0]; e[1] = dv[1]; e[2] = dv[2];
+    return L;
+  }
+  int best = 0;
+  T bd = h[0] - fabs(p[0]);
+  for (int k = 1; k < 3; k++) {
+    T dk = h[k] - fabs(p[k]);
+    if (dk < bd) { bd = dk; best = k; }
+  }
+  e[0] = e[1] = e[2] = 0;
+  e[best] = p[best] >= 0 ? (T)1 : (T)-1;
+  return -bd;
+}
+
+template <typename T>
+__device__ int sphere_box_core(const T* c, T r, const T* bp, const T* bm, const T* h, T margin, Con<T>* out) {
+  T tmp[3] = {c[0] - bp[0], c[1] - bp[1], c[2] - bp[2]}, pl[3], e[3], ew[3];
+  mulmatTvec3(pl, bm, tmp);
+  T sd = box_sd(pl, h, e);
+  T dist = sd - r;
+  if (dist > margin) return 0;
+  mulmatvec3(ew, bm, e);
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = -ew[k]; out->pos[k] = c[k] - ew[k] * (r + (T)0.5 * dist); }
+  return 1;
+}
+
+template <typename T>
+__device__ int capsule_box(const T* cp, const T* cm, const T* cs, const T* bp, const T* bm, const T* h, T margin,
+                           Con<T>* out) {
+  T a[3], b[3], al[3], bl[3], tmp[3], e[3], p[3];
+  T r = cs[0];
+  seg_ends(cp, cm, cs[1], a, b);
+  for (int k = 0; k < 3; k++) tmp[k] = a[k] - bp[k];
+  mulmatTvec3(al, bm, tmp);
+  for (int k = 0; k < 3; k++) tmp[k] = b[k] - bp[k];
+  mulmatTvec3(bl, bm, tmp);
+  T lo = 0, hi = 1;
+  const T gr = (T)0.6180339887498949;
+  T x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), f1, f2;
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+  f1 = box_sd(p, h, e);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+  f2 = box_sd(p, h, e);
+  for (int it = 0; it < 40; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+      f1 = box_sd(p, h, e);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+      f2 = box_sd(p, h, e);
+    }
+  }
+  T ts = (T)0.5 * (lo + hi);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + ts * (bl[k] - al[k]);
+  T fs = box_sd(p, h, e);
+  T f0 = box_sd(al, h, e), f1e = box_sd(bl, h, e);
+  int n = 0;
+  if (f0 - r <= margin) n += sphere_box_core(a, r, bp, bm, h, margin, out + n);
+  if (f1e - r <= margin) n += sphere_box_core(b, r, bp, bm, h, margin, out + n);
+  if (ts > (T)0.02 && ts < (T)0.98 && fs - r <= margin && fs < (f0 < f1e ? f0 : f1e) - (T)0.01 * r) {
+    T cw[3];
+    for (int k = 0; k < 3; k++) cw[k] = a[k] + ts * (b[k] - a[k]);
+    n += sphere_box_core(cw, r, bp, bm, h, margin, out + n);
+  }
+  return n;
+}
+
+template <typename T>
+__device__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T (*out)[2]) {
+  int m = 0;
+  for (int i = 0; i < n; i++) {
+    T* P = in[i];
+    T* Q = in[(i + 1) % n];
+    T dp = sgn * P[axis] - lim, dq = sgn * Q[axis] - lim;
+    if (dp <= 0) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
+    if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+      T t = dp / (dp - dq);
+      out[m][0] = P[0] + t * (Q[0] - P[0]);
+      out[m][1] = P[1] + t * (Q[1] - P[1]);
+      m++;
+    }
+  }
+  return m;
+}
+
+template <typename T>
+__device__ int box_box(const T* pa, const T* Ra, const T* ha, const T* pb, const T* Rb, const T* hb, T margin,
+                       Con<T>* out) {
+  T d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+  T A[3][3], B[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { A[i][k] = Ra[3 * k + i]; B[i][k] = Rb[3 * k + i]; }
+  T best_face = (T)-1e30, best_edge = (T)-1e30;
+  int face_axis = -1, edge_i = -1, edge_j = -1;
+  T edge_n[3] = {0, 0, 0};
+  for (int ax = 0; ax < 6; ax++) {
+    const T* n = ax < 3 ? A[ax] : B[ax - 3];
+    T ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(A[k], n)); rb += hb[k] * fabs(dot3(B[k], n)); }
+    T s = fabs(dot3(d, n)) - ra - rb;
+    if (s > margin) return 0;
+    if (s > best_face) { best_face = s; face_axis = ax; }
+  }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      T n[3];
+      cross3(n, A[i], B[j]);
+      T L = sqrt(dot3(n, n));
+      if (L < (T)1e-6) continue;
+      for (int k = 0; k < 3; k++) n[k] /= L;
+      T ra = 0, rb = 0;
+      for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(A[k], n)); rb += hb[k] * fabs(dot3(B[k], n)); }
+      T s = fabs(dot3(d, n)) - ra - rb;
+      if (s > margin) return 0;
+      if (s > best_edge) { best_edge = s; edge_i = i; edge_j = j; edge_n[0] = n[0]; edge_n[1] = n[1]; edge_n[2] = n[2]; }
+    }
+  if (edge_i >= 0 && best_edge > best_face + (T)1e-5 + (T)0.05 * fabs(best_face)) {
+    T n[3] = {edge_n[0], edge_n[1], edge_n[2]};
+    if (dot3(n, d) < 0) for (int k = 0; k < 3; k++) n[k] = -n[k];
+    T ca[3] = {pa[0], pa[1], pa[2]}, cb[3] = {pb[0], pb[1], pb[2]};
+    for (int k = 0; k < 3; k++) {
+      if (k != edge_i) { T sg = dot3(A[k], n) >= 0 ? (T)1 : (T)-1; for (int c = 0; c < 3; c++) ca[c] += sg * ha[k] * A[k][c]; }
+      if (k != edge_j) { T sg = dot3(B[k], n) <= 0 ? (T)1 : (T)-1; for (int c = 0; c < 3; c++) cb[c] += sg * hb[k] * B[k][c]; }
+    }
+    T a0[3], a1[3], b0[3], b1[3], s, t, P[3], Q[3];
+    for (int c = 0; c < 3; c++) {
+      a0[c] = ca[c] - ha[edge_i] * A[edge_i][c]; a1[c] = ca[c] + ha[edge_i] * A[edge_i][c];
+      b0[c] = cb[c] - hb[edge_j] * B[edge_j][c]; b1[c] = cb[c] + hb[edge_j] * B[edge_j][c];
+    }
+    seg_seg(a0, a1, b0, b1, &s, &t);
+    for (int c = 0; c < 3; c++) { P[c] = a0[c] + s * (a1[c] - a0[c]); Q[c] = b0[c] + t * (b1[c] - b0[c]); }
+    T dq[3] = {Q[0] - P[0], Q[1] - P[1], Q[2] - P[2]};
+    out[0].dist = dot3(dq, n);
+    if (out[0].dist > margin) return 0;
+    for (int c = 0; c < 3; c++) { out[0].n[c] = n[c]; out[0].pos[c] = (T)0.5 * (P[c] + Q[c]); }
+    return 1;
+  }
+  bool refA = face_axis < 3;
+  int ri = refA ? face_axis : face_axis - 3;
+  const T* pr = refA ? pa : pb;
+  const T* pi = refA ? pb : pa;
+  const T* hr = refA ? ha : hb;
+  const T* hi = refA ? hb : ha;
+  T (*R)[3] = refA ? A : B;
+  T (*I)[3] = refA ? B : A;
+  T toI[3] = {pi[0] - pr[0], pi[1] - pr[1], pi[2] - pr[2]};
+  T nr[3];
+  T sg = dot3(toI, R[ri]) >= 0 ? (T)1 : (T)-1;
+  for (int k = 0; k < 3; k++) nr[k] = sg * R[ri][k];
+  int ii = 0;
+  T bestd = -1;
+  for (int k = 0; k < 3; k++) { T v = fabs(dot3(I[k], nr)); if (v > bestd) { bestd = v; ii = k; } }
+  T si = dot3(I[ii], nr) > 0 ? (T)-1 : (T)1;
+  T fc[3];
+  for (int k = 0; k < 3; k++) fc[k] = pi[k] + si * hi[ii] * I[ii][k];
+  int u = (ii + 1) % 3, v = (ii + 2) % 3;
+  int ru = (ri + 1) % 3, rv = (ri + 2) % 3;
+  T poly[8][2], tmp[8][2];
+  const T sgn4[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
+  for (int c = 0; c < 4; c++) {
+    T P[3], rel[3];
+    for (int k = 0; k < 3; k++) P[k] = fc[k] + sgn4[c][0] * hi[u] * I[u][k] + sgn4[c][1] * hi[v] * I[v][k];
+    for (int k = 0; k < 3; k++) rel[k] = P[k] - pr[k];
+    poly[c][0] = dot3(rel, R[ru]);
+    poly[c][1] = dot3(rel, R[rv]);
+  }
+  int np = 4;
+  np = clip_poly(poly, np, 0, hr[ru], (T)1, tmp);
+  np = clip_poly(tmp, np, 0, hr[ru], (T)-1, poly);
+  np = clip_poly(poly, np, 1, hr[rv], (T)1, tmp);
+  np = clip_poly(tmp, np, 1, hr[rv], (T)-1, poly);
+  T fn[3];
+  for (int k = 0; k < 3; k++) fn[k] = si * I[ii][k];
+  T fndn = dot3(fn, nr);
+  int n = 0;
+  for (int c = 0; c < np && n < MGX_MAX_CONPAIR; c++) {
+    T P[3];
+    for (int k = 0; k < 3; k++) P[k] = pr[k] + poly[c][0] * R[ru][k] + poly[c][1] * R[rv][k] + hr[ri] * nr[k];
+    T rel[3] = {P[0] - fc[0], P[1] - fc[1], P[2] - fc[2]};
+    T t = fabs(fndn) > minval<T>() ? -dot3(rel, fn) / fndn : (T)0;
+    if (t > margin) continue;
+    out[n].dist = t;
+    for (int k = 0; k < 3; k++) {
+      out[n].n[k] = refA ? nr[k] : -nr[k];
+      out[n].pos[k] = P[k] + (T)0.5 * t * nr[k];
+    }
+    n++;
+  }
+  return n;
+}
+
+template <typename T>
+__device__ __forceinline__ int plane_sphere(const T* pp, const T* pm, const T* c, T r, T margin, Con<T>* out) {
+  T n[3] = {pm[2], pm[5], pm[8]};
+  T rel[3] = {c[0] - pp[0], c[1] - pp[1], c[2] - pp[2]};
+  T dist = dot3(rel, n) - r;
+  if (dist > margin) return 0;
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = n[k]; out->pos[k] = c[k] - n[k] * (r + (T)0.5 * dist); }
+  return 1;
+}
+
+template <typename T>
+__device__ int plane_box(const T* pp, const T* pm, const T* bp, const T* bm, const T* h, T margin, Con<T>* out) {
+  T n[3] = {pm[2], pm[5], pm[8]};
+  int cnt = 0;
+  for (int c = 0; c < 8 && cnt < 4; c++) {
+    T v[3], loc[3] = {(c & 1) ? h[0] : -h[0], (c & 2) ? h[1] : -h[1], (c & 4) ? h[2] : -h[2]};
+    mulmatvec3(v, bm, loc);
+    for (int k = 0; k < 3; k++) v[k] += bp[k];
+    T rel[3] = {v[0] - pp[0], v[1] - pp[1], v[2] - pp[2]};
+    T dist = dot3(rel, n);
+    if (dist > margin) continue;
+    out[cnt].dist = dist;
+    for (int k = 0; k < 3; k++) { out[cnt].n[k] = n[k]; out[cnt].pos[k] = v[k] - (T)0.5 * dist * n[k]; }
+    cnt++;
+  }
+  return cnt;
+}
+
+// Dispatch one candidate pair. Geom frames come from LDS.
+template <typename T>
+__device__ int collide_pair(int t1, int t2, const T* p1, const T* m1, const T* s1, const T* p2, const T* m2,
+                            const T* s2, T margin, Con<T>* out) {
+  if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph(p1, s1[0], p2, s2[0], margin, out);
+  if (t1 == GSPHERE && t2 == GCAPSULE) {
+    T a[3], b[3], q[3];
+    seg_ends(p2, m2, s2[1], a, b);
+    T ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p1[0] - a[0], p1[1] - a[1], p1[2] - a[2]};
+    T L2 = dot3(ab, ab), t = L2 > minval<T>() ? clampv(dot3(ap, ab) / L2, (T)0, (T)1) : (T)0;
+    for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k];
+    return sph_sph(p1, s1[0], q, s2[0], margin, out);
+  }
+  if (t1 == GCAPSULE && t2 == GCAPSULE) {
+    T a1[3], b1[3], a2[3], b2[3], s, t, P[3], Q[3];
+    seg_ends(p1, m1, s1[1], a1, b1);
+    seg_ends(p2, m2, s2[1], a2, b2);
+    seg_seg(a1, b1, a2, b2, &s, &t);
+    for (int k = 0; k < 3; k++) { P[k] = a1[k] + s * (b1[k] - a1[k]); Q[k] = a2[k] + t * (b2[k] - a2[k]); }
+    return sph_sph(P, s1[0], Q, s2[0], margin, out);
+  }
+  if (t1 == GSPHERE && t2 == GBOX) return sphere_box_core(p1, s1[0], p2, m2, s2, margin, out);
+  if (t1 == GCAPSULE && t2 == GBOX) return capsule_box(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GBOX && t2 == GBOX) return box_box(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GPLANE && t2 == GSPHERE) return plane_sphere(p1, m1, p2, s2[0], margin, out);
+  if (t1 == GPLANE && t2 == GCAPSULE) {
+    T a[3], b[3];
+    seg_ends(p2, m2, s2[1], a, b);
+    int n = plane_sphere(p1, m1, a, s2[0], margin, out);
+    n += plane_sphere(p1, m1, b, s2[0], margin, out + n);
+    return n;
+  }
+  if (t1 == GPLANE && t2 == GBOX) return plane_box(p1, m1, p2, m2, s2, margin, out);
+  return 0;
+}
+
+// mju_makeFrame: normal -> (normal, tangent1, tangent2)
+template <typename T>
+__device__ __forceinline__ void make_frame(T* f) {
+  normalize3(f);
+  f[3] = f[4] = f[5] = 0;
+  if (f[1] < (T)0.5 && f[1] > (T)-0.5) f[4] = 1; else f[5] = 1;
+  T s = dot3(f, f + 3);
+  for (int k = 0; k < 3; k++) f[3 + k] -= f[k] * s;
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+}  // namespace mgx

@@ -1,0 +1,230 @@
+// mgx_common.h — device model tables, per-env LDS layout and wavefront helpers.
+//
+// Execution model: one 64-lane wavefront = one environment. A workgroup is
+// exactly one wavefront, so __syncthreads() is a cheap wave barrier (s_waitcnt + s_barrier
+// on a single wave) and LDS is private to the env. Lane k owns dof k (nv <= 64), body k,
+// joint k, ... in the stages that parallelise over them; per-row solver data is spread
+// lane r % 64, register slot r / 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MGX_WAVE 64
+#define MGX_MAX_NV 64
+#define MGX_MAX_NBODY 64
+#define MGX_MAX_DEPTH 16      // longest dof chain (root..dof), soccer: 13
+#define MGX_MAX_CONPAIR 8     // contacts per geom pair (box-box)
+#define MGX_EFC_SLOTS 3       // per-lane register slots for row data -> max_nefc <= 192
+
+namespace mgx {
+
+enum { JFREE = 0, JBALL = 1, JSLIDE = 2, JHINGE = 3 };
+enum { GPLANE = 0, GHFIELD = 1, GSPHERE = 2, GCAPSULE = 3, GELLIPSOID = 4, GCYLINDER = 5, GBOX = 6 };
+enum { C_LIMIT_JOINT = 3, C_CONTACT_FRICTIONLESS = 5, C_CONTACT_PYRAMIDAL = 6 };
+
+// LDS layout, in elements of T (reals) or int32 (ints), offsets computed on the host.
+struct Layout {
+  int qpos, qvel, ctrl, xfrc, xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cfrc;
+  int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, geom_xpos, geom_xmat, act_force;
+  int con_dist, con_pos, con_frame;
+  int efc_pos, efc_margin, efc_diag, efc_K, efc_B, efc_imp, efc_R, efc_aref, efc_b, efc_f;
+  int Bmat, Bstride;
+  int reals;  // total reals
+  // int region (after reals)
+  int con_geom, con_pair, act_list, efc_type, efc_id;
+  int ints;
+  int bytes;
+  int max_ncon, max_nefc, max_active;
+};
+
+// Device-resident model: pointers into one device allocation.
+template <typename T>
+struct DevModel {
+  int nq, nv, nu, nbody, njnt, ngeom, npair, nM, nmaskword;
+  int solver, integrator, cone, iterations;
+  T timestep, tolerance, impratio, meaninertia, gravity[3];
+  // bodies
+  const int *body_parentid, *body_rootid, *body_jntnum, *body_jntadr, *body_dofnum, *body_dofadr;
+  const int *body_subtree_end, *body_chain, *body_depth;  // chain: [nbody][MAX_DEPTH] root..body
+  const uint32_t *body_dofmask;                           // [nbody][nmaskword]
+  const T *body_pos, *body_quat, *body_ipos, *body_iquat, *body_mass, *body_inertia, *body_invweight0;
+  // joints
+  const int *jnt_type, *jnt_bodyid, *jnt_qposadr, *jnt_dofadr, *jnt_limited;
+  const T *jnt_pos, *jnt_axis, *jnt_range, *jnt_stiffness, *jnt_margin, *jnt_solref, *jnt_solimp;
+  // dofs
+  const int *dof_bodyid, *dof_jntid, *dof_parentid, *dof_Madr, *dof_chainlen, *dof_anc;  // anc: [nv][MAX_DEPTH]
+  const uint64_t *dof_ancmask;  // bit i set if dof i is a strict ancestor of the dof
+  const T *dof_armature, *dof_damping, *dof_invweight0;
+  // geoms
+  const int *geom_type, *geom_bodyid;
+  const T *geom_size, *geom_pos, *geom_quat, *geom_rbound;
+  // pairs
+  const int *pair_geom, *pair_condim;
+  const T *pair_friction, *pair_margin, *pair_gap, *pair_solref, *pair_solimp;
+  // actuators
+  const int *actuator_trnid, *actuator_ctrllimited, *actuator_forcelimited;
+  const T *actuator_gear, *actuator_ctrlrange, *actuator_forcerange, *actuator_gainprm, *actuator_biasprm;
+  const T *qpos0, *qpos_spring;
+  Layout L;
+};
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__device__ __forceinline__ float readlane(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+__device__ __forceinline__ double readlane(double x, int l) {
+  int2 v = __builtin_bit_cast(int2, x);
+  v.x = __builtin_amdgcn_readlane(v.x, l);
+  v.y = __builtin_amdgcn_readlane(v.y, l);
+  return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ int readlane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+
+// full-wave sum, result in every lane (butterfly over 6 xor steps)
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o);
+  return x;
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float x) {
+  // rows of 16 with DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_ror 4 / 8), then the four row
+  // totals through readlane: fixed order, identical in every lane
+  x += dpp_f<0xB1>(x);
+  x += dpp_f<0x4E>(x);
+  x += dpp_f<0x124>(x);
+  x += dpp_f<0x128>(x);
+  return (readlane(x, 0) + readlane(x, 16)) + (readlane(x, 32) + readlane(x, 48));
+}
+__device__ __forceinline__ double wave_sum_dpp(double x) { return wave_sum(x); }
+
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int prefix_count(unsigned long long mask) {  // set bits below this lane
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+}
+__device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
+
+// inclusive-exclusive prefix sum of small ints across the wave
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o);
+    if (lane_id() >= o) x += y;
+  }
+  *total = __shfl(x, 63);
+  return x - v;
+}
+
+// ------------------------------------------------------------------ small math (MuJoCo forms)
+template <typename T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
+template <typename T> __device__ __forceinline__ T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <typename T> __device__ __forceinline__ void cross3(T* r, const T* a, const T* b) {
+  T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <typename T> __device__ __forceinline__ T minval() { return (T)1e-15; }
+template <> __device__ __forceinline__ float minval<float>() { return 1e-15f; }
+
+template <typename T> __device__ __forceinline__ T normalize3(T* v) {
+  T n = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  if (n < minval<T>()) { v[0] = 1; v[1] = 0; v[2] = 0; }
+  else { T s = (T)1 / n; v[0] *= s; v[1] *= s; v[2] *= s; }
+  return n;
+}
+template <typename T> __device__ __forceinline__ void normalize4(T* q) {
+  T n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < minval<T>()) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else if (fabs(n - (T)1) > minval<T>()) { T s = (T)1 / n; q[0] *= s; q[1] *= s; q[2] *= s; q[3] *= s; }
+}
+template <typename T> __device__ __forceinline__ void mulquat(T* r, const T* a, const T* b) {
+  T t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  T t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  T t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  T t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+template <typename T> __device__ __forceinline__ void quat2mat(T* r, const T* q) {
+  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
+    r[0] = 1; r[1] = 0; r[2] = 0; r[3] = 0; r[4] = 1; r[5] = 0; r[6] = 0; r[7] = 0; r[8] = 1;
+    return;
+  }
+  T q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  T q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  T q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  r[0] = q00 + q11 - q22 - q33; r[4] = q00 - q11 + q22 - q33; r[8] = q00 - q11 - q22 + q33;
+  r[1] = 2 * (q12 - q03); r[2] = 2 * (q13 + q02); r[3] = 2 * (q12 + q03);
+  r[5] = 2 * (q23 - q01); r[6] = 2 * (q13 - q02); r[7] = 2 * (q23 + q01);
+}
+template <typename T> __device__ __forceinline__ void rotvecquat(T* r, const T* v, const T* q) {
+  if (v[0] == 0 && v[1] == 0 && v[2] == 0) { r[0] = r[1] = r[2] = 0; return; }
+  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) { r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; return; }
+  T t0 = q[0] * v[0] + q[2] * v[2] - q[3] * v[1];
+  T t1 = q[0] * v[1] + q[3] * v[0] - q[1] * v[2];
+  T t2 = q[0] * v[2] + q[1] * v[1] - q[2] * v[0];
+  T o0 = v[0] + 2 * (q[2] * t2 - q[3] * t1);
+  T o1 = v[1] + 2 * (q[3] * t0 - q[1] * t2);
+  T o2 = v[2] + 2 * (q[1] * t1 - q[2] * t0);
+  r[0] = o0; r[1] = o1; r[2] = o2;
+}
+template <typename T> __device__ __forceinline__ void axisangle2quat(T* q, const T* ax, T ang) {
+  if (ang == 0) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  T s = sin(ang * (T)0.5);
+  q[0] = cos(ang * (T)0.5); q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
+}
+template <typename T> __device__ __forceinline__ void mulmatvec3(T* r, const T* M, const T* v) {
+  T t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+  T t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+  T t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <typename T> __device__ __forceinline__ void mulmatTvec3(T* r, const T* M, const T* v) {
+  T t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
+  T t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
+  T t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <typename T> __device__ __forceinline__ bool isbad(T x) { return x != x || x > (T)1e10 || x < (T)-1e10; }
+
+template <typename T> __device__ __forceinline__ T dot6(const T* a, const T* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+template <typename T> __device__ __forceinline__ void mulinertvec(T* res, const T* i, const T* v) {
+  res[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  res[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  res[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  res[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  res[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  res[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+template <typename T> __device__ __forceinline__ void crossmotion(T* res, const T* v, const T* u) {
+  res[0] = -v[2] * u[1] + v[1] * u[2];
+  res[1] = v[2] * u[0] - v[0] * u[2];
+  res[2] = -v[1] * u[0] + v[0] * u[1];
+  res[3] = -v[2] * u[4] + v[1] * u[5];
+  res[4] = v[2] * u[3] - v[0] * u[5];
+  res[5] = -v[1] * u[3] + v[0] * u[4];
+  res[3] += -v[5] * u[1] + v[4] * u[2];
+  res[4] += v[5] * u[0] - v[3] * u[2];
+  res[5] += -v[4] * u[0] + v[3] * u[1];
+}
+template <typename T> __device__ __forceinline__ void crossforce(T* res, const T* v, const T* f) {
+  res[0] = -v[2] * f[1] + v[1] * f[2];
+  res[1] = v[2] * f[0] - v[0] * f[2];
+  res[2] = -v[1] * f[0] + v[0] * f[1];
+  res[3] = -v[2] * f[4] + v[1] * f[5];
+  res[4] = v[2] * f[3] - v[0] * f[5];
+  res[5] = -v[1] * f[3] + v[0] * f[4];
+  res[0] += -v[5] * f[4] + v[4] * f[5];
+  res[1] += v[5] * f[3] - v[3] * f[5];
+  res[2] += -v[4] * f[3] + v[3] * f[4];
+}
+
+}  // namespace mgx

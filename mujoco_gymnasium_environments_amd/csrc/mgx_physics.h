@@ -1,0 +1,897 @@
+// mgx_physics.h — one mj_step for one env, executed by one wavefront.
+//
+// Stage order restates MuJoCo's mj_step [ext] as reached from the reference's hot path
+// (humanoid_soccer_env/soccer_env.py:414): checkPos/Vel -> kinematics -> comPos -> CRB ->
+// factorM -> collision -> makeConstraint -> (B = D^-1/2 L^-T J') -> comVel -> passive ->
+// RNE -> actuation -> xfrc -> qacc_smooth -> PGS (warmstart) -> checkAcc -> Euler with
+// implicit damping -> integratePos.
+//
+// Data placement: everything per-env lives in LDS; dof-indexed vectors that
+// only feed solves live in registers (lane k = dof k) and move with readlane; the constraint
+// Jacobian is never stored — each row is turned into B_r = D^-1/2 L^-T J_r' in place, so the
+// Delassus operator is A = B B' + R and PGS keeps v = B' f in registers (one LDS row read and
+// one wave reduction per row update).
+#pragma once
+#include "mgx_collide.h"
+
+namespace mgx {
+
+template <typename T>
+struct Env {
+  T *qpos, *qvel, *ctrl, *xfrc, *xpos, *xquat, *xmat, *xipos, *ximat, *subtree_com, *cinert, *crb, *cvel, *cfrc;
+  T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *geom_xpos, *geom_xmat, *act_force;
+  T *con_dist, *con_pos, *con_frame;
+  T *efc_pos, *efc_margin, *efc_diag, *efc_K, *efc_B, *efc_imp, *efc_R, *efc_aref, *efc_b, *efc_f;
+  T *Bm;
+  int Bs;
+  int *con_geom, *con_pair, *act_list, *efc_type, *efc_id;
+  int ncon, nefc, niter, overflow;
+  // dof-lane registers
+  T qacc_ws, qfrc_applied, qfrc_smooth, qacc_smooth, qacc, qfrc_constraint, diaginv, time;
+  int chainlen;
+  uint64_t ancmask;
+};
+
+template <typename T>
+__device__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
+  T* R = reinterpret_cast<T*>(smem);
+  const Layout& L = m.L;
+  e.qpos = R + L.qpos; e.qvel = R + L.qvel; e.ctrl = R + L.ctrl; e.xfrc = R + L.xfrc;
+  e.xpos = R + L.xpos; e.xquat = R + L.xquat; e.xmat = R + L.xmat; e.xipos = R + L.xipos;
+  e.ximat = R + L.ximat; e.subtree_com = R + L.subtree_com; e.cinert = R + L.cinert; e.crb = R + L.crb;
+  e.cvel = R + L.cvel; e.cfrc = R + L.cfrc; e.xaxis = R + L.xaxis; e.xanchor = R + L.xanchor;
+  e.cdof = R + L.cdof; e.cdof_dot = R + L.cdof_dot; e.qLD = R + L.qLD; e.qMH = R + L.qMH;
+  e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.geom_xpos = R + L.geom_xpos;
+  e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.con_dist = R + L.con_dist;
+  e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.efc_pos = R + L.efc_pos;
+  e.efc_margin = R + L.efc_margin; e.efc_diag = R + L.efc_diag; e.efc_K = R + L.efc_K;
+  e.efc_B = R + L.efc_B; e.efc_imp = R + L.efc_imp; e.efc_R = R + L.efc_R; e.efc_aref = R + L.efc_aref;
+  e.efc_b = R + L.efc_b; e.efc_f = R + L.efc_f; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
+  int* I = reinterpret_cast<int*>(R + L.reals);
+  e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
+  e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id;
+  int l = lane_id();
+  e.chainlen = l < m.nv ? m.dof_chainlen[l] : 0;
+  e.ancmask = l < m.nv ? m.dof_ancmask[l] : 0ull;
+  e.overflow = 0;
+}
+
+// ---------------------------------------------------------------- state load / store / reset
+template <typename T>
+__device__ void load_state(const DevModel<T>& m, Env<T>& e, const T* gqpos, const T* gqvel, const T* gqacc,
+                           const T* gctrl, const T* gqfrc, const T* gxfrc, const T* gtime, int env) {
+  int l = lane_id();
+  for (int k = l; k < m.nq; k += 64) e.qpos[k] = gqpos[(size_t)env * m.nq + k];
+  for (int k = l; k < m.nv; k += 64) e.qvel[k] = gqvel[(size_t)env * m.nv + k];
+  for (int k = l; k < m.nu; k += 64) e.ctrl[k] = gctrl[(size_t)env * m.nu + k];
+  for (int k = l; k < 6 * m.nbody; k += 64) e.xfrc[k] = gxfrc[(size_t)env * 6 * m.nbody + k];
+  e.qacc_ws = l < m.nv ? gqacc[(size_t)env * m.nv + l] : (T)0;
+  e.qfrc_applied = l < m.nv ? gqfrc[(size_t)env * m.nv + l] : (T)0;
+  e.time = gtime[env];
+  wsync();
+}
+
+template <typename T>
+__device__ void store_state(const DevModel<T>& m, Env<T>& e, T* gqpos, T* gqvel, T* gqacc, T* gctrl, T* gqfrc,
+                            T* gxfrc, T* gtime, int env) {
+  wsync();
+  int l = lane_id();
+  for (int k = l; k < m.nq; k += 64) gqpos[(size_t)env * m.nq + k] = e.qpos[k];
+  for (int k = l; k < m.nv; k += 64) gqvel[(size_t)env * m.nv + k] = e.qvel[k];
+  for (int k = l; k < m.nu; k += 64) gctrl[(size_t)env * m.nu + k] = e.ctrl[k];
+  for (int k = l; k < 6 * m.nbody; k += 64) gxfrc[(size_t)env * 6 * m.nbody + k] = e.xfrc[k];
+  if (l < m.nv) { gqacc[(size_t)env * m.nv + l] = e.qacc_ws; gqfrc[(size_t)env * m.nv + l] = e.qfrc_applied; }
+  if (l == 0) gtime[env] = e.time;
+}
+
+// mj_resetData on the LDS copy (soccer_env.py:354 reaches it; also the bad-state reset)
+template <typename T>
+__device__ void reset_env(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  wsync();
+  for (int k = l; k < m.nq; k += 64) e.qpos[k] = m.qpos0[k];
+  for (int k = l; k < m.nv; k += 64) e.qvel[k] = 0;
+  for (int k = l; k < m.nu; k += 64) e.ctrl[k] = 0;
+  for (int k = l; k < 6 * m.nbody; k += 64) e.xfrc[k] = 0;
+  e.qacc_ws = 0;
+  e.qfrc_applied = 0;
+  e.time = 0;
+  wsync();
+}
+
+template <typename T>
+__device__ bool any_bad(const T* x, int n) {
+  bool b = false;
+  for (int k = lane_id(); k < n; k += 64) b |= isbad(x[k]);
+  return ballot(b) != 0ull;
+}
+
+// ---------------------------------------------------------------- kinematics (mj_kinematics)
+// Lane b recomputes the chain root..b, so no level-by-level barriers are needed.
+template <typename T>
+__device__ void body_pose_step(const DevModel<T>& m, Env<T>& e, int i, T* pos, T* quat, T* mat, bool store_joints) {
+  int ja = m.body_jntadr[i], jn = m.body_jntnum[i];
+  if (jn == 1 && m.jnt_type[ja] == JFREE) {
+    int a = m.jnt_qposadr[ja];
+    pos[0] = e.qpos[a]; pos[1] = e.qpos[a + 1]; pos[2] = e.qpos[a + 2];
+    quat[0] = e.qpos[a + 3]; quat[1] = e.qpos[a + 4]; quat[2] = e.qpos[a + 5]; quat[3] = e.qpos[a + 6];
+    normalize4(quat);
+    if (store_joints) {
+      for (int k = 0; k < 3; k++) { e.xanchor[3 * ja + k] = pos[k]; e.xaxis[3 * ja + k] = m.jnt_axis[3 * ja + k]; }
+    }
+  } else {
+    T np[3], nq[4];
+    mulmatvec3(np, mat, m.body_pos + 3 * i);
+    for (int k = 0; k < 3; k++) np[k] += pos[k];
+    mulquat(nq, quat, m.body_quat + 4 * i);
+    for (int j = ja; j < ja + jn; j++) {
+      int a = m.jnt_qposadr[j];
+      T xaxis[3], xanchor[3];
+      rotvecquat(xaxis, m.jnt_axis + 3 * j, nq);
+      rotvecquat(xanchor, m.jnt_pos + 3 * j, nq);
+      for (int k = 0; k < 3; k++) xanchor[k] += np[k];
+      int t = m.jnt_type[j];
+      if (t == JSLIDE) {
+        T s = e.qpos[a] - m.qpos0[a];
+        for (int k = 0; k < 3; k++) np[k] += xaxis[k] * s;
+      } else if (t == JHINGE || t == JBALL) {
+        T ql[4], v[3];
+        if (t == JBALL) { ql[0] = e.qpos[a]; ql[1] = e.qpos[a + 1]; ql[2] = e.qpos[a + 2]; ql[3] = e.qpos[a + 3]; normalize4(ql); }
+        else axisangle2quat(ql, m.jnt_axis + 3 * j, e.qpos[a] - m.qpos0[a]);
+        mulquat(nq, nq, ql);
+        rotvecquat(v, m.jnt_pos + 3 * j, nq);
+        for (int k = 0; k < 3; k++) np[k] = xanchor[k] - v[k];
+      }
+      if (store_joints) for (int k = 0; k < 3; k++) { e.xaxis[3 * j + k] = xaxis[k]; e.xanchor[3 * j + k] = xanchor[k]; }
+    }
+    pos[0] = np[0]; pos[1] = np[1]; pos[2] = np[2];
+    quat[0] = nq[0]; quat[1] = nq[1]; quat[2] = nq[2]; quat[3] = nq[3];
+  }
+  normalize4(quat);
+  quat2mat(mat, quat);
+}
+
+template <typename T>
+__device__ void kinematics(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  for (int b = l; b < m.nbody; b += 64) {
+    T pos[3] = {0, 0, 0}, quat[4] = {1, 0, 0, 0}, mat[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    int depth = m.body_depth[b];
+    for (int c = 0; c < depth; c++) {
+      int i = m.body_chain[b * MGX_MAX_DEPTH + c];
+      body_pose_step(m, e, i, pos, quat, mat, i == b);
+    }
+    for (int k = 0; k < 3; k++) e.xpos[3 * b + k] = pos[k];
+    for (int k = 0; k < 4; k++) e.xquat[4 * b + k] = quat[k];
+    for (int k = 0; k < 9; k++) e.xmat[9 * b + k] = mat[k];
+    T q[4];
+    T ip[3];
+    mulmatvec3(ip, mat, m.body_ipos + 3 * b);
+    for (int k = 0; k < 3; k++) e.xipos[3 * b + k] = ip[k] + pos[k];
+    mulquat(q, quat, m.body_iquat + 4 * b);
+    quat2mat(e.ximat + 9 * b, q);
+  }
+  wsync();
+  for (int g = l; g < m.ngeom; g += 64) {
+    int b = m.geom_bodyid[g];
+    T q[4], gp[3];
+    mulmatvec3(gp, e.xmat + 9 * b, m.geom_pos + 3 * g);
+    for (int k = 0; k < 3; k++) e.geom_xpos[3 * g + k] = gp[k] + e.xpos[3 * b + k];
+    mulquat(q, e.xquat + 4 * b, m.geom_quat + 4 * g);
+    quat2mat(e.geom_xmat + 9 * g, q);
+  }
+  wsync();
+}
+
+// ---------------------------------------------------------------- comPos, CRB, M
+template <typename T>
+__device__ void inertcom(T* res, const T* inert, const T* mat, const T* dif, T mass) {
+  T tmp[9] = {mat[0] * inert[0], mat[3] * inert[0], mat[6] * inert[0],
+              mat[1] * inert[1], mat[4] * inert[1], mat[7] * inert[1],
+              mat[2] * inert[2], mat[5] * inert[2], mat[8] * inert[2]};
+  res[0] = mat[0] * tmp[0] + mat[1] * tmp[3] + mat[2] * tmp[6];
+  res[1] = mat[3] * tmp[1] + mat[4] * tmp[4] + mat[5] * tmp[7];
+  res[2] = mat[6] * tmp[2] + mat[7] * tmp[5] + mat[8] * tmp[8];
+  res[3] = mat[0] * tmp[1] + mat[1] * tmp[4] + mat[2] * tmp[7];
+  res[4] = mat[0] * tmp[2] + mat[1] * tmp[5] + mat[2] * tmp[8];
+  res[5] = mat[3] * tmp[2] + mat[4] * tmp[5] + mat[5] * tmp[8];
+  res[0] += mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+  res[1] += mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+  res[2] += mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+  res[3] -= mass * dif[0] * dif[1];
+  res[4] -= mass * dif[0] * dif[2];
+  res[5] -= mass * dif[1] * dif[2];
+  res[6] = mass * dif[0]; res[7] = mass * dif[1]; res[8] = mass * dif[2];
+  res[9] = mass;
+}
+
+template <typename T>
+__device__ void com_crb(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  // subtree com: lane b sums its DFS-contiguous subtree
+  for (int b = l; b < m.nbody; b += 64) {
+    T s0 = 0, s1 = 0, s2 = 0, ms = 0;
+    int end = m.body_subtree_end[b];
+    for (int i = b; i < end; i++) {
+      T mi = m.body_mass[i];
+      s0 += e.xipos[3 * i] * mi; s1 += e.xipos[3 * i + 1] * mi; s2 += e.xipos[3 * i + 2] * mi;
+      ms += mi;
+    }
+    if (ms < minval<T>()) { s0 = e.xipos[3 * b]; s1 = e.xipos[3 * b + 1]; s2 = e.xipos[3 * b + 2]; }
+    else { T inv = (T)1 / ms; s0 *= inv; s1 *= inv; s2 *= inv; }
+    e.subtree_com[3 * b] = s0; e.subtree_com[3 * b + 1] = s1; e.subtree_com[3 * b + 2] = s2;
+  }
+  wsync();
+  for (int b = l; b < m.nbody; b += 64) {
+    if (b == 0) { for (int k = 0; k < 10; k++) e.cinert[k] = 0; continue; }
+    T off[3];
+    int r = m.body_rootid[b];
+    for (int k = 0; k < 3; k++) off[k] = e.xipos[3 * b + k] - e.subtree_com[3 * r + k];
+    inertcom(e.cinert + 10 * b, m.body_inertia + 3 * b, e.ximat + 9 * b, off, m.body_mass[b]);
+  }
+  // cdof: lane = dof
+  if (l < m.nv) {
+    int b = m.dof_bodyid[l], j = m.dof_jntid[l], t = m.jnt_type[j], k = l - m.jnt_dofadr[j];
+    T off[3];
+    int r = m.body_rootid[b];
+    for (int c = 0; c < 3; c++) off[c] = e.subtree_com[3 * r + c] - e.xanchor[3 * j + c];
+    T* cd = e.cdof + 6 * l;
+    if (t == JFREE && k < 3) {
+      for (int c = 0; c < 6; c++) cd[c] = 0;
+      cd[3 + k] = 1;
+    } else if (t == JFREE || t == JBALL) {
+      int kk = t == JFREE ? k - 3 : k;
+      T ax[3] = {e.xmat[9 * b + kk], e.xmat[9 * b + kk + 3], e.xmat[9 * b + kk + 6]};
+      cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+      cross3(cd + 3, ax, off);
+    } else if (t == JSLIDE) {
+      cd[0] = cd[1] = cd[2] = 0;
+      cd[3] = e.xaxis[3 * j]; cd[4] = e.xaxis[3 * j + 1]; cd[5] = e.xaxis[3 * j + 2];
+    } else {
+      T ax[3] = {e.xaxis[3 * j], e.xaxis[3 * j + 1], e.xaxis[3 * j + 2]};
+      cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+      cross3(cd + 3, ax, off);
+    }
+  }
+  wsync();
+  // composite inertia: lane b sums cinert over its subtree
+  for (int b = l; b < m.nbody; b += 64) {
+    if (b == 0) continue;
+    T acc[10];
+    for (int k = 0; k < 10; k++) acc[k] = 0;
+    int end = m.body_subtree_end[b];
+    for (int i = b; i < end; i++)
+      for (int k = 0; k < 10; k++) acc[k] += e.cinert[10 * i + k];
+    for (int k = 0; k < 10; k++) e.crb[10 * b + k] = acc[k];
+  }
+  wsync();
+  // qM rows (tree-sparse, dof_Madr layout) and qMH = qM + h*diag(damping)
+  if (l < m.nv) {
+    T buf[6];
+    mulinertvec(buf, e.crb + 10 * m.dof_bodyid[l], e.cdof + 6 * l);
+    int adr = m.dof_Madr[l];
+    int j = l;
+    for (int t = 0; j >= 0; t++, j = m.dof_parentid[j]) {
+      T v = dot6(e.cdof + 6 * j, buf);
+      if (t == 0) v += m.dof_armature[l];
+      e.qLD[adr + t] = v;
+      e.qMH[adr + t] = t == 0 ? v + m.timestep * m.dof_damping[l] : v;
+    }
+  }
+  wsync();
+}
+
+// mj_factorI on an LDS tree-sparse matrix: M = L' D L in place; returns diaginv in a register
+template <typename T>
+__device__ T factor_ld(const DevModel<T>& m, T* LD) {
+  int l = lane_id();
+  for (int k = m.nv - 1; k >= 0; k--) {
+    int akk = m.dof_Madr[k];
+    int mk = m.dof_chainlen[k] - 1;  // number of ancestors
+    T dkk = LD[akk];
+    if (dkk < minval<T>()) dkk = minval<T>();
+    // pairs (t, s): t = 1..mk (ancestor index), s = 0..mk-t
+    int npair = mk * (mk + 1) / 2;
+    T tmp_own = 0;
+    for (int p = l; p < npair; p += 64) {
+      int t = 1, rem = p;
+      while (rem >= mk - t + 1) { rem -= mk - t + 1; t++; }
+      int s = rem;
+      T tmp = LD[akk + t] / dkk;
+      int ai = m.dof_Madr[m.dof_anc[k * MGX_MAX_DEPTH + t]];
+      LD[ai + s] -= LD[akk + t + s] * tmp;
+    }
+    if (l >= 1 && l <= mk) tmp_own = LD[akk + l] / dkk;
+    wsync();
+    if (l >= 1 && l <= mk) LD[akk + l] = tmp_own;
+    if (l == 0) LD[akk] = dkk;
+    wsync();
+  }
+  return l < m.nv ? (T)1 / LD[m.dof_Madr[l]] : (T)0;
+}
+
+// x <- L'^-1 x (lane-distributed vector)
+template <typename T>
+__device__ T solve_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
+  int l = lane_id();
+  for (int k = m.nv - 1; k >= 0; k--) {
+    T xk = readlane(x, k);
+    uint64_t am = m.dof_ancmask[k];
+    if (l < m.nv && ((am >> l) & 1ull)) x -= LD[m.dof_Madr[k] + m.dof_chainlen[k] - e.chainlen] * xk;
+  }
+  return x;
+}
+// x <- L^-1 x
+template <typename T>
+__device__ T solve_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
+  int l = lane_id();
+  int madr = l < m.nv ? m.dof_Madr[l] : 0;
+  for (int i = 0; i < m.nv; i++) {
+    T xi = readlane(x, i);
+    if (l < m.nv && ((e.ancmask >> i) & 1ull)) x -= LD[madr + e.chainlen - m.dof_chainlen[i]] * xi;
+  }
+  return x;
+}
+// y = L x
+template <typename T>
+__device__ T mul_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
+  int l = lane_id();
+  int madr = l < m.nv ? m.dof_Madr[l] : 0;
+  T y = x;
+  for (int i = 0; i < m.nv; i++) {
+    T xi = readlane(x, i);
+    if (l < m.nv && ((e.ancmask >> i) & 1ull)) y += LD[madr + e.chainlen - m.dof_chainlen[i]] * xi;
+  }
+  return y;
+}
+// y = L' u
+template <typename T>
+__device__ T mul_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T u) {
+  int l = lane_id();
+  T y = u;
+  for (int k = 0; k < m.nv; k++) {
+    T uk = readlane(u, k);
+    uint64_t am = m.dof_ancmask[k];
+    if (l < m.nv && ((am >> l) & 1ull)) y += LD[m.dof_Madr[k] + m.dof_chainlen[k] - e.chainlen] * uk;
+  }
+  return y;
+}
+// x = M^-1 y
+template <typename T>
+__device__ T solve_M(const DevModel<T>& m, const Env<T>& e, const T* LD, T diaginv, T y) {
+  T x = solve_LT(m, e, LD, y);
+  x *= diaginv;
+  return solve_L(m, e, LD, x);
+}
+
+// ---------------------------------------------------------------- collision (mj_collision)
+template <typename T>
+__device__ void collision(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  const Layout& L = m.L;
+  // broadphase: bounding spheres (planes always pass); compact survivors in pair order
+  int nact = 0;
+  for (int base = 0; base < m.npair; base += 64) {
+    int p = base + l;
+    bool act = false;
+    if (p < m.npair) {
+      int g1 = m.pair_geom[2 * p], g2 = m.pair_geom[2 * p + 1];
+      T margin = m.pair_margin[p];
+      if (m.geom_type[g1] == GPLANE) {
+        const T* pm = e.geom_xmat + 9 * g1;
+        T n[3] = {pm[2], pm[5], pm[8]};
+        T rel[3] = {e.geom_xpos[3 * g2] - e.geom_xpos[3 * g1], e.geom_xpos[3 * g2 + 1] - e.geom_xpos[3 * g1 + 1],
+                    e.geom_xpos[3 * g2 + 2] - e.geom_xpos[3 * g1 + 2]};
+        act = dot3(rel, n) <= m.geom_rbound[g2] + margin;
+      } else {
+        T dv[3] = {e.geom_xpos[3 * g2] - e.geom_xpos[3 * g1], e.geom_xpos[3 * g2 + 1] - e.geom_xpos[3 * g1 + 1],
+                   e.geom_xpos[3 * g2 + 2] - e.geom_xpos[3 * g1 + 2]};
+        act = sqrt(dot3(dv, dv)) <= m.geom_rbound[g1] + m.geom_rbound[g2] + margin;
+      }
+    }
+    unsigned long long mask = ballot(act);
+    int pos = nact + prefix_count(mask);
+    if (act && pos < L.max_active) e.act_list[pos] = p;
+    nact += popc64(mask);
+  }
+  if (nact > L.max_active) { nact = L.max_active; e.overflow |= 1; }
+  wsync();
+  // narrowphase: one active pair per lane, compaction by exclusive scan keeps pair order
+  int ncon = 0;
+  for (int base = 0; base < nact; base += 64) {
+    int a = base + l;
+    Con<T> rc[MGX_MAX_CONPAIR];
+    int n = 0, p = -1;
+    if (a < nact) {
+      p = e.act_list[a];
+      int g1 = m.pair_geom[2 * p], g2 = m.pair_geom[2 * p + 1];
+      n = collide_pair(m.geom_type[g1], m.geom_type[g2], e.geom_xpos + 3 * g1, e.geom_xmat + 9 * g1,
+                       m.geom_size + 3 * g1, e.geom_xpos + 3 * g2, e.geom_xmat + 9 * g2, m.geom_size + 3 * g2,
+                       m.pair_margin[p], rc);
+    }
+    int total;
+    int off = wave_excl_scan(n, &total);
+    for (int c = 0; c < n; c++) {
+      int k = ncon + off + c;
+      if (k >= L.max_ncon) break;
+      e.con_dist[k] = rc[c].dist;
+      for (int q = 0; q < 3; q++) { e.con_pos[3 * k + q] = rc[c].pos[q]; e.con_frame[9 * k + q] = rc[c].n[q]; }
+      make_frame(e.con_frame + 9 * k);
+      e.con_pair[k] = p;
+      e.con_geom[2 * k] = m.pair_geom[2 * p];
+      e.con_geom[2 * k + 1] = m.pair_geom[2 * p + 1];
+    }
+    ncon += total;
+  }
+  if (ncon > L.max_ncon) { ncon = L.max_ncon; e.overflow |= 2; }
+  e.ncon = ncon;
+  wsync();
+}
+
+// ---------------------------------------------------------------- constraints
+template <typename T>
+__device__ __forceinline__ bool body_has_dof(const DevModel<T>& m, int b, int d) {
+  return (m.body_dofmask[b * m.nmaskword + (d >> 5)] >> (d & 31)) & 1u;
+}
+
+template <typename T>
+__device__ T impedance(const T* solimp, T pos, T margin) {
+  T d0 = clampv(solimp[0], (T)0.0001, (T)0.9999), d1 = clampv(solimp[1], (T)0.0001, (T)0.9999);
+  T width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (d0 == d1 || width <= minval<T>()) return (T)0.5 * (d0 + d1);
+  T x = (pos - margin) / width;
+  if (x < 0) x = -x;
+  if (x >= 1 || x <= 0) return x >= 1 ? d1 : d0;
+  T y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = pow(x, power) / pow(mid, power - 1);
+  else y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+  return d0 + y * (d1 - d0);
+}
+
+// joint limits then pyramidal contacts; rows are written as J and transformed in place
+template <typename T>
+__device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  const Layout& L = m.L;
+  int nefc = 0;
+  // ---- joint limits (lane per joint), order (joint, lower, upper)
+  for (int base = 0; base < m.njnt; base += 64) {
+    int j = base + l;
+    int cnt = 0;
+    T dl = 0, du = 0;
+    bool lo = false, hi = false;
+    if (j < m.njnt && m.jnt_limited[j] && (m.jnt_type[j] == JHINGE || m.jnt_type[j] == JSLIDE)) {
+      T val = e.qpos[m.jnt_qposadr[j]], margin = m.jnt_margin[j];
+      dl = val - m.jnt_range[2 * j];
+      du = m.jnt_range[2 * j + 1] - val;
+      lo = dl < margin;
+      hi = du < margin;
+      cnt = (int)lo + (int)hi;
+    }
+    int total;
+    int off = wave_excl_scan(cnt, &total);
+    int r = nefc + off;
+    for (int side = 0; side < 2; side++) {
+      bool on = side == 0 ? lo : hi;
+      if (!on) continue;
+      if (r < L.max_nefc) {
+        e.efc_type[r] = C_LIMIT_JOINT; e.efc_id[r] = j;
+        e.efc_pos[r] = side == 0 ? dl : du;
+        e.efc_margin[r] = m.jnt_margin[j];
+        e.efc_diag[r] = m.dof_invweight0[m.jnt_dofadr[j]];
+        e.efc_f[r] = side == 0 ? (T)1 : (T)-1;  // J entry, scattered below
+      }
+      r++;
+    }
+    nefc += total;
+  }
+  if (nefc > L.max_nefc) { nefc = L.max_nefc; e.overflow |= 4; }
+  wsync();
+  // zero-fill + set the single nonzero of each limit row (lane per row)
+  for (int r = l; r < nefc; r += 64) {
+    T* row = e.Bm + r * e.Bs;
+    for (int k = 0; k < m.nv; k++) row[k] = 0;
+    row[m.jnt_dofadr[e.efc_id[r]]] = e.efc_f[r];
+  }
+  // ---- contacts: 2*(condim-1) pyramid rows (condim 3) or 1 row (condim 1); lane = dof
+  for (int c = 0; c < e.ncon; c++) {
+    int p = e.con_pair[c];
+    int dim = m.pair_condim[p];
+    int nrow = dim == 1 ? 1 : 4;
+    if (nefc + nrow > L.max_nefc) { e.overflow |= 4; break; }
+    int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
+    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+    const T* fr = e.con_frame + 9 * c;
+    const T* pos = e.con_pos + 3 * c;
+    if (l < m.nv) {
+      T j1[3] = {0, 0, 0}, j2[3] = {0, 0, 0};
+      const T* cd = e.cdof + 6 * l;
+      if (b2 > 0 && body_has_dof(m, b2, l)) {
+        int r2 = m.body_rootid[b2];
+        T off[3] = {pos[0] - e.subtree_com[3 * r2], pos[1] - e.subtree_com[3 * r2 + 1], pos[2] - e.subtree_com[3 * r2 + 2]}, t[3];
+        cross3(t, cd, off);
+        j2[0] = cd[3] + t[0]; j2[1] = cd[4] + t[1]; j2[2] = cd[5] + t[2];
+      }
+      if (b1 > 0 && body_has_dof(m, b1, l)) {
+        int r1 = m.body_rootid[b1];
+        T off[3] = {pos[0] - e.subtree_com[3 * r1], pos[1] - e.subtree_com[3 * r1 + 1], pos[2] - e.subtree_com[3 * r1 + 2]}, t[3];
+        cross3(t, cd, off);
+        j1[0] = cd[3] + t[0]; j1[1] = cd[4] + t[1]; j1[2] = cd[5] + t[2];
+      }
+      T jd[3] = {j2[0] - j1[0], j2[1] - j1[1], j2[2] - j1[2]};
+      T cj0 = fr[0] * jd[0] + fr[1] * jd[1] + fr[2] * jd[2];
+      if (dim == 1) {
+        e.Bm[nefc * e.Bs + l] = cj0;
+      } else {
+        T cj1 = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
+        T cj2 = fr[6] * jd[0] + fr[7] * jd[1] + fr[8] * jd[2];
+        T mu0 = m.pair_friction[5 * p], mu1 = m.pair_friction[5 * p + 1];
+        e.Bm[(nefc + 0) * e.Bs + l] = cj0 + mu0 * cj1;
+        e.Bm[(nefc + 1) * e.Bs + l] = cj0 - mu0 * cj1;
+        e.Bm[(nefc + 2) * e.Bs + l] = cj0 + mu1 * cj2;
+        e.Bm[(nefc + 3) * e.Bs + l] = cj0 - mu1 * cj2;
+      }
+    }
+    if (l < nrow) {
+      int r = nefc + l;
+      T tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      T f = dim == 1 ? (T)0 : m.pair_friction[5 * p + (l >> 1)];
+      e.efc_type[r] = dim == 1 ? C_CONTACT_FRICTIONLESS : C_CONTACT_PYRAMIDAL;
+      e.efc_id[r] = c;
+      e.efc_pos[r] = e.con_dist[c];
+      e.efc_margin[r] = m.pair_margin[p] - m.pair_gap[p];
+      e.efc_diag[r] = tran + f * f * tran;
+    }
+    nefc += nrow;
+  }
+  e.nefc = nefc;
+  wsync();
+  // impedance, K, B, R per row (lane per row)
+  for (int r = l; r < nefc; r += 64) {
+    const T *solref, *solimp;
+    if (e.efc_type[r] == C_LIMIT_JOINT) {
+      solref = m.jnt_solref + 2 * e.efc_id[r];
+      solimp = m.jnt_solimp + 5 * e.efc_id[r];
+    } else {
+      int p = e.con_pair[e.efc_id[r]];
+      solref = m.pair_solref + 2 * p;
+      solimp = m.pair_solimp + 5 * p;
+    }
+    T imp = impedance(solimp, e.efc_pos[r], e.efc_margin[r]);
+    T dmax = clampv(solimp[1], (T)0.0001, (T)0.9999), K, B;
+    if (solref[0] > 0) {
+      T tc = solref[0], dr = solref[1];
+      if (tc < 2 * m.timestep) tc = 2 * m.timestep;
+      K = (T)1 / (dmax * dmax * tc * tc * dr * dr);
+      B = (T)2 / (dmax * tc);
+    } else {
+      K = -solref[0] / (dmax * dmax);
+      B = -solref[1] / dmax;
+    }
+    T R = ((T)1 - imp) * e.efc_diag[r] / imp;
+    e.efc_K[r] = K; e.efc_B[r] = B; e.efc_imp[r] = imp;
+    e.efc_R[r] = R > minval<T>() ? R : minval<T>();
+  }
+  wsync();
+}
+
+// B_r = D^-1/2 L'^-1 J_r' in place (lane per row), sqrtdi in vec0
+template <typename T>
+__device__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  for (int r = l; r < e.nefc; r += 64) {
+    T* x = e.Bm + r * e.Bs;
+    for (int k = m.nv - 1; k >= 0; k--) {
+      T xk = x[k];
+      int a = m.dof_Madr[k] + 1;
+      int mk = m.dof_chainlen[k] - 1;
+      for (int t = 1; t <= mk; t++) x[m.dof_anc[k * MGX_MAX_DEPTH + t]] -= e.qLD[a + t - 1] * xk;
+      x[k] = xk * e.vec0[k];
+    }
+  }
+  wsync();
+}
+
+// ---------------------------------------------------------------- velocity stage
+template <typename T>
+__device__ void velocity(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  // comVel: lane b walks its chain; cdof_dot for the body's own dofs
+  for (int b = l; b < m.nbody; b += 64) {
+    T cvel[6] = {0, 0, 0, 0, 0, 0};
+    int depth = m.body_depth[b];
+    for (int c = 0; c < depth; c++) {
+      int i = m.body_chain[b * MGX_MAX_DEPTH + c];
+      int bda = m.body_dofadr[i], nd = m.body_dofnum[i];
+      bool own = i == b;
+      for (int j = 0; j < nd; j++) {
+        int dof = bda + j;
+        int t = m.jnt_type[m.dof_jntid[dof]];
+        if (t == JFREE) {
+          if (own) for (int q = 0; q < 18; q++) e.cdof_dot[6 * dof + q] = 0;
+          for (int q = 0; q < 3; q++)
+            for (int k = 0; k < 6; k++) cvel[k] += e.cdof[6 * (dof + q) + k] * e.qvel[dof + q];
+          if (own) for (int q = 3; q < 6; q++) crossmotion(e.cdof_dot + 6 * (dof + q), cvel, e.cdof + 6 * (dof + q));
+          for (int q = 3; q < 6; q++)
+            for (int k = 0; k < 6; k++) cvel[k] += e.cdof[6 * (dof + q) + k] * e.qvel[dof + q];
+          j += 5;
+        } else if (t == JBALL) {
+          if (own) for (int q = 0; q < 3; q++) crossmotion(e.cdof_dot + 6 * (dof + q), cvel, e.cdof + 6 * (dof + q));
+          for (int q = 0; q < 3; q++)
+            for (int k = 0; k < 6; k++) cvel[k] += e.cdof[6 * (dof + q) + k] * e.qvel[dof + q];
+          j += 2;
+        } else {
+          if (own) crossmotion(e.cdof_dot + 6 * dof, cvel, e.cdof + 6 * dof);
+          for (int k = 0; k < 6; k++) cvel[k] += e.cdof[6 * dof + k] * e.qvel[dof];
+        }
+      }
+    }
+    for (int k = 0; k < 6; k++) e.cvel[6 * b + k] = cvel[k];
+  }
+  // actuator forces (lane per actuator)
+  for (int u = l; u < m.nu; u += 64) {
+    int j = m.actuator_trnid[u];
+    T ctrl = e.ctrl[u];
+    if (m.actuator_ctrllimited[u]) ctrl = clampv(ctrl, m.actuator_ctrlrange[2 * u], m.actuator_ctrlrange[2 * u + 1]);
+    T g = m.actuator_gear[u];
+    T len = g * e.qpos[m.jnt_qposadr[j]], vel = g * e.qvel[m.jnt_dofadr[j]];
+    const T* gp = m.actuator_gainprm + 3 * u;
+    const T* bp = m.actuator_biasprm + 3 * u;
+    T f = gp[0] * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
+    if (m.actuator_forcelimited[u]) f = clampv(f, m.actuator_forcerange[2 * u], m.actuator_forcerange[2 * u + 1]);
+    e.act_force[u] = f;
+  }
+  wsync();
+  // RNE forward: cacc by chain walk, cfrc_body
+  for (int b = l; b < m.nbody; b += 64) {
+    if (b == 0) { for (int k = 0; k < 6; k++) e.cfrc[k] = 0; continue; }
+    T cacc[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
+    int depth = m.body_depth[b];
+    for (int c = 0; c < depth; c++) {
+      int i = m.body_chain[b * MGX_MAX_DEPTH + c];
+      int bda = m.body_dofadr[i], nd = m.body_dofnum[i];
+      for (int j = 0; j < nd; j++)
+        for (int k = 0; k < 6; k++) cacc[k] += e.cdof_dot[6 * (bda + j) + k] * e.qvel[bda + j];
+    }
+    T f[6], tmp[6], tmp1[6];
+    mulinertvec(f, e.cinert + 10 * b, cacc);
+    mulinertvec(tmp, e.cinert + 10 * b, e.cvel + 6 * b);
+    crossforce(tmp1, e.cvel + 6 * b, tmp);
+    for (int k = 0; k < 6; k++) e.cfrc[6 * b + k] = f[k] + tmp1[k];
+  }
+  wsync();
+  // subtree sums of cfrc into crb storage (cfrc_total), lane per body
+  for (int b = l; b < m.nbody; b += 64) {
+    T acc[6] = {0, 0, 0, 0, 0, 0};
+    if (b > 0) {
+      int end = m.body_subtree_end[b];
+      for (int i = b; i < end; i++)
+        for (int k = 0; k < 6; k++) acc[k] += e.cfrc[6 * i + k];
+    }
+    for (int k = 0; k < 6; k++) e.crb[10 * b + k] = acc[k];  // crb no longer needed
+  }
+  wsync();
+  // per-dof forces
+  if (l < m.nv) {
+    int b = m.dof_bodyid[l];
+    T bias = dot6(e.cdof + 6 * l, e.crb + 10 * b);
+    T passive = -m.dof_damping[l] * e.qvel[l];
+    int j = m.dof_jntid[l];
+    T st = m.jnt_stiffness[j];
+    if (st != 0) {
+      int t = m.jnt_type[j], a = m.jnt_qposadr[j], k = l - m.jnt_dofadr[j];
+      if (t == JHINGE || t == JSLIDE) passive -= st * (e.qpos[a] - m.qpos_spring[a]);
+      else if (t == JFREE && k < 3) passive -= st * (e.qpos[a + k] - m.qpos_spring[a + k]);
+    }
+    T act = 0;
+    for (int u = 0; u < m.nu; u++)
+      if (m.jnt_dofadr[m.actuator_trnid[u]] == l) act += m.actuator_gear[u] * e.act_force[u];
+    // xfrc_applied: J(xipos)' f for every body with a nonzero wrench whose chain holds this dof
+    T xf = 0;
+    for (int i = 1; i < m.nbody; i++) {
+      const T* f = e.xfrc + 6 * i;
+      if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
+      if (!body_has_dof(m, i, l)) continue;
+      int r = m.body_rootid[i];
+      const T* cd = e.cdof + 6 * l;
+      T off[3] = {e.xipos[3 * i] - e.subtree_com[3 * r], e.xipos[3 * i + 1] - e.subtree_com[3 * r + 1],
+                  e.xipos[3 * i + 2] - e.subtree_com[3 * r + 2]}, t[3];
+      cross3(t, cd, off);
+      xf += (cd[3] + t[0]) * f[0] + (cd[4] + t[1]) * f[1] + (cd[5] + t[2]) * f[2] + cd[0] * f[3] + cd[1] * f[4] + cd[2] * f[5];
+    }
+    e.qfrc_smooth = passive - bias + e.qfrc_applied + act + xf;
+  } else {
+    e.qfrc_smooth = 0;
+  }
+}
+
+// ---------------------------------------------------------------- constraint solver (PGS)
+template <typename T>
+__device__ void pgs(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  int ne = e.nefc;
+  T sqrtD = l < m.nv ? sqrt(e.qLD[m.dof_Madr[l]]) : (T)0;
+  if (ne == 0) {
+    e.qacc = e.qacc_smooth;
+    e.qfrc_constraint = 0;
+    e.niter = 0;
+    return;
+  }
+  // w vectors: D^1/2 L x for qvel, qacc_smooth, qacc_warmstart -> vec0 / vec1 / vec2
+  T qv = l < m.nv ? e.qvel[l] : (T)0;
+  T wv = sqrtD * mul_L(m, e, e.qLD, qv);
+  T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
+  T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
+  wsync();
+  if (l < m.nv) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww; }
+  wsync();
+  // per-row: vel, aref, b, warmstart force, AR diag (lane per row; registers by slot)
+  T f[MGX_EFC_SLOTS], bb[MGX_EFC_SLOTS], RR[MGX_EFC_SLOTS], AD[MGX_EFC_SLOTS];
+#pragma unroll
+  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
+    int r = s * 64 + l;
+    f[s] = 0; bb[s] = 0; RR[s] = 0; AD[s] = 1;
+    if (r < ne) {
+      const T* row = e.Bm + r * e.Bs;
+      T dv = 0, ds = 0, dw = 0, nn = 0;
+      for (int k = 0; k < m.nv; k++) {
+        T x = row[k];
+        dv += x * e.vec0[k]; ds += x * e.vec1[k]; dw += x * e.vec2[k]; nn += x * x;
+      }
+      T aref = -e.efc_B[r] * dv - e.efc_K[r] * e.efc_imp[r] * (e.efc_pos[r] - e.efc_margin[r]);
+      e.efc_aref[r] = aref;
+      bb[s] = ds - aref;
+      RR[s] = e.efc_R[r];
+      AD[s] = nn + RR[s];
+      T jar = dw - aref;
+      f[s] = jar < 0 ? -jar / RR[s] : (T)0;
+    }
+  }
+  // v = B' f (lane = dof) and warmstart cost
+  T v = 0;
+#pragma unroll
+  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
+    int cnt = ne - s * 64;
+    if (cnt > 64) cnt = 64;
+    for (int rl = 0; rl < cnt; rl++) {
+      T fr = readlane(f[s], rl);
+      if (l < m.nv) v += fr * e.Bm[(s * 64 + rl) * e.Bs + l];
+    }
+  }
+  wsync();
+  if (l < m.nv) e.vec0[l] = v;
+  wsync();
+  T cpart = 0;
+#pragma unroll
+  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
+    int r = s * 64 + l;
+    if (r < ne) {
+      const T* row = e.Bm + r * e.Bs;
+      T bv = 0;
+      for (int k = 0; k < m.nv; k++) bv += row[k] * e.vec0[k];
+      cpart += f[s] * (bb[s] + (T)0.5 * (bv + RR[s] * f[s]));
+    }
+  }
+  T cost = wave_sum(cpart);
+  if (cost > 0) {
+#pragma unroll
+    for (int s = 0; s < MGX_EFC_SLOTS; s++) f[s] = 0;
+    v = 0;
+  }
+  // Gauss-Seidel sweeps
+  T scale = (T)1 / (m.meaninertia * (T)(m.nv > 1 ? m.nv : 1));
+  int iter = 0;
+  while (iter < m.iterations) {
+    T improvement = 0;
+#pragma unroll
+    for (int s = 0; s < MGX_EFC_SLOTS; s++) {
+      int cnt = ne - s * 64;
+      if (cnt > 64) cnt = 64;
+      for (int rl = 0; rl < cnt; rl++) {
+        int r = s * 64 + rl;
+        T bv = l < m.nv ? e.Bm[r * e.Bs + l] : (T)0;
+        T dot = wave_sum_dpp(bv * v);
+        T fr = readlane(f[s], rl), br = readlane(bb[s], rl), Rr = readlane(RR[s], rl), Ar = readlane(AD[s], rl);
+        T res = br + dot + Rr * fr;
+        T fn = fr - res / Ar;
+        if (fn < 0) fn = 0;
+        T delta = fn - fr;
+        T change = (T)0.5 * delta * delta * Ar + delta * res;
+        if (change > (T)1e-10) { fn = fr; delta = 0; change = 0; }
+        if (l == rl) f[s] = fn;
+        v += delta * bv;
+        improvement -= change;
+      }
+    }
+    iter++;
+    if (improvement * scale < m.tolerance) break;
+  }
+  e.niter = iter;
+#pragma unroll
+  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
+    int r = s * 64 + l;
+    if (r < ne) e.efc_f[r] = f[s];
+  }
+  // qacc = qacc_smooth + L^-1 D^-1/2 v ; qfrc_constraint = L' D^1/2 v
+  T z = l < m.nv ? v * e.diaginv * sqrtD : (T)0;  // D^-1/2 = diaginv * sqrt(D)
+  z = solve_L(m, e, e.qLD, z);
+  e.qacc = e.qacc_smooth + z;
+  e.qfrc_constraint = mul_LT(m, e, e.qLD, sqrtD * v);
+  wsync();
+}
+
+// ---------------------------------------------------------------- integration
+template <typename T>
+__device__ void quat_integrate(T* q, const T* w, T h) {
+  T ax[3] = {w[0], w[1], w[2]}, qr[4];
+  T ang = h * normalize3(ax);
+  axisangle2quat(qr, ax, ang);
+  normalize4(q);
+  mulquat(q, q, qr);
+}
+
+template <typename T>
+__device__ void euler(const DevModel<T>& m, Env<T>& e) {
+  int l = lane_id();
+  bool damp = false;
+  for (int k = 0; k < m.nv; k++) damp |= m.dof_damping[k] > 0;
+  T qa;
+  if (!damp) qa = e.qacc;
+  else {
+    T di = factor_ld(m, e.qMH);
+    qa = solve_M(m, e, e.qMH, di, e.qfrc_smooth + e.qfrc_constraint);
+  }
+  if (l < m.nv) e.qvel[l] += m.timestep * qa;
+  wsync();
+  for (int j = l; j < m.njnt; j += 64) {
+    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j], t = m.jnt_type[j];
+    T h = m.timestep;
+    if (t == JFREE) {
+      for (int k = 0; k < 3; k++) e.qpos[a + k] += h * e.qvel[da + k];
+      quat_integrate(e.qpos + a + 3, e.qvel + da + 3, h);
+    } else if (t == JBALL) {
+      quat_integrate(e.qpos + a, e.qvel + da, h);
+    } else {
+      e.qpos[a] += h * e.qvel[da];
+    }
+  }
+  e.time += m.timestep;
+  wsync();
+}
+
+// ---------------------------------------------------------------- forward + step
+template <typename T>
+__device__ void forward(const DevModel<T>& m, Env<T>& e) {
+  kinematics(m, e);
+  com_crb(m, e);
+  e.diaginv = factor_ld(m, e.qLD);
+  collision(m, e);
+  make_constraint(m, e);
+  // D^-1/2 per dof for the row transform
+  if (lane_id() < m.nv) e.vec0[lane_id()] = sqrt(e.diaginv);
+  wsync();
+  transform_rows(m, e);
+  velocity(m, e);
+  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
+  pgs(m, e);
+}
+
+// returns the number of bad-state resets performed (0..3)
+template <typename T>
+__device__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
+  int warn = 0;
+  if (any_bad(e.qpos, m.nq)) { reset_env(m, e); warn++; }
+  if (any_bad(e.qvel, m.nv)) { reset_env(m, e); warn++; }
+  forward(m, e);
+  if (ballot(lane_id() < m.nv && isbad(e.qacc)) != 0ull) {
+    reset_env(m, e);
+    warn++;
+    forward(m, e);
+  }
+  e.qacc_ws = e.qacc;
+  euler(m, e);
+  return warn;
+}
+
+}  // namespace mgx

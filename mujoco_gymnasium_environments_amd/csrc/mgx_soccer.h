@@ -1,0 +1,235 @@
+// mgx_soccer.h — humanoid_soccer_env task logic fused around the physics step.
+//
+// Restates, per env and on the GPU, the reference's Python around mj_step:
+//   step():          humanoid_soccer_env/soccer_env.py:398-452
+//   goalkeeper:      :506-524   (reads the STALE ball xpos of the previous forward pass,
+//                                writes qfrc_applied[joint id 0]; persists otherwise)
+//   wind:            :526-537   (xfrc_applied[ball, :2] accumulates while ball z > 0.5)
+//   observation:     :539-631   (80 floats; "torso" velocities are qvel[0:6] = goalkeeper +
+//                                ball dofs)
+//   reward:          :633-690, ball contact :787-803, upright :818-833
+//   termination:     :692-716, truncation :427
+//   reset:           :347-396, randomisation :454-504 (applied with the aliasing quirk S1)
+#pragma once
+#include "mgx_physics.h"
+
+namespace mgx {
+
+template <typename T>
+struct SoccerIds {
+  int torso, ball, goalkeeper, ball_geom, right_foot, left_foot, field_geom;
+  int ball_qposadr, ball_dofadr, gk_qposadr, gk_qfrc_index, max_episode_steps;
+  int obs_qposadr[25], obs_dofadr[25];
+  T obs_lo[25], obs_hi[25];
+  uint64_t robot_mask_lo, robot_mask_hi;
+  int root_qposadr;        // jnt_qposadr[0] (soccer_env.py:463,468)
+  int noise_qposadr[29];   // joint_indices -> qposadr (soccer_env.py:480-488)
+  T noise_lo[29], noise_hi[29];
+  int n_noise;
+};
+
+// Pre-physics env logic: action clip -> ctrl, goalkeeper, wind (soccer_env.py:401-411)
+template <typename T>
+__device__ void soccer_pre(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action,
+                           const T* prev_ball, const T* wind) {
+  int l = lane_id();
+  for (int u = l; u < m.nu; u += 64) {
+    float a = action[u];
+    a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);   // action_space bounds, float32
+    e.ctrl[u] = (T)a;
+  }
+  // goalkeeper P-controller on the stale ball position
+  T bx = prev_ball[0], by = prev_ball[1], bz = prev_ball[2];
+  if (bx < (T)-10) {
+    T target = clampv(by, (T)-3, (T)3);
+    T err = target - e.qpos[ids.gk_qposadr];
+    T force = clampv((T)50 * err, (T)-100, (T)100);
+    if (l == ids.gk_qfrc_index) e.qfrc_applied = force;
+  }
+  // wind on the ball body while airborne
+  if (bz > (T)0.5 && l < 2) e.xfrc[6 * ids.ball + l] += wind[0] * wind[1 + l] * (T)0.1;
+  wsync();
+}
+
+template <typename T>
+__device__ __forceinline__ T clip1(T x) { return clampv(x, (T)-1, (T)1); }
+
+template <typename T>
+__device__ T norm3v(T a, T b, T c) { return sqrt(a * a + b * b + c * c); }
+
+// Observation (80 floats) from the forward-pass frames + post-integration qpos/qvel.
+template <typename T>
+__device__ void soccer_obs(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, int step, float* obs) {
+  int l = lane_id();
+  // foot "contact forces": last matching contact wins (soccer_env.py:765-785)
+  int lastR = -1, lastL = -1;
+  for (int base = 0; base < e.ncon; base += 64) {
+    int c = base + l;
+    bool mr = false, ml = false;
+    if (c < e.ncon) {
+      int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
+      mr = (g1 == ids.right_foot && g2 == 0) || (g2 == ids.right_foot && g1 == 0);
+      ml = (g1 == ids.left_foot && g2 == 0) || (g2 == ids.left_foot && g1 == 0);
+    }
+    unsigned long long br = ballot(mr), bl = ballot(ml);
+    if (br) lastR = base + 63 - __clzll(br);
+    if (bl) lastL = base + 63 - __clzll(bl);
+  }
+  const T* tx = e.xpos + 3 * ids.torso;
+  const T* bxp = e.xpos + 3 * ids.ball;
+  for (int i = l; i < 80; i += 64) {
+    T v = 0;
+    if (i < 25) {
+      T q = e.qpos[ids.obs_qposadr[i]], lo = ids.obs_lo[i], hi = ids.obs_hi[i];
+      v = lo < hi ? clip1((T)2 * (q - lo) / (hi - lo) - (T)1) : (T)0;
+    } else if (i < 50) {
+      v = clip1(e.qvel[ids.obs_dofadr[i - 25]] / (T)10);
+    } else if (i < 54) {
+      v = e.xquat[4 * ids.torso + (i - 50)];
+    } else if (i < 57) {
+      v = clip1(e.qvel[i - 54] / (T)5);
+    } else if (i < 60) {
+      v = clip1(e.qvel[3 + (i - 57)] / (T)10);
+    } else if (i < 63) {
+      v = clip1((bxp[i - 60] - tx[i - 60]) / (T)30);
+    } else if (i < 66) {
+      v = clip1(e.qvel[ids.ball_dofadr + (i - 63)] / (T)20);
+    } else if (i < 69) {
+      const T goal[3] = {(T)24.5, (T)0, (T)1.22};
+      v = clip1((goal[i - 66] - tx[i - 66]) / (T)30);
+    } else if (i < 73) {
+      int k = i - 69;
+      int c = k < 2 ? lastR : lastL;
+      T f = 0;
+      if (c >= 0) {
+        if ((k & 1) == 0) f = e.con_dist[c];
+        else {
+          const T* fr = m.pair_friction + 5 * e.con_pair[c];
+          f = sqrt(fr[0] * fr[0] + fr[1] * fr[1]);
+        }
+      }
+      v = clip1(f / (T)1000);
+    } else if (i < 76) {
+      v = clip1(e.subtree_com[3 * ids.torso + (i - 73)] / (T)30);
+    } else if (i == 76) {
+      v = (T)1 - (T)step / (T)ids.max_episode_steps;
+    } else if (i == 77) {
+      T d = norm3v(bxp[0] - tx[0], bxp[1] - tx[1], bxp[2] - tx[2]);
+      v = clampv(d / (T)50, (T)0, (T)1);
+    } else {
+      v = clip1(e.xpos[3 * ids.goalkeeper + (i - 78)] / (T)15);
+    }
+    obs[i] = (float)v;
+  }
+}
+
+template <typename T>
+__device__ bool soccer_ball_contact(Env<T>& e, const SoccerIds<T>& ids) {
+  bool hit = false;
+  for (int base = 0; base < e.ncon; base += 64) {
+    int c = base + lane_id();
+    if (c < e.ncon) {
+      int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
+      if (g1 == ids.ball_geom || g2 == ids.ball_geom) {
+        int other = g1 == ids.ball_geom ? g2 : g1;
+        uint64_t mask = other < 64 ? ids.robot_mask_lo : ids.robot_mask_hi;
+        if (other < 128 && ((mask >> (other & 63)) & 1ull)) hit = true;
+      }
+    }
+  }
+  return ballot(hit) != 0ull;
+}
+
+template <typename T>
+__device__ bool soccer_upright(const Env<T>& e, const SoccerIds<T>& ids) {
+  T q[4] = {e.xquat[4 * ids.torso], e.xquat[4 * ids.torso + 1], e.xquat[4 * ids.torso + 2], e.xquat[4 * ids.torso + 3]};
+  T R[9];
+  quat2mat(R, q);
+  return R[8] > (T)0.7;
+}
+
+// Post-physics: step count, obs, reward, termination, stats, prev snapshots
+template <typename T>
+__device__ void soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
+                            uint8_t* goal_scored, T* prev_ball, T* prev_robot, T* stats, float* obs, double* reward,
+                            uint8_t* terminated, uint8_t* truncated) {
+  int l = lane_id();
+  int st = *step + 1;
+  soccer_obs(m, e, ids, st, obs);
+  const T* tx = e.xpos + 3 * ids.torso;
+  const T* bp = e.xpos + 3 * ids.ball;
+  bool goal_now = bp[0] > (T)24 && fabs(bp[1]) < (T)3.66 && bp[2] < (T)2.44;
+  bool ball_contact = soccer_ball_contact(e, ids);
+  bool upright = soccer_upright(e, ids);
+  // energy term: sum of squares of the clipped float32 action
+  float part = 0.0f;
+  for (int u = l; u < m.nu; u += 64) {
+    float a = action[u];
+    a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);
+    part += a * a;
+  }
+  float energy = wave_sum(part);
+  T r = 0;
+  bool gs = *goal_scored != 0;
+  if (goal_now) { r += (T)10000; gs = true; }
+  if (ball_contact) r += (T)1000;
+  T cur_bd = norm3v(bp[0] - tx[0], bp[1] - tx[1], bp[2] - tx[2]);
+  T prev_bd = norm3v(prev_ball[0] - prev_robot[0], prev_ball[1] - prev_robot[1], prev_ball[2] - prev_robot[2]);
+  if (cur_bd < prev_bd && cur_bd > (T)2) r += (T)500 * (prev_bd - cur_bd);
+  if (upright) r += (T)200;
+  T prev_gd = norm3v(prev_robot[0] - (T)24.5, prev_robot[1], prev_robot[2]);
+  T cur_gd = norm3v(tx[0] - (T)24.5, tx[1], tx[2]);
+  if (cur_gd < prev_gd) r += (T)100 * (prev_gd - cur_gd);
+  r += (T)-0.1 * (T)energy;
+  if (!upright) r += (T)-1000;
+  T prev_bgd = norm3v(prev_ball[0] - (T)24.5, prev_ball[1], prev_ball[2]);
+  T cur_bgd = norm3v(bp[0] - (T)24.5, bp[1], bp[2]);
+  if (cur_bgd < prev_bgd) r += (T)300 * (prev_bgd - cur_bgd);
+  bool term = gs || (!upright && st > 100) ||
+              (fabs(bp[0]) > (T)30 || fabs(bp[1]) > (T)20 || bp[2] < (T)-1 || bp[2] > (T)10) ||
+              (fabs(tx[0]) > (T)30 || fabs(tx[1]) > (T)20 || tx[2] < (T)0 || tx[2] > (T)5);
+  bool trunc = st >= ids.max_episode_steps;
+  // episode stats (soccer_env.py:718-730), then the prev_* snapshots (:444-446)
+  T bv = norm3v(e.qvel[ids.ball_dofadr], e.qvel[ids.ball_dofadr + 1], e.qvel[ids.ball_dofadr + 2]);
+  T dist = norm3v(tx[0] - prev_robot[0], tx[1] - prev_robot[1], tx[2] - prev_robot[2]);
+  wsync();
+  if (l == 0) {
+    if (goal_now) stats[0] += 1;
+    if (ball_contact) stats[1] += 1;
+    stats[2] += dist;
+    if (upright) stats[3] += m.timestep;
+    stats[4] = stats[4] > bv ? stats[4] : bv;
+    *reward = (double)r;
+    *terminated = term;
+    *truncated = trunc;
+    *goal_scored = gs;
+    *step = st;
+  }
+  if (l < 3) { prev_ball[l] = bp[l]; prev_robot[l] = tx[l]; }
+}
+
+// Reset: mj_resetData + the reference's randomisation (draws in reference order), with the
+// jnt_qposadr[0] aliasing quirk (the robot pose lands on goalkeeper + ball qpos).
+template <typename T>
+__device__ void soccer_apply_reset(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const T* draws, T* wind) {
+  reset_env(m, e);
+  int l = lane_id();
+  if (l == 0) {
+    T rx = draws[0], ry = draws[1], ang = draws[2];
+    int a0 = ids.root_qposadr;
+    e.qpos[a0] = rx; e.qpos[a0 + 1] = ry; e.qpos[a0 + 2] = (T)1.4;
+    e.qpos[a0 + 3] = cos(ang / 2); e.qpos[a0 + 4] = 0; e.qpos[a0 + 5] = 0; e.qpos[a0 + 6] = sin(ang / 2);
+    e.qpos[ids.ball_qposadr] = rx + (T)2; e.qpos[ids.ball_qposadr + 1] = ry; e.qpos[ids.ball_qposadr + 2] = (T)0.15;
+    for (int i = 0; i < ids.n_noise; i++) {
+      T lo = ids.noise_lo[i], hi = ids.noise_hi[i];
+      e.qpos[ids.noise_qposadr[i]] = clampv((lo + hi) / (T)2 + draws[3 + i], lo, hi);
+    }
+    e.qpos[ids.gk_qposadr] = draws[3 + ids.n_noise];
+    wind[0] = draws[4 + ids.n_noise];
+    wind[1] = cos(draws[5 + ids.n_noise]);
+    wind[2] = sin(draws[5 + ids.n_noise]);
+  }
+  wsync();
+}
+
+}  // namespace mgx

@@ -1,0 +1,89 @@
+"""Loader for the in-tree HIP library ``libmgx.so`` (C-ABI in include/mgx.h).
+
+The product path has no CPU fallback: if the library is missing or cannot be loaded this
+module raises. ``build()`` compiles it for gfx950 with hipcc (cross-compiles without a GPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from . import cabi
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libmgx.so")
+CSRC = os.path.join(PKG, "csrc")
+SOURCES = ["mgx_api.hip"]
+HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h"]
+
+MGX_OK = 0
+MGX_F32 = 0
+MGX_F64 = 1
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libmgx.so for gfx950 in-tree (hipcc). Returns the library path."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "mgx.h")]
+    if not force and os.path.exists(LIB_PATH):
+        lib_t = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(s) <= lib_t for s in srcs):
+            return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-o", LIB_PATH + ".tmp", os.path.join(CSRC, "mgx_api.hip")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise NativeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    if verbose:
+        print(f"built {LIB_PATH}")
+    return LIB_PATH
+
+
+_lib = None
+
+_VP = C.c_void_p
+_SIGS = {
+    "mgx_model_create": ([C.POINTER(cabi.MgxModelDesc), C.c_int, C.c_int, C.POINTER(_VP)], C.c_int),
+    "mgx_model_destroy": ([_VP], C.c_int),
+    "mgx_model_get_info": ([_VP, C.POINTER(cabi.MgxModelInfo)], C.c_int),
+    "mgx_last_error": ([], C.c_char_p),
+    "mgx_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxFrames), C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_reset_data": ([_VP, C.POINTER(cabi.MgxState), C.c_int, _VP, _VP], C.c_int),
+    "mgx_debug_forward": ([_VP, C.POINTER(cabi.MgxState), C.c_int, _VP, _VP], C.c_int),
+    "mgx_debug_layout": ([_VP, C.POINTER(C.c_int32), C.c_int32], C.c_int),
+    "mgx_soccer_configure": ([_VP, C.POINTER(cabi.MgxSoccerIds)], C.c_int),
+    "mgx_soccer_configure_reset": ([_VP, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double)], C.c_int),
+    "mgx_soccer_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, _VP, _VP, _VP,
+                         C.c_int, _VP, _VP], C.c_int),
+    "mgx_soccer_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, C.c_int, _VP, _VP],
+                         C.c_int),
+}
+EXPORTS = tuple(_SIGS)
+
+
+def lib() -> C.CDLL:
+    """Load libmgx.so (raises NativeError if absent — there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"{LIB_PATH} not found: run __graft_entry__.build() (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        for name, (argt, rest) in _SIGS.items():
+            f = getattr(L, name)
+            f.argtypes = argt
+            f.restype = rest
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc < 0:
+        msg = lib().mgx_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed ({rc}): {msg}")

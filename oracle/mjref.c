@@ -1,0 +1,1234 @@
+/* mjref.c — CPU fp64 oracle: restatement of MuJoCo's mj_step for the reference tasks.
+ * TEST INFRASTRUCTURE ONLY (see mjref.h). Each stage cites the MuJoCo routine it
+ * restates [ext] and the reference call site that reaches it.
+ */
+#include "mjref.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MINVAL 1e-15
+#define MAXVAL 1e10
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+#define MAXCONPAIR 8
+
+enum { JFREE = 0, JBALL = 1, JSLIDE = 2, JHINGE = 3 };
+enum { GPLANE = 0, GHFIELD = 1, GSPHERE = 2, GCAPSULE = 3, GELLIPSOID = 4, GCYLINDER = 5, GBOX = 6 };
+enum { C_EQUALITY = 0, C_FRICTION_DOF, C_FRICTION_TENDON, C_LIMIT_JOINT, C_LIMIT_TENDON,
+       C_CONTACT_FRICTIONLESS, C_CONTACT_PYRAMIDAL, C_CONTACT_ELLIPTIC };
+
+struct ref_data {
+  int ncon_max, nefc_max, nv, nq, nu, nbody, njnt, ngeom, nM;
+  /* state */
+  double *qpos, *qvel, *qacc_warmstart, *ctrl, *qfrc_applied, *xfrc_applied, *time;
+  int *warning;
+  /* position stage */
+  double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis, *geom_xpos, *geom_xmat;
+  double *subtree_com, *cinert, *cdof, *crb, *qM, *qLD, *qLDiagInv;
+  /* velocity / force stage */
+  double *cvel, *cdof_dot, *qfrc_bias, *qfrc_passive, *actuator_force, *qfrc_actuator;
+  double *qfrc_smooth, *qacc_smooth, *qfrc_constraint, *qacc;
+  /* contacts */
+  int *ncon;
+  double *con_dist, *con_pos, *con_frame, *con_friction, *con_includemargin, *con_solref, *con_solimp;
+  int *con_geom, *con_dim, *con_pair;
+  /* constraints */
+  int *nefc;
+  int *efc_type, *efc_id;
+  double *efc_J, *efc_pos, *efc_margin, *efc_diagApprox, *efc_R, *efc_D, *efc_KBIP;
+  double *efc_vel, *efc_aref, *efc_b, *efc_force, *efc_AR;
+  int *solver_niter;
+  /* scratch */
+  double *scratch;
+};
+
+/* ====================================================================== vector helpers */
+static double dot3(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void cross3(double *r, const double *a, const double *b) {
+  double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+static double norm3(const double *a) { return sqrt(dot3(a, a)); }
+static double normalize3(double *v) { /* mju_normalize3 */
+  double n = norm3(v);
+  if (n < MINVAL) { v[0] = 1; v[1] = 0; v[2] = 0; }
+  else { double s = 1 / n; v[0] *= s; v[1] *= s; v[2] *= s; }
+  return n;
+}
+static void normalize4(double *q) { /* mju_normalize4 */
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else if (fabs(n - 1) > MINVAL) { double s = 1 / n; q[0] *= s; q[1] *= s; q[2] *= s; q[3] *= s; }
+}
+static void mulquat(double *r, const double *a, const double *b) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof t);
+}
+static void quat2mat(double *r, const double *q) { /* mju_quat2Mat */
+  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    memcpy(r, I, sizeof I);
+    return;
+  }
+  double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  r[0] = q00 + q11 - q22 - q33; r[4] = q00 - q11 + q22 - q33; r[8] = q00 - q11 - q22 + q33;
+  r[1] = 2 * (q12 - q03); r[2] = 2 * (q13 + q02); r[3] = 2 * (q12 + q03);
+  r[5] = 2 * (q23 - q01); r[6] = 2 * (q13 - q02); r[7] = 2 * (q23 + q01);
+}
+static void rotvecquat(double *r, const double *v, const double *q) { /* mju_rotVecQuat */
+  if (v[0] == 0 && v[1] == 0 && v[2] == 0) { r[0] = r[1] = r[2] = 0; return; }
+  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) { r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; return; }
+  double t[3] = {q[0] * v[0] + q[2] * v[2] - q[3] * v[1],
+                 q[0] * v[1] + q[3] * v[0] - q[1] * v[2],
+                 q[0] * v[2] + q[1] * v[1] - q[2] * v[0]};
+  double o[3] = {v[0] + 2 * (q[2] * t[2] - q[3] * t[1]),
+                 v[1] + 2 * (q[3] * t[0] - q[1] * t[2]),
+                 v[2] + 2 * (q[1] * t[1] - q[2] * t[0])};
+  r[0] = o[0]; r[1] = o[1]; r[2] = o[2];
+}
+static void axisangle2quat(double *q, const double *ax, double ang) {
+  if (ang == 0) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  double s = sin(ang * 0.5);
+  q[0] = cos(ang * 0.5); q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
+}
+static void mulmatvec3(double *r, const double *M, const double *v) { /* r = M v */
+  double t[3] = {M[0] * v[0] + M[1] * v[1] + M[2] * v[2], M[3] * v[0] + M[4] * v[1] + M[5] * v[2],
+                 M[6] * v[0] + M[7] * v[1] + M[8] * v[2]};
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+static void mulmatTvec3(double *r, const double *M, const double *v) { /* r = M' v */
+  double t[3] = {M[0] * v[0] + M[3] * v[1] + M[6] * v[2], M[1] * v[0] + M[4] * v[1] + M[7] * v[2],
+                 M[2] * v[0] + M[5] * v[1] + M[8] * v[2]};
+  r[0] = t[0]; r[1] = t[1]; r[2] = t[2];
+}
+static int isbad(double x) { return x != x || x > MAXVAL || x < -MAXVAL; }
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* ====================================================================== allocation */
+#define ALLOC(f, n) d->f = calloc((size_t)((n) > 0 ? (n) : 1), sizeof(*d->f))
+
+ref_data *ref_create(const mgx_model_desc *m, int ncon_max, int nefc_max) {
+  ref_data *d = calloc(1, sizeof(ref_data));
+  d->ncon_max = ncon_max; d->nefc_max = nefc_max;
+  d->nv = m->nv; d->nq = m->nq; d->nu = m->nu; d->nbody = m->nbody; d->njnt = m->njnt;
+  d->ngeom = m->ngeom; d->nM = m->nM;
+  int nb = m->nbody, nv = m->nv;
+  ALLOC(qpos, m->nq); ALLOC(qvel, nv); ALLOC(qacc_warmstart, nv); ALLOC(ctrl, m->nu);
+  ALLOC(qfrc_applied, nv); ALLOC(xfrc_applied, 6 * nb); ALLOC(time, 1); ALLOC(warning, 1);
+  ALLOC(xpos, 3 * nb); ALLOC(xquat, 4 * nb); ALLOC(xmat, 9 * nb); ALLOC(xipos, 3 * nb);
+  ALLOC(ximat, 9 * nb); ALLOC(xanchor, 3 * m->njnt); ALLOC(xaxis, 3 * m->njnt);
+  ALLOC(geom_xpos, 3 * m->ngeom); ALLOC(geom_xmat, 9 * m->ngeom);
+  ALLOC(subtree_com, 3 * nb); ALLOC(cinert, 10 * nb); ALLOC(cdof, 6 * nv); ALLOC(crb, 10 * nb);
+  ALLOC(qM, m->nM); ALLOC(qLD, m->nM); ALLOC(qLDiagInv, nv);
+  ALLOC(cvel, 6 * nb); ALLOC(cdof_dot, 6 * nv); ALLOC(qfrc_bias, nv); ALLOC(qfrc_passive, nv);
+  ALLOC(actuator_force, m->nu); ALLOC(qfrc_actuator, nv); ALLOC(qfrc_smooth, nv);
+  ALLOC(qacc_smooth, nv); ALLOC(qfrc_constraint, nv); ALLOC(qacc, nv);
+  ALLOC(ncon, 1); ALLOC(con_dist, ncon_max); ALLOC(con_pos, 3 * ncon_max);
+  ALLOC(con_frame, 9 * ncon_max); ALLOC(con_friction, 5 * ncon_max);
+  ALLOC(con_includemargin, ncon_max); ALLOC(con_solref, 2 * ncon_max);
+  ALLOC(con_solimp, 5 * ncon_max); ALLOC(con_geom, 2 * ncon_max); ALLOC(con_dim, ncon_max);
+  ALLOC(con_pair, ncon_max);
+  ALLOC(nefc, 1); ALLOC(efc_type, nefc_max); ALLOC(efc_id, nefc_max);
+  ALLOC(efc_J, (size_t)nefc_max * nv); ALLOC(efc_pos, nefc_max); ALLOC(efc_margin, nefc_max);
+  ALLOC(efc_diagApprox, nefc_max); ALLOC(efc_R, nefc_max); ALLOC(efc_D, nefc_max);
+  ALLOC(efc_KBIP, 4 * nefc_max); ALLOC(efc_vel, nefc_max); ALLOC(efc_aref, nefc_max);
+  ALLOC(efc_b, nefc_max); ALLOC(efc_force, nefc_max);
+  ALLOC(efc_AR, (size_t)nefc_max * nefc_max); ALLOC(solver_niter, 1);
+  ALLOC(scratch, (size_t)nefc_max * nv + 16 * nv + 8 * nefc_max + 64);
+  ref_reset(m, d);
+  return d;
+}
+
+void ref_free(ref_data *d) {
+  if (!d) return;
+  void **p[] = {(void **)&d->qpos, (void **)&d->qvel, (void **)&d->qacc_warmstart, (void **)&d->ctrl,
+                (void **)&d->qfrc_applied, (void **)&d->xfrc_applied, (void **)&d->time,
+                (void **)&d->warning, (void **)&d->xpos, (void **)&d->xquat, (void **)&d->xmat,
+                (void **)&d->xipos, (void **)&d->ximat, (void **)&d->xanchor, (void **)&d->xaxis,
+                (void **)&d->geom_xpos, (void **)&d->geom_xmat, (void **)&d->subtree_com,
+                (void **)&d->cinert, (void **)&d->cdof, (void **)&d->crb, (void **)&d->qM,
+                (void **)&d->qLD, (void **)&d->qLDiagInv, (void **)&d->cvel, (void **)&d->cdof_dot,
+                (void **)&d->qfrc_bias, (void **)&d->qfrc_passive, (void **)&d->actuator_force,
+                (void **)&d->qfrc_actuator, (void **)&d->qfrc_smooth, (void **)&d->qacc_smooth,
+                (void **)&d->qfrc_constraint, (void **)&d->qacc, (void **)&d->ncon,
+                (void **)&d->con_dist, (void **)&d->con_pos, (void **)&d->con_frame,
+                (void **)&d->con_friction, (void **)&d->con_includemargin, (void **)&d->con_solref,
+                (void **)&d->con_solimp, (void **)&d->con_geom, (void **)&d->con_dim,
+                (void **)&d->con_pair, (void **)&d->nefc, (void **)&d->efc_type, (void **)&d->efc_id,
+                (void **)&d->efc_J, (void **)&d->efc_pos, (void **)&d->efc_margin,
+                (void **)&d->efc_diagApprox, (void **)&d->efc_R, (void **)&d->efc_D,
+                (void **)&d->efc_KBIP, (void **)&d->efc_vel, (void **)&d->efc_aref, (void **)&d->efc_b,
+                (void **)&d->efc_force, (void **)&d->efc_AR, (void **)&d->solver_niter,
+                (void **)&d->scratch};
+  for (size_t i = 0; i < sizeof p / sizeof p[0]; i++) free(*p[i]);
+  free(d);
+}
+
+void *ref_field(ref_data *d, const char *name, int *count) {
+  struct { const char *n; void *p; int c; } t[] = {
+    {"qpos", d->qpos, d->nq}, {"qvel", d->qvel, d->nv}, {"qacc_warmstart", d->qacc_warmstart, d->nv},
+    {"ctrl", d->ctrl, d->nu}, {"qfrc_applied", d->qfrc_applied, d->nv},
+    {"xfrc_applied", d->xfrc_applied, 6 * d->nbody}, {"time", d->time, 1}, {"warning", d->warning, 1},
+    {"xpos", d->xpos, 3 * d->nbody}, {"xquat", d->xquat, 4 * d->nbody}, {"xmat", d->xmat, 9 * d->nbody},
+    {"xipos", d->xipos, 3 * d->nbody}, {"ximat", d->ximat, 9 * d->nbody},
+    {"xanchor", d->xanchor, 3 * d->njnt}, {"xaxis", d->xaxis, 3 * d->njnt},
+    {"geom_xpos", d->geom_xpos, 3 * d->ngeom}, {"geom_xmat", d->geom_xmat, 9 * d->ngeom},
+    {"subtree_com", d->subtree_com, 3 * d->nbody}, {"cinert", d->cinert, 10 * d->nbody},
+    {"cdof", d->cdof, 6 * d->nv}, {"crb", d->crb, 10 * d->nbody}, {"qM", d->qM, d->nM},
+    {"qLD", d->qLD, d->nM}, {"qLDiagInv", d->qLDiagInv, d->nv}, {"cvel", d->cvel, 6 * d->nbody},
+    {"cdof_dot", d->cdof_dot, 6 * d->nv}, {"qfrc_bias", d->qfrc_bias, d->nv},
+    {"qfrc_passive", d->qfrc_passive, d->nv}, {"actuator_force", d->actuator_force, d->nu},
+    {"qfrc_actuator", d->qfrc_actuator, d->nv}, {"qfrc_smooth", d->qfrc_smooth, d->nv},
+    {"qacc_smooth", d->qacc_smooth, d->nv}, {"qfrc_constraint", d->qfrc_constraint, d->nv},
+    {"qacc", d->qacc, d->nv}, {"ncon", d->ncon, 1}, {"con_dist", d->con_dist, d->ncon_max},
+    {"con_pos", d->con_pos, 3 * d->ncon_max}, {"con_frame", d->con_frame, 9 * d->ncon_max},
+    {"con_friction", d->con_friction, 5 * d->ncon_max},
+    {"con_includemargin", d->con_includemargin, d->ncon_max}, {"con_geom", d->con_geom, 2 * d->ncon_max},
+    {"con_dim", d->con_dim, d->ncon_max}, {"con_pair", d->con_pair, d->ncon_max},
+    {"nefc", d->nefc, 1}, {"efc_type", d->efc_type, d->nefc_max}, {"efc_id", d->efc_id, d->nefc_max},
+    {"efc_J", d->efc_J, d->nefc_max * d->nv}, {"efc_pos", d->efc_pos, d->nefc_max},
+    {"efc_margin", d->efc_margin, d->nefc_max}, {"efc_diagApprox", d->efc_diagApprox, d->nefc_max},
+    {"efc_R", d->efc_R, d->nefc_max}, {"efc_D", d->efc_D, d->nefc_max},
+    {"efc_KBIP", d->efc_KBIP, 4 * d->nefc_max}, {"efc_vel", d->efc_vel, d->nefc_max},
+    {"efc_aref", d->efc_aref, d->nefc_max}, {"efc_b", d->efc_b, d->nefc_max},
+    {"efc_force", d->efc_force, d->nefc_max}, {"efc_AR", d->efc_AR, d->nefc_max * d->nefc_max},
+    {"solver_niter", d->solver_niter, 1},
+  };
+  for (size_t i = 0; i < sizeof t / sizeof t[0]; i++)
+    if (!strcmp(t[i].n, name)) { if (count) *count = t[i].c; return t[i].p; }
+  if (count) *count = 0;
+  return NULL;
+}
+
+/* mj_resetData (engine_io.c) [ext]; reached from soccer_env.py:354 */
+void ref_reset(const mgx_model_desc *m, ref_data *d) {
+  memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
+  memset(d->qvel, 0, sizeof(double) * m->nv);
+  memset(d->qacc_warmstart, 0, sizeof(double) * m->nv);
+  memset(d->ctrl, 0, sizeof(double) * (m->nu > 0 ? m->nu : 1));
+  memset(d->qfrc_applied, 0, sizeof(double) * m->nv);
+  memset(d->xfrc_applied, 0, sizeof(double) * 6 * m->nbody);
+  memset(d->qacc, 0, sizeof(double) * m->nv);
+  d->time[0] = 0;
+  d->ncon[0] = 0;
+  d->nefc[0] = 0;
+}
+
+/* ====================================================================== kinematics */
+/* mj_kinematics (engine_core_smooth.c) [ext] */
+static void kinematics(const mgx_model_desc *m, ref_data *d) {
+  d->xpos[0] = d->xpos[1] = d->xpos[2] = 0;
+  d->xquat[0] = 1; d->xquat[1] = d->xquat[2] = d->xquat[3] = 0;
+  quat2mat(d->xmat, d->xquat);
+  for (int i = 1; i < m->nbody; i++) {
+    double xpos[3], xquat[4];
+    int ja = m->body_jntadr[i], jn = m->body_jntnum[i];
+    if (jn == 1 && m->jnt_type[ja] == JFREE) {
+      int a = m->jnt_qposadr[ja];
+      memcpy(xpos, d->qpos + a, 3 * sizeof(double));
+      memcpy(xquat, d->qpos + a + 3, 4 * sizeof(double));
+      normalize4(xquat);
+      memcpy(d->xanchor + 3 * ja, xpos, 3 * sizeof(double));
+      memcpy(d->xaxis + 3 * ja, m->jnt_axis + 3 * ja, 3 * sizeof(double));
+    } else {
+      int p = m->body_parentid[i];
+      mulmatvec3(xpos, d->xmat + 9 * p, m->body_pos + 3 * i);
+      for (int k = 0; k < 3; k++) xpos[k] += d->xpos[3 * p + k];
+      mulquat(xquat, d->xquat + 4 * p, m->body_quat + 4 * i);
+      for (int j = ja; j < ja + jn; j++) {
+        int a = m->jnt_qposadr[j];
+        rotvecquat(d->xaxis + 3 * j, m->jnt_axis + 3 * j, xquat);
+        rotvecquat(d->xanchor + 3 * j, m->jnt_pos + 3 * j, xquat);
+        for (int k = 0; k < 3; k++) d->xanchor[3 * j + k] += xpos[k];
+        if (m->jnt_type[j] == JSLIDE) {
+          double s = d->qpos[a] - m->qpos0[a];
+          for (int k = 0; k < 3; k++) xpos[k] += d->xaxis[3 * j + k] * s;
+        } else if (m->jnt_type[j] == JHINGE || m->jnt_type[j] == JBALL) {
+          double ql[4], v[3];
+          if (m->jnt_type[j] == JBALL) { memcpy(ql, d->qpos + a, 4 * sizeof(double)); normalize4(ql); }
+          else axisangle2quat(ql, m->jnt_axis + 3 * j, d->qpos[a] - m->qpos0[a]);
+          mulquat(xquat, xquat, ql);
+          rotvecquat(v, m->jnt_pos + 3 * j, xquat);
+          for (int k = 0; k < 3; k++) xpos[k] = d->xanchor[3 * j + k] - v[k];
+        }
+      }
+    }
+    normalize4(xquat);
+    memcpy(d->xquat + 4 * i, xquat, 4 * sizeof(double));
+    memcpy(d->xpos + 3 * i, xpos, 3 * sizeof(double));
+    quat2mat(d->xmat + 9 * i, xquat);
+  }
+  /* inertial frames and geom frames: mj_local2Global */
+  for (int i = 0; i < m->nbody; i++) {
+    double q[4];
+    mulmatvec3(d->xipos + 3 * i, d->xmat + 9 * i, m->body_ipos + 3 * i);
+    for (int k = 0; k < 3; k++) d->xipos[3 * i + k] += d->xpos[3 * i + k];
+    mulquat(q, d->xquat + 4 * i, m->body_iquat + 4 * i);
+    quat2mat(d->ximat + 9 * i, q);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    double q[4];
+    mulmatvec3(d->geom_xpos + 3 * g, d->xmat + 9 * b, m->geom_pos + 3 * g);
+    for (int k = 0; k < 3; k++) d->geom_xpos[3 * g + k] += d->xpos[3 * b + k];
+    mulquat(q, d->xquat + 4 * b, m->geom_quat + 4 * g);
+    quat2mat(d->geom_xmat + 9 * g, q);
+  }
+}
+
+/* mju_dofCom */
+static void dofcom(double *res, const double *axis, const double *offset) {
+  if (offset) {
+    res[0] = axis[0]; res[1] = axis[1]; res[2] = axis[2];
+    cross3(res + 3, axis, offset);
+  } else {
+    res[0] = res[1] = res[2] = 0;
+    res[3] = axis[0]; res[4] = axis[1]; res[5] = axis[2];
+  }
+}
+
+/* mju_inertCom: 10-vector (Ixx Iyy Izz Ixy Ixz Iyz, m*d, m) about the subtree com */
+static void inertcom(double *res, const double *inert, const double *mat, const double *dif, double mass) {
+  double tmp[9] = {mat[0] * inert[0], mat[3] * inert[0], mat[6] * inert[0],
+                   mat[1] * inert[1], mat[4] * inert[1], mat[7] * inert[1],
+                   mat[2] * inert[2], mat[5] * inert[2], mat[8] * inert[2]};
+  res[0] = mat[0] * tmp[0] + mat[1] * tmp[3] + mat[2] * tmp[6];
+  res[1] = mat[3] * tmp[1] + mat[4] * tmp[4] + mat[5] * tmp[7];
+  res[2] = mat[6] * tmp[2] + mat[7] * tmp[5] + mat[8] * tmp[8];
+  res[3] = mat[0] * tmp[1] + mat[1] * tmp[4] + mat[2] * tmp[7];
+  res[4] = mat[0] * tmp[2] + mat[1] * tmp[5] + mat[2] * tmp[8];
+  res[5] = mat[3] * tmp[2] + mat[4] * tmp[5] + mat[5] * tmp[8];
+  res[0] += mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+  res[1] += mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+  res[2] += mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+  res[3] -= mass * dif[0] * dif[1];
+  res[4] -= mass * dif[0] * dif[2];
+  res[5] -= mass * dif[1] * dif[2];
+  res[6] = mass * dif[0]; res[7] = mass * dif[1]; res[8] = mass * dif[2];
+  res[9] = mass;
+}
+
+/* mj_comPos [ext] */
+static void compos(const mgx_model_desc *m, ref_data *d) {
+  double *mass_sub = d->scratch;
+  memset(mass_sub, 0, sizeof(double) * m->nbody);
+  memset(d->subtree_com, 0, sizeof(double) * 3 * m->nbody);
+  for (int i = m->nbody - 1; i >= 0; i--) {
+    for (int k = 0; k < 3; k++) d->subtree_com[3 * i + k] += d->xipos[3 * i + k] * m->body_mass[i];
+    mass_sub[i] += m->body_mass[i];
+    if (i) {
+      int p = m->body_parentid[i];
+      for (int k = 0; k < 3; k++) d->subtree_com[3 * p + k] += d->subtree_com[3 * i + k];
+      mass_sub[p] += mass_sub[i];
+    }
+    if (mass_sub[i] < MINVAL) memcpy(d->subtree_com + 3 * i, d->xipos + 3 * i, 3 * sizeof(double));
+    else for (int k = 0; k < 3; k++) d->subtree_com[3 * i + k] /= (mass_sub[i] > MINVAL ? mass_sub[i] : MINVAL);
+  }
+  memset(d->cinert, 0, 10 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double off[3];
+    for (int k = 0; k < 3; k++) off[k] = d->xipos[3 * i + k] - d->subtree_com[3 * m->body_rootid[i] + k];
+    inertcom(d->cinert + 10 * i, m->body_inertia + 3 * i, d->ximat + 9 * i, off, m->body_mass[i]);
+  }
+  for (int j = 0; j < m->nv; j++) {
+    int b = m->dof_bodyid[j], jid = m->dof_jntid[j];
+    double off[3];
+    for (int k = 0; k < 3; k++) off[k] = d->subtree_com[3 * m->body_rootid[b] + k] - d->xanchor[3 * jid + k];
+    int t = m->jnt_type[jid];
+    if (t == JFREE) {
+      memset(d->cdof + 6 * j, 0, 18 * sizeof(double));
+      for (int k = 0; k < 3; k++) d->cdof[6 * (j + k) + 3 + k] = 1;
+      for (int k = 0; k < 3; k++) {
+        double ax[3] = {d->xmat[9 * b + k], d->xmat[9 * b + k + 3], d->xmat[9 * b + k + 6]};
+        dofcom(d->cdof + 6 * (j + 3 + k), ax, off);
+      }
+      j += 5;
+    } else if (t == JBALL) {
+      for (int k = 0; k < 3; k++) {
+        double ax[3] = {d->xmat[9 * b + k], d->xmat[9 * b + k + 3], d->xmat[9 * b + k + 6]};
+        dofcom(d->cdof + 6 * (j + k), ax, off);
+      }
+      j += 2;
+    } else if (t == JSLIDE) {
+      dofcom(d->cdof + 6 * j, d->xaxis + 3 * jid, NULL);
+    } else {
+      dofcom(d->cdof + 6 * j, d->xaxis + 3 * jid, off);
+    }
+  }
+}
+
+/* mju_mulInertVec: 6D spatial inertia times motion vector */
+static void mulinertvec(double *res, const double *i, const double *v) {
+  res[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  res[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  res[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  res[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  res[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  res[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+static double dot6(const double *a, const double *b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+/* mj_crb + dense-forward qM assembly [ext] */
+static void crb(const mgx_model_desc *m, ref_data *d) {
+  memcpy(d->crb, d->cinert, sizeof(double) * 10 * m->nbody);
+  for (int i = m->nbody - 1; i > 0; i--) {
+    int p = m->body_parentid[i];
+    if (p > 0) for (int k = 0; k < 10; k++) d->crb[10 * p + k] += d->crb[10 * i + k];
+  }
+  memset(d->qM, 0, sizeof(double) * m->nM);
+  for (int i = 0; i < m->nv; i++) {
+    double buf[6];
+    int adr = m->dof_Madr[i];
+    d->qM[adr] = m->dof_armature[i];
+    mulinertvec(buf, d->crb + 10 * m->dof_bodyid[i], d->cdof + 6 * i);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) d->qM[adr++] += dot6(d->cdof + 6 * j, buf);
+  }
+}
+
+/* mj_factorI: M = L' D L, tree-sparse, in place (qLD) [ext] */
+static void factor_ld(const mgx_model_desc *m, const double *M, double *LD, double *diaginv) {
+  if (LD != M) memcpy(LD, M, sizeof(double) * m->nM);
+  for (int k = m->nv - 1; k >= 0; k--) {
+    int akk = m->dof_Madr[k];
+    if (LD[akk] < MINVAL) LD[akk] = MINVAL;
+    int aki = akk + 1;
+    int i = m->dof_parentid[k];
+    while (i >= 0) {
+      double tmp = LD[aki] / LD[akk];
+      int cnt = 0;
+      for (int j = i; j >= 0; j = m->dof_parentid[j]) cnt++;
+      int ai = m->dof_Madr[i];
+      for (int s = 0; s < cnt; s++) LD[ai + s] -= LD[aki + s] * tmp;
+      LD[aki] = tmp;
+      i = m->dof_parentid[i];
+      aki++;
+    }
+  }
+  for (int i = 0; i < m->nv; i++) diaginv[i] = 1 / LD[m->dof_Madr[i]];
+}
+
+/* mj_solveLD: x = M^-1 x using the L'DL factor */
+static void solve_ld(const mgx_model_desc *m, const double *LD, const double *diaginv, double *x) {
+  for (int k = m->nv - 1; k >= 0; k--) { /* x <- L'^-1 x */
+    double xk = x[k];
+    if (xk == 0) continue;
+    int a = m->dof_Madr[k] + 1;
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) x[i] -= LD[a++] * xk;
+  }
+  for (int k = 0; k < m->nv; k++) x[k] *= diaginv[k];
+  for (int k = 0; k < m->nv; k++) { /* x <- L^-1 x */
+    int a = m->dof_Madr[k] + 1;
+    double s = 0;
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) s += LD[a++] * x[i];
+    x[k] -= s;
+  }
+}
+
+/* ====================================================================== jacobians */
+static int body_has_dof(const mgx_model_desc *m, int body, int dof) {
+  return (m->body_dofmask[body * m->nmaskword + (dof >> 5)] >> (dof & 31)) & 1u;
+}
+/* mj_jac: translational (jacp, 3 x nv) and rotational (jacr) Jacobians of a point on body */
+static void jac(const mgx_model_desc *m, ref_data *d, double *jacp, double *jacr, const double *pt, int body) {
+  int nv = m->nv;
+  double off[3];
+  for (int k = 0; k < 3; k++) off[k] = pt[k] - d->subtree_com[3 * m->body_rootid[body] + k];
+  if (jacp) memset(jacp, 0, 3 * nv * sizeof(double));
+  if (jacr) memset(jacr, 0, 3 * nv * sizeof(double));
+  if (body == 0) return;
+  for (int j = 0; j < nv; j++) {
+    if (!body_has_dof(m, body, j)) continue;
+    const double *c = d->cdof + 6 * j;
+    if (jacr) { jacr[j] = c[0]; jacr[j + nv] = c[1]; jacr[j + 2 * nv] = c[2]; }
+    if (jacp) {
+      double t[3];
+      cross3(t, c, off);
+      jacp[j] = c[3] + t[0]; jacp[j + nv] = c[4] + t[1]; jacp[j + 2 * nv] = c[5] + t[2];
+    }
+  }
+}
+
+/* ====================================================================== collision */
+/* mju_makeFrame: normal -> (normal, tangent1, tangent2) */
+static void make_frame(double *f) {
+  double tmp[3];
+  normalize3(f);
+  f[3] = f[4] = f[5] = 0;
+  if (f[1] < 0.5 && f[1] > -0.5) f[4] = 1; else f[5] = 1;
+  double s = dot3(f, f + 3);
+  for (int k = 0; k < 3; k++) tmp[k] = f[k] * s;
+  for (int k = 0; k < 3; k++) f[3 + k] -= tmp[k];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+typedef struct { double dist, pos[3], n[3]; } rcon;
+
+/* sphere-sphere core: normal from 1 to 2, pos = midpoint of the surfaces */
+static int sph_sph(const double *c1, double r1, const double *c2, double r2, double margin, rcon *out) {
+  double dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  double L = normalize3(dv);
+  double dist = L - r1 - r2;
+  if (dist > margin) return 0;
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = dv[k]; out->pos[k] = c1[k] + dv[k] * (r1 + 0.5 * dist); }
+  return 1;
+}
+
+static void seg_ends(const double *pos, const double *mat, double hl, double *a, double *b) {
+  for (int k = 0; k < 3; k++) { a[k] = pos[k] - hl * mat[3 * k + 2]; b[k] = pos[k] + hl * mat[3 * k + 2]; }
+}
+
+/* closest points between segments p1q1 and p2q2 (parameters s, t in [0,1]) */
+static void seg_seg(const double *p1, const double *q1, const double *p2, const double *q2, double *s, double *t) {
+  double d1[3], d2[3], r[3];
+  for (int k = 0; k < 3; k++) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+  double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  if (a <= MINVAL && e <= MINVAL) { *s = *t = 0; return; }
+  if (a <= MINVAL) { *s = 0; *t = clampd(f / e, 0, 1); return; }
+  double c = dot3(d1, r);
+  if (e <= MINVAL) { *t = 0; *s = clampd(-c / a, 0, 1); return; }
+  double b = dot3(d1, d2), den = a * e - b * b;
+  double ss = den > 1e-12 * a * e ? clampd((b * f - c * e) / den, 0, 1) : 0;
+  double tt = (b * ss + f) / e;
+  if (tt < 0) { tt = 0; ss = clampd(-c / a, 0, 1); }
+  else if (tt > 1) { tt = 1; ss = clampd((b - c) / a, 0, 1); }
+  *s = ss; *t = tt;
+}
+
+/* signed distance of a box-local point to the box; e = outward unit normal at the closest
+ * surface feature (box frame). Inside: nearest face, ties -> lowest axis. */
+static double box_sd(const double *p, const double *h, double *e) {
+  int outside = 0;
+  double q[3], dv[3];
+  for (int k = 0; k < 3; k++) {
+    q[k] = clampd(p[k], -h[k], h[k]);
+    dv[k] = p[k] - q[k];
+    if (dv[k] != 0) outside = 1;
+  }
+  if (outside) {
+    double L = normalize3(dv);
+    e[0] = dv[0]; e[1] = dv[1]; e[2] = dv[2];
+    return L;
+  }
+  int best = 0;
+  double bd = h[0] - fabs(p[0]);
+  for (int k = 1; k < 3; k++) {
+    double dk = h[k] - fabs(p[k]);
+    if (dk < bd) { bd = dk; best = k; }
+  }
+  e[0] = e[1] = e[2] = 0;
+  e[best] = p[best] >= 0 ? 1 : -1;
+  return -bd;
+}
+
+/* sphere (center c world, radius r) vs box geom; normal from sphere to box */
+static int sphere_box_core(const double *c, double r, const double *bp, const double *bm, const double *h,
+                           double margin, rcon *out) {
+  double tmp[3] = {c[0] - bp[0], c[1] - bp[1], c[2] - bp[2]}, pl[3], e[3], ew[3];
+  mulmatTvec3(pl, bm, tmp);
+  double sd = box_sd(pl, h, e);
+  double dist = sd - r;
+  if (dist > margin) return 0;
+  mulmatvec3(ew, bm, e);
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = -ew[k]; out->pos[k] = c[k] - ew[k] * (r + 0.5 * dist); }
+  return 1;
+}
+
+/* capsule (geom1) vs box (geom2): endpoint spheres + the deepest interior point when it is
+ * deeper than both ends (golden-section over the convex signed-distance profile). */
+static int capsule_box(const double *cp, const double *cm, const double *cs, const double *bp, const double *bm,
+                       const double *h, double margin, rcon *out) {
+  double a[3], b[3], al[3], bl[3], tmp[3], e[3];
+  double r = cs[0];
+  seg_ends(cp, cm, cs[1], a, b);
+  for (int k = 0; k < 3; k++) tmp[k] = a[k] - bp[k];
+  mulmatTvec3(al, bm, tmp);
+  for (int k = 0; k < 3; k++) tmp[k] = b[k] - bp[k];
+  mulmatTvec3(bl, bm, tmp);
+  double lo = 0, hi = 1;
+  const double gr = 0.6180339887498949;
+  double x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), f1, f2, p[3];
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+  f1 = box_sd(p, h, e);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+  f2 = box_sd(p, h, e);
+  for (int it = 0; it < 40; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+      f1 = box_sd(p, h, e);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+      f2 = box_sd(p, h, e);
+    }
+  }
+  double ts = 0.5 * (lo + hi);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + ts * (bl[k] - al[k]);
+  double fs = box_sd(p, h, e);
+  double f0 = box_sd(al, h, e), f1e = box_sd(bl, h, e);
+  int n = 0;
+  double cw[3];
+  if (f0 - r <= margin) n += sphere_box_core(a, r, bp, bm, h, margin, out + n);
+  if (f1e - r <= margin) n += sphere_box_core(b, r, bp, bm, h, margin, out + n);
+  if (ts > 0.02 && ts < 0.98 && fs - r <= margin && fs < (f0 < f1e ? f0 : f1e) - 0.01 * r) {
+    for (int k = 0; k < 3; k++) cw[k] = a[k] + ts * (b[k] - a[k]);
+    n += sphere_box_core(cw, r, bp, bm, h, margin, out + n);
+  }
+  return n;
+}
+
+/* box (geom1) vs box (geom2): separating-axis test over 15 axes, then face clipping
+ * (reference face vs incident face, up to 8 points) or one edge-edge contact. */
+static int clip_poly(double (*in)[2], int n, int axis, double lim, double sgn, double (*out)[2]) {
+  int m = 0;
+  for (int i = 0; i < n; i++) {
+    double *P = in[i], *Q = in[(i + 1) % n];
+    double dp = sgn * P[axis] - lim, dq = sgn * Q[axis] - lim;
+    if (dp <= 0) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
+    if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+      double t = dp / (dp - dq);
+      out[m][0] = P[0] + t * (Q[0] - P[0]);
+      out[m][1] = P[1] + t * (Q[1] - P[1]);
+      m++;
+    }
+  }
+  return m;
+}
+
+static int box_box(const double *pa, const double *Ra, const double *ha, const double *pb, const double *Rb,
+                   const double *hb, double margin, rcon *out) {
+  double d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+  double A[3][3], B[3][3]; /* A[i] = i-th axis of box a (column i of Ra) */
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { A[i][k] = Ra[3 * k + i]; B[i][k] = Rb[3 * k + i]; }
+  double best_face = -1e30, best_edge = -1e30;
+  int face_axis = -1, edge_i = -1, edge_j = -1;
+  double edge_n[3] = {0, 0, 0};
+  for (int ax = 0; ax < 6; ax++) {
+    const double *n = ax < 3 ? A[ax] : B[ax - 3];
+    double ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(A[k], n)); rb += hb[k] * fabs(dot3(B[k], n)); }
+    double s = fabs(dot3(d, n)) - ra - rb;
+    if (s > margin) return 0;
+    if (s > best_face) { best_face = s; face_axis = ax; }
+  }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      double n[3];
+      cross3(n, A[i], B[j]);
+      double L = norm3(n);
+      if (L < 1e-6) continue;
+      for (int k = 0; k < 3; k++) n[k] /= L;
+      double ra = 0, rb = 0;
+      for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(A[k], n)); rb += hb[k] * fabs(dot3(B[k], n)); }
+      double s = fabs(dot3(d, n)) - ra - rb;
+      if (s > margin) return 0;
+      if (s > best_edge) { best_edge = s; edge_i = i; edge_j = j; memcpy(edge_n, n, sizeof edge_n); }
+    }
+  if (edge_i >= 0 && best_edge > best_face + 1e-5 + 0.05 * fabs(best_face)) {
+    double n[3] = {edge_n[0], edge_n[1], edge_n[2]};
+    if (dot3(n, d) < 0) for (int k = 0; k < 3; k++) n[k] = -n[k];
+    double ca[3], cb[3];
+    memcpy(ca, pa, sizeof ca);
+    memcpy(cb, pb, sizeof cb);
+    for (int k = 0; k < 3; k++) {
+      if (k != edge_i) { double sg = dot3(A[k], n) >= 0 ? 1 : -1; for (int c = 0; c < 3; c++) ca[c] += sg * ha[k] * A[k][c]; }
+      if (k != edge_j) { double sg = dot3(B[k], n) <= 0 ? 1 : -1; for (int c = 0; c < 3; c++) cb[c] += sg * hb[k] * B[k][c]; }
+    }
+    double a0[3], a1[3], b0[3], b1[3], s, t, P[3], Q[3];
+    for (int c = 0; c < 3; c++) {
+      a0[c] = ca[c] - ha[edge_i] * A[edge_i][c]; a1[c] = ca[c] + ha[edge_i] * A[edge_i][c];
+      b0[c] = cb[c] - hb[edge_j] * B[edge_j][c]; b1[c] = cb[c] + hb[edge_j] * B[edge_j][c];
+    }
+    seg_seg(a0, a1, b0, b1, &s, &t);
+    for (int c = 0; c < 3; c++) { P[c] = a0[c] + s * (a1[c] - a0[c]); Q[c] = b0[c] + t * (b1[c] - b0[c]); }
+    double dq[3] = {Q[0] - P[0], Q[1] - P[1], Q[2] - P[2]};
+    out[0].dist = dot3(dq, n);
+    if (out[0].dist > margin) return 0;
+    for (int c = 0; c < 3; c++) { out[0].n[c] = n[c]; out[0].pos[c] = 0.5 * (P[c] + Q[c]); }
+    return 1;
+  }
+  /* face contact: reference box R, incident box I */
+  int refA = face_axis < 3;
+  int ri = refA ? face_axis : face_axis - 3;
+  const double *pr = refA ? pa : pb, *pi = refA ? pb : pa;
+  const double *hr = refA ? ha : hb, *hi = refA ? hb : ha;
+  double (*R)[3] = refA ? A : B, (*I)[3] = refA ? B : A;
+  double toI[3] = {pi[0] - pr[0], pi[1] - pr[1], pi[2] - pr[2]};
+  double nr[3];
+  double sg = dot3(toI, R[ri]) >= 0 ? 1 : -1;
+  for (int k = 0; k < 3; k++) nr[k] = sg * R[ri][k];
+  /* incident face: most anti-parallel to nr */
+  int ii = 0;
+  double bestd = -1;
+  for (int k = 0; k < 3; k++) { double v = fabs(dot3(I[k], nr)); if (v > bestd) { bestd = v; ii = k; } }
+  double si = dot3(I[ii], nr) > 0 ? -1 : 1;
+  double fc[3];
+  for (int k = 0; k < 3; k++) fc[k] = pi[k] + si * hi[ii] * I[ii][k];
+  int u = (ii + 1) % 3, v = (ii + 2) % 3;
+  int ru = (ri + 1) % 3, rv = (ri + 2) % 3;
+  double poly[8][2], tmp[8][2];
+  const double sgn4[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
+  for (int c = 0; c < 4; c++) {
+    double P[3], rel[3];
+    for (int k = 0; k < 3; k++)
+      P[k] = fc[k] + sgn4[c][0] * hi[u] * I[u][k] + sgn4[c][1] * hi[v] * I[v][k];
+    for (int k = 0; k < 3; k++) rel[k] = P[k] - pr[k];
+    poly[c][0] = dot3(rel, R[ru]);
+    poly[c][1] = dot3(rel, R[rv]);
+  }
+  int np = 4;
+  np = clip_poly(poly, np, 0, hr[ru], 1, tmp);
+  np = clip_poly(tmp, np, 0, hr[ru], -1, poly);
+  np = clip_poly(poly, np, 1, hr[rv], 1, tmp);
+  np = clip_poly(tmp, np, 1, hr[rv], -1, poly);
+  /* depth of each clipped point: intersect the incident face plane along nr */
+  double fn[3];
+  for (int k = 0; k < 3; k++) fn[k] = si * I[ii][k];
+  double fndn = dot3(fn, nr);
+  int n = 0;
+  for (int c = 0; c < np && n < MAXCONPAIR; c++) {
+    double P[3];
+    for (int k = 0; k < 3; k++) P[k] = pr[k] + poly[c][0] * R[ru][k] + poly[c][1] * R[rv][k] + hr[ri] * nr[k];
+    /* move P along nr onto the incident face plane: (P + t nr - fc).fn = 0 */
+    double rel[3] = {P[0] - fc[0], P[1] - fc[1], P[2] - fc[2]};
+    double t = fabs(fndn) > MINVAL ? -dot3(rel, fn) / fndn : 0;
+    double depth = t; /* signed distance from reference face to incident point along nr */
+    if (depth > margin) continue;
+    out[n].dist = depth;
+    for (int k = 0; k < 3; k++) {
+      out[n].n[k] = refA ? nr[k] : -nr[k];
+      out[n].pos[k] = P[k] + 0.5 * t * nr[k];
+    }
+    n++;
+  }
+  return n;
+}
+
+/* plane (geom1, infinite, normal = local z) vs primitives */
+static int plane_sphere(const double *pp, const double *pm, const double *c, double r, double margin, rcon *out) {
+  double n[3] = {pm[2], pm[5], pm[8]};
+  double rel[3] = {c[0] - pp[0], c[1] - pp[1], c[2] - pp[2]};
+  double dist = dot3(rel, n) - r;
+  if (dist > margin) return 0;
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = n[k]; out->pos[k] = c[k] - n[k] * (r + 0.5 * dist); }
+  return 1;
+}
+
+static int plane_box(const double *pp, const double *pm, const double *bp, const double *bm, const double *h,
+                     double margin, rcon *out) {
+  double n[3] = {pm[2], pm[5], pm[8]};
+  int cnt = 0;
+  for (int c = 0; c < 8 && cnt < 4; c++) {
+    double v[3], loc[3] = {(c & 1) ? h[0] : -h[0], (c & 2) ? h[1] : -h[1], (c & 4) ? h[2] : -h[2]};
+    mulmatvec3(v, bm, loc);
+    for (int k = 0; k < 3; k++) v[k] += bp[k];
+    double rel[3] = {v[0] - pp[0], v[1] - pp[1], v[2] - pp[2]};
+    double dist = dot3(rel, n);
+    if (dist > margin) continue;
+    out[cnt].dist = dist;
+    for (int k = 0; k < 3; k++) { out[cnt].n[k] = n[k]; out[cnt].pos[k] = v[k] - 0.5 * dist * n[k]; }
+    cnt++;
+  }
+  return cnt;
+}
+
+/* dispatch one candidate pair (geom types ordered type1 <= type2) */
+static int collide_geoms(const mgx_model_desc *m, ref_data *d, int g1, int g2, double margin, rcon *out) {
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const double *p1 = d->geom_xpos + 3 * g1, *m1 = d->geom_xmat + 9 * g1, *s1 = m->geom_size + 3 * g1;
+  const double *p2 = d->geom_xpos + 3 * g2, *m2 = d->geom_xmat + 9 * g2, *s2 = m->geom_size + 3 * g2;
+  /* bounding-sphere cull (mid-phase; no effect on results) */
+  if (t1 != GPLANE) {
+    double dv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    if (norm3(dv) > m->geom_rbound[g1] + m->geom_rbound[g2] + margin) return 0;
+  }
+  if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph(p1, s1[0], p2, s2[0], margin, out);
+  if (t1 == GSPHERE && t2 == GCAPSULE) {
+    double a[3], b[3], q[3];
+    seg_ends(p2, m2, s2[1], a, b);
+    double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p1[0] - a[0], p1[1] - a[1], p1[2] - a[2]};
+    double L2 = dot3(ab, ab), t = L2 > MINVAL ? clampd(dot3(ap, ab) / L2, 0, 1) : 0;
+    for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k];
+    return sph_sph(p1, s1[0], q, s2[0], margin, out);
+  }
+  if (t1 == GCAPSULE && t2 == GCAPSULE) {
+    double a1[3], b1[3], a2[3], b2[3], s, t, P[3], Q[3];
+    seg_ends(p1, m1, s1[1], a1, b1);
+    seg_ends(p2, m2, s2[1], a2, b2);
+    seg_seg(a1, b1, a2, b2, &s, &t);
+    for (int k = 0; k < 3; k++) { P[k] = a1[k] + s * (b1[k] - a1[k]); Q[k] = a2[k] + t * (b2[k] - a2[k]); }
+    return sph_sph(P, s1[0], Q, s2[0], margin, out);
+  }
+  if (t1 == GSPHERE && t2 == GBOX) return sphere_box_core(p1, s1[0], p2, m2, s2, margin, out);
+  if (t1 == GCAPSULE && t2 == GBOX) return capsule_box(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GBOX && t2 == GBOX) return box_box(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GPLANE && t2 == GSPHERE) return plane_sphere(p1, m1, p2, s2[0], margin, out);
+  if (t1 == GPLANE && t2 == GCAPSULE) {
+    double a[3], b[3];
+    seg_ends(p2, m2, s2[1], a, b);
+    int n = plane_sphere(p1, m1, a, s2[0], margin, out);
+    n += plane_sphere(p1, m1, b, s2[0], margin, out + n);
+    return n;
+  }
+  if (t1 == GPLANE && t2 == GBOX) return plane_box(p1, m1, p2, m2, s2, margin, out);
+  return 0; /* unsupported pair types (cylinder, ellipsoid): not used by the headline task */
+}
+
+static int add_contacts(const mgx_model_desc *m, ref_data *d, int pi, rcon *rc, int n) {
+  int g1 = m->pair_geom[2 * pi], g2 = m->pair_geom[2 * pi + 1];
+  for (int c = 0; c < n; c++) {
+    int k = d->ncon[0];
+    if (k >= d->ncon_max) return 0;
+    d->con_dist[k] = rc[c].dist;
+    memcpy(d->con_pos + 3 * k, rc[c].pos, 3 * sizeof(double));
+    double *f = d->con_frame + 9 * k;
+    f[0] = rc[c].n[0]; f[1] = rc[c].n[1]; f[2] = rc[c].n[2];
+    make_frame(f);
+    memcpy(d->con_friction + 5 * k, m->pair_friction + 5 * pi, 5 * sizeof(double));
+    d->con_includemargin[k] = m->pair_margin[pi] - m->pair_gap[pi];
+    memcpy(d->con_solref + 2 * k, m->pair_solref + 2 * pi, 2 * sizeof(double));
+    memcpy(d->con_solimp + 5 * k, m->pair_solimp + 5 * pi, 5 * sizeof(double));
+    d->con_geom[2 * k] = g1; d->con_geom[2 * k + 1] = g2;
+    d->con_dim[k] = m->pair_condim[pi];
+    d->con_pair[k] = pi;
+    d->ncon[0]++;
+  }
+  return n;
+}
+
+int ref_collide_pair(const mgx_model_desc *m, ref_data *d, int pi) {
+  rcon rc[MAXCONPAIR];
+  int n = collide_geoms(m, d, m->pair_geom[2 * pi], m->pair_geom[2 * pi + 1], m->pair_margin[pi], rc);
+  return add_contacts(m, d, pi, rc, n);
+}
+
+/* mj_collision [ext]: candidate pairs already in MuJoCo order (explicit, then sorted body pairs) */
+static void collision(const mgx_model_desc *m, ref_data *d) {
+  d->ncon[0] = 0;
+  for (int pi = 0; pi < m->npair; pi++) ref_collide_pair(m, d, pi);
+}
+
+/* ====================================================================== constraints */
+static void getimpedance(const double *solimp, double pos, double margin, double *imp) {
+  double d0 = clampd(solimp[0], MINIMP, MAXIMP), d1 = clampd(solimp[1], MINIMP, MAXIMP);
+  double width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (d0 == d1 || width <= MINVAL) { *imp = 0.5 * (d0 + d1); return; }
+  double x = (pos - margin) / width;
+  if (x < 0) x = -x;
+  if (x >= 1 || x <= 0) { *imp = x >= 1 ? d1 : d0; return; }
+  double y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = pow(x, power) / pow(mid, power - 1);
+  else y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+  *imp = d0 + y * (d1 - d0);
+}
+
+static int add_row(ref_data *d, int type, int id, double pos, double margin, double diag) {
+  int r = d->nefc[0];
+  if (r >= d->nefc_max) return -1;
+  d->efc_type[r] = type; d->efc_id[r] = id; d->efc_pos[r] = pos; d->efc_margin[r] = margin;
+  d->efc_diagApprox[r] = diag;
+  memset(d->efc_J + (size_t)r * d->nv, 0, sizeof(double) * d->nv);
+  d->nefc[0]++;
+  return r;
+}
+
+/* mj_makeConstraint: joint limits (mj_instantiateLimit) then contacts
+ * (mj_instantiateContact, pyramidal cone) [ext] */
+static void make_constraint(const mgx_model_desc *m, ref_data *d) {
+  int nv = m->nv;
+  d->nefc[0] = 0;
+  for (int j = 0; j < m->njnt; j++) {
+    if (!m->jnt_limited[j]) continue;
+    int t = m->jnt_type[j];
+    if (t != JHINGE && t != JSLIDE) continue;
+    double val = d->qpos[m->jnt_qposadr[j]], margin = m->jnt_margin[j];
+    for (int side = -1; side <= 1; side += 2) {
+      double dist = side * (m->jnt_range[2 * j + (side + 1) / 2] - val);
+      if (dist < margin) {
+        int r = add_row(d, C_LIMIT_JOINT, j, dist, margin, m->dof_invweight0[m->jnt_dofadr[j]]);
+        if (r < 0) return;
+        d->efc_J[(size_t)r * nv + m->jnt_dofadr[j]] = -side;
+      }
+    }
+  }
+  double *jp1 = d->scratch, *jp2 = jp1 + 3 * nv, *jd = jp2 + 3 * nv;
+  for (int c = 0; c < d->ncon[0]; c++) {
+    int g1 = d->con_geom[2 * c], g2 = d->con_geom[2 * c + 1];
+    int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+    int dim = d->con_dim[c];
+    const double *fr = d->con_frame + 9 * c, *mu = d->con_friction + 5 * c;
+    jac(m, d, jp1, NULL, d->con_pos + 3 * c, b1);
+    jac(m, d, jp2, NULL, d->con_pos + 3 * c, b2);
+    for (int k = 0; k < 3 * nv; k++) jd[k] = jp2[k] - jp1[k];
+    double tran = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
+    /* contact-frame rows: cj[0] normal, cj[1..2] tangents */
+    double *cj = jd + 3 * nv;
+    for (int a = 0; a < 3; a++)
+      for (int k = 0; k < nv; k++)
+        cj[a * nv + k] = fr[3 * a] * jd[k] + fr[3 * a + 1] * jd[nv + k] + fr[3 * a + 2] * jd[2 * nv + k];
+    if (dim == 1) {
+      int r = add_row(d, C_CONTACT_FRICTIONLESS, c, d->con_dist[c], d->con_includemargin[c], tran);
+      if (r < 0) return;
+      memcpy(d->efc_J + (size_t)r * nv, cj, sizeof(double) * nv);
+    } else {
+      for (int k = 1; k < 3; k++)
+        for (int sgn = 0; sgn < 2; sgn++) {
+          double f = mu[k - 1];
+          int r = add_row(d, C_CONTACT_PYRAMIDAL, c, d->con_dist[c], d->con_includemargin[c],
+                          tran + f * f * tran);
+          if (r < 0) return;
+          double s = sgn ? -f : f;
+          for (int q = 0; q < nv; q++) d->efc_J[(size_t)r * nv + q] = cj[q] + s * cj[k * nv + q];
+        }
+    }
+  }
+}
+
+/* mj_makeImpedance: K, B, imp, R, D per row [ext] */
+static void make_impedance(const mgx_model_desc *m, ref_data *d) {
+  for (int r = 0; r < d->nefc[0]; r++) {
+    const double *solref, *solimp;
+    if (d->efc_type[r] == C_LIMIT_JOINT) {
+      solref = m->jnt_solref + 2 * d->efc_id[r];
+      solimp = m->jnt_solimp + 5 * d->efc_id[r];
+    } else {
+      solref = d->con_solref + 2 * d->efc_id[r];
+      solimp = d->con_solimp + 5 * d->efc_id[r];
+    }
+    double imp;
+    getimpedance(solimp, d->efc_pos[r], d->efc_margin[r], &imp);
+    double dmax = clampd(solimp[1], MINIMP, MAXIMP), K, B;
+    if (solref[0] > 0) {
+      double tc = solref[0], dr = solref[1];
+      if (tc < 2 * m->timestep) tc = 2 * m->timestep; /* refsafe */
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -solref[0] / (dmax * dmax);
+      B = -solref[1] / dmax;
+    }
+    d->efc_KBIP[4 * r] = K; d->efc_KBIP[4 * r + 1] = B; d->efc_KBIP[4 * r + 2] = imp; d->efc_KBIP[4 * r + 3] = 0;
+    double R = (1 - imp) * d->efc_diagApprox[r] / imp;
+    d->efc_R[r] = R > MINVAL ? R : MINVAL;
+    d->efc_D[r] = 1 / d->efc_R[r];
+  }
+}
+
+/* mj_projectConstraint: AR = J M^-1 J' + diag(R) (dense) [ext] */
+static void project_constraint(const mgx_model_desc *m, ref_data *d) {
+  int nv = m->nv, ne = d->nefc[0];
+  double *MinvJT = d->scratch; /* [ne][nv] */
+  for (int r = 0; r < ne; r++) {
+    memcpy(MinvJT + (size_t)r * nv, d->efc_J + (size_t)r * nv, sizeof(double) * nv);
+    solve_ld(m, d->qLD, d->qLDiagInv, MinvJT + (size_t)r * nv);
+  }
+  for (int r = 0; r < ne; r++)
+    for (int c = 0; c < ne; c++) {
+      double s = 0;
+      for (int k = 0; k < nv; k++) s += d->efc_J[(size_t)r * nv + k] * MinvJT[(size_t)c * nv + k];
+      d->efc_AR[(size_t)r * ne + c] = s + (r == c ? d->efc_R[r] : 0);
+    }
+}
+
+/* ====================================================================== velocity stage */
+static void crossmotion(double *res, const double *v, const double *u) {
+  res[0] = -v[2] * u[1] + v[1] * u[2];
+  res[1] = v[2] * u[0] - v[0] * u[2];
+  res[2] = -v[1] * u[0] + v[0] * u[1];
+  res[3] = -v[2] * u[4] + v[1] * u[5];
+  res[4] = v[2] * u[3] - v[0] * u[5];
+  res[5] = -v[1] * u[3] + v[0] * u[4];
+  res[3] += -v[5] * u[1] + v[4] * u[2];
+  res[4] += v[5] * u[0] - v[3] * u[2];
+  res[5] += -v[4] * u[0] + v[3] * u[1];
+}
+static void crossforce(double *res, const double *v, const double *f) {
+  res[0] = -v[2] * f[1] + v[1] * f[2];
+  res[1] = v[2] * f[0] - v[0] * f[2];
+  res[2] = -v[1] * f[0] + v[0] * f[1];
+  res[3] = -v[2] * f[4] + v[1] * f[5];
+  res[4] = v[2] * f[3] - v[0] * f[5];
+  res[5] = -v[1] * f[3] + v[0] * f[4];
+  res[0] += -v[5] * f[4] + v[4] * f[5];
+  res[1] += v[5] * f[3] - v[3] * f[5];
+  res[2] += -v[4] * f[3] + v[3] * f[4];
+}
+
+/* mj_comVel [ext] */
+static void comvel(const mgx_model_desc *m, ref_data *d) {
+  memset(d->cvel, 0, 6 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double cvel[6];
+    memcpy(cvel, d->cvel + 6 * m->body_parentid[i], sizeof cvel);
+    int bda = m->body_dofadr[i], nd = m->body_dofnum[i];
+    for (int j = 0; j < nd; j++) {
+      int dof = bda + j, t = m->jnt_type[m->dof_jntid[dof]];
+      if (t == JFREE) {
+        for (int k = 0; k < 18; k++) d->cdof_dot[6 * dof + k] = 0;
+        for (int q = 0; q < 3; q++)
+          for (int k = 0; k < 6; k++) cvel[k] += d->cdof[6 * (dof + q) + k] * d->qvel[dof + q];
+        for (int q = 3; q < 6; q++) crossmotion(d->cdof_dot + 6 * (dof + q), cvel, d->cdof + 6 * (dof + q));
+        for (int q = 3; q < 6; q++)
+          for (int k = 0; k < 6; k++) cvel[k] += d->cdof[6 * (dof + q) + k] * d->qvel[dof + q];
+        j += 5;
+      } else if (t == JBALL) {
+        for (int q = 0; q < 3; q++) crossmotion(d->cdof_dot + 6 * (dof + q), cvel, d->cdof + 6 * (dof + q));
+        for (int q = 0; q < 3; q++)
+          for (int k = 0; k < 6; k++) cvel[k] += d->cdof[6 * (dof + q) + k] * d->qvel[dof + q];
+        j += 2;
+      } else {
+        crossmotion(d->cdof_dot + 6 * dof, cvel, d->cdof + 6 * dof);
+        for (int k = 0; k < 6; k++) cvel[k] += d->cdof[6 * dof + k] * d->qvel[dof];
+      }
+    }
+    memcpy(d->cvel + 6 * i, cvel, sizeof cvel);
+  }
+}
+
+/* mj_passive: joint springs (hinge/slide) and dof damping [ext] */
+static void passive(const mgx_model_desc *m, ref_data *d) {
+  for (int k = 0; k < m->nv; k++) d->qfrc_passive[k] = -m->dof_damping[k] * d->qvel[k];
+  for (int j = 0; j < m->njnt; j++) {
+    double st = m->jnt_stiffness[j];
+    if (st == 0) continue;
+    int t = m->jnt_type[j], a = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    if (t == JHINGE || t == JSLIDE) d->qfrc_passive[da] -= st * (d->qpos[a] - m->qpos_spring[a]);
+    else if (t == JFREE) for (int k = 0; k < 3; k++) d->qfrc_passive[da + k] -= st * (d->qpos[a + k] - m->qpos_spring[a + k]);
+  }
+}
+
+/* mj_rne with flg_acc = 0: qfrc_bias = C(q, v) + gravity [ext] */
+static void rne(const mgx_model_desc *m, ref_data *d) {
+  int nb = m->nbody;
+  double *cacc = d->scratch, *cfrc = cacc + 6 * nb, tmp[6], tmp1[6];
+  memset(cacc, 0, 6 * sizeof(double));
+  for (int k = 0; k < 3; k++) cacc[3 + k] = -m->gravity[k];
+  for (int i = 1; i < nb; i++) {
+    int bda = m->body_dofadr[i], nd = m->body_dofnum[i], p = m->body_parentid[i];
+    for (int k = 0; k < 6; k++) cacc[6 * i + k] = cacc[6 * p + k];
+    for (int j = 0; j < nd; j++)
+      for (int k = 0; k < 6; k++) cacc[6 * i + k] += d->cdof_dot[6 * (bda + j) + k] * d->qvel[bda + j];
+    mulinertvec(cfrc + 6 * i, d->cinert + 10 * i, cacc + 6 * i);
+    mulinertvec(tmp, d->cinert + 10 * i, d->cvel + 6 * i);
+    crossforce(tmp1, d->cvel + 6 * i, tmp);
+    for (int k = 0; k < 6; k++) cfrc[6 * i + k] += tmp1[k];
+  }
+  memset(cfrc, 0, 6 * sizeof(double));
+  for (int i = nb - 1; i > 0; i--) {
+    int p = m->body_parentid[i];
+    if (p) for (int k = 0; k < 6; k++) cfrc[6 * p + k] += cfrc[6 * i + k];
+  }
+  for (int k = 0; k < m->nv; k++) d->qfrc_bias[k] = dot6(d->cdof + 6 * k, cfrc + 6 * m->dof_bodyid[k]);
+}
+
+/* mj_fwdActuation for joint transmissions [ext] */
+static void actuation(const mgx_model_desc *m, ref_data *d) {
+  memset(d->qfrc_actuator, 0, sizeof(double) * m->nv);
+  for (int u = 0; u < m->nu; u++) {
+    int j = m->actuator_trnid[u];
+    double ctrl = d->ctrl[u];
+    if (m->actuator_ctrllimited[u]) ctrl = clampd(ctrl, m->actuator_ctrlrange[2 * u], m->actuator_ctrlrange[2 * u + 1]);
+    double g = m->actuator_gear[u];
+    double len = g * d->qpos[m->jnt_qposadr[j]], vel = g * d->qvel[m->jnt_dofadr[j]];
+    const double *gp = m->actuator_gainprm + 3 * u, *bp = m->actuator_biasprm + 3 * u;
+    double f = gp[0] * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
+    if (m->actuator_forcelimited[u]) f = clampd(f, m->actuator_forcerange[2 * u], m->actuator_forcerange[2 * u + 1]);
+    d->actuator_force[u] = f;
+    d->qfrc_actuator[m->jnt_dofadr[j]] += g * f;
+  }
+}
+
+/* mj_xfrcAccumulate: qfrc += J(xipos)' * xfrc_applied [ext] */
+static void xfrc_accumulate(const mgx_model_desc *m, ref_data *d, double *qfrc) {
+  int nv = m->nv;
+  double *jp = d->scratch + 12 * m->nbody, *jr = jp + 3 * nv;
+  for (int i = 1; i < m->nbody; i++) {
+    const double *f = d->xfrc_applied + 6 * i;
+    if (!f[0] && !f[1] && !f[2] && !f[3] && !f[4] && !f[5]) continue;
+    jac(m, d, jp, jr, d->xipos + 3 * i, i);
+    for (int k = 0; k < nv; k++)
+      qfrc[k] += jp[k] * f[0] + jp[nv + k] * f[1] + jp[2 * nv + k] * f[2] +
+                 jr[k] * f[3] + jr[nv + k] * f[4] + jr[2 * nv + k] * f[5];
+  }
+}
+
+/* ====================================================================== solver */
+/* mj_constraintUpdate restricted to limit/contact rows (one-sided) */
+static void constraint_force_from_jar(ref_data *d, const double *jar) {
+  for (int r = 0; r < d->nefc[0]; r++) d->efc_force[r] = jar[r] < 0 ? -d->efc_D[r] * jar[r] : 0;
+}
+
+/* mj_fwdConstraint with warmstart + mj_solPGS [ext] */
+static void fwd_constraint(const mgx_model_desc *m, ref_data *d) {
+  int nv = m->nv, ne = d->nefc[0];
+  if (!ne) {
+    memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
+    memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+    d->solver_niter[0] = 0;
+    return;
+  }
+  double *jar = d->scratch, *ARf = jar + ne;
+  /* efc_b = J qacc_smooth - aref */
+  for (int r = 0; r < ne; r++) {
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += d->efc_J[(size_t)r * nv + k] * d->qacc_smooth[k];
+    d->efc_b[r] = s - d->efc_aref[r];
+  }
+  /* warmstart: forces implied by qacc_warmstart; zero if its dual cost is positive */
+  for (int r = 0; r < ne; r++) {
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += d->efc_J[(size_t)r * nv + k] * d->qacc_warmstart[k];
+    jar[r] = s - d->efc_aref[r];
+  }
+  constraint_force_from_jar(d, jar);
+  double cost = 0;
+  for (int r = 0; r < ne; r++) {
+    double s = 0;
+    for (int c = 0; c < ne; c++) s += d->efc_AR[(size_t)r * ne + c] * d->efc_force[c];
+    ARf[r] = s;
+    cost += d->efc_force[r] * (d->efc_b[r] + 0.5 * s);
+  }
+  if (cost > 0) memset(d->efc_force, 0, sizeof(double) * ne);
+  /* PGS sweeps */
+  double scale = 1 / (m->meaninertia * (nv > 1 ? nv : 1));
+  int iter = 0;
+  while (iter < m->iterations) {
+    double improvement = 0;
+    for (int r = 0; r < ne; r++) {
+      const double *Ar = d->efc_AR + (size_t)r * ne;
+      double res = d->efc_b[r];
+      for (int c = 0; c < ne; c++) res += Ar[c] * d->efc_force[c];
+      double Arr = Ar[r], old = d->efc_force[r];
+      double f = old - res / Arr;
+      if (d->efc_type[r] >= C_LIMIT_JOINT && f < 0) f = 0;
+      double delta = f - old;
+      double change = 0.5 * delta * delta * Arr + delta * res;
+      if (change > 1e-10) { f = old; change = 0; }
+      d->efc_force[r] = f;
+      improvement -= change;
+    }
+    iter++;
+    if (improvement * scale < m->tolerance) break;
+  }
+  d->solver_niter[0] = iter;
+  /* qfrc_constraint = J' f ; qacc = qacc_smooth + M^-1 qfrc_constraint */
+  memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+  for (int r = 0; r < ne; r++)
+    for (int k = 0; k < nv; k++) d->qfrc_constraint[k] += d->efc_J[(size_t)r * nv + k] * d->efc_force[r];
+  double *tmp = d->scratch;
+  memcpy(tmp, d->qfrc_constraint, sizeof(double) * nv);
+  solve_ld(m, d->qLD, d->qLDiagInv, tmp);
+  for (int k = 0; k < nv; k++) d->qacc[k] = d->qacc_smooth[k] + tmp[k];
+}
+
+/* ====================================================================== forward / step */
+void ref_forward(const mgx_model_desc *m, ref_data *d) {
+  int nv = m->nv;
+  /* mj_fwdPosition */
+  kinematics(m, d);
+  compos(m, d);
+  crb(m, d);
+  factor_ld(m, d->qM, d->qLD, d->qLDiagInv);
+  collision(m, d);
+  make_constraint(m, d);
+  make_impedance(m, d);
+  project_constraint(m, d);
+  /* mj_fwdVelocity */
+  comvel(m, d);
+  passive(m, d);
+  for (int r = 0; r < d->nefc[0]; r++) { /* mj_referenceConstraint */
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += d->efc_J[(size_t)r * nv + k] * d->qvel[k];
+    d->efc_vel[r] = s;
+    d->efc_aref[r] = -d->efc_KBIP[4 * r + 1] * s -
+                     d->efc_KBIP[4 * r] * d->efc_KBIP[4 * r + 2] * (d->efc_pos[r] - d->efc_margin[r]);
+  }
+  rne(m, d);
+  /* mj_fwdActuation, mj_fwdAcceleration */
+  actuation(m, d);
+  for (int k = 0; k < nv; k++)
+    d->qfrc_smooth[k] = d->qfrc_passive[k] - d->qfrc_bias[k] + d->qfrc_applied[k] + d->qfrc_actuator[k];
+  xfrc_accumulate(m, d, d->qfrc_smooth);
+  memcpy(d->qacc_smooth, d->qfrc_smooth, sizeof(double) * nv);
+  solve_ld(m, d->qLD, d->qLDiagInv, d->qacc_smooth);
+  /* mj_fwdConstraint */
+  fwd_constraint(m, d);
+}
+
+/* mju_quatIntegrate */
+static void quat_integrate(double *q, const double *w, double h) {
+  double ax[3] = {w[0], w[1], w[2]}, qr[4];
+  double ang = h * normalize3(ax);
+  axisangle2quat(qr, ax, ang);
+  normalize4(q);
+  mulquat(q, q, qr);
+}
+
+/* mj_integratePos [ext] */
+static void integrate_pos(const mgx_model_desc *m, double *qpos, const double *qvel, double h) {
+  for (int j = 0; j < m->njnt; j++) {
+    int a = m->jnt_qposadr[j], da = m->jnt_dofadr[j], t = m->jnt_type[j];
+    if (t == JFREE) {
+      for (int k = 0; k < 3; k++) qpos[a + k] += h * qvel[da + k];
+      quat_integrate(qpos + a + 3, qvel + da + 3, h);
+    } else if (t == JBALL) {
+      quat_integrate(qpos + a, qvel + da, h);
+    } else {
+      qpos[a] += h * qvel[da];
+    }
+  }
+}
+
+/* mj_Euler with implicit joint damping:
+ * qacc <- (M + h diag(damping))^-1 (qfrc_smooth + qfrc_constraint) [ext] */
+static void euler(const mgx_model_desc *m, ref_data *d) {
+  int nv = m->nv;
+  double *qacc = d->scratch, *MH = qacc + nv, *MHinv = MH + m->nM;
+  int damp = 0;
+  for (int k = 0; k < nv; k++) if (m->dof_damping[k] > 0) damp = 1;
+  if (!damp) memcpy(qacc, d->qacc, sizeof(double) * nv);
+  else {
+    memcpy(MH, d->qM, sizeof(double) * m->nM);
+    for (int k = 0; k < nv; k++) MH[m->dof_Madr[k]] += m->timestep * m->dof_damping[k];
+    factor_ld(m, MH, MH, MHinv);
+    for (int k = 0; k < nv; k++) qacc[k] = d->qfrc_smooth[k] + d->qfrc_constraint[k];
+    solve_ld(m, MH, MHinv, qacc);
+  }
+  for (int k = 0; k < nv; k++) d->qvel[k] += m->timestep * qacc[k];
+  integrate_pos(m, d->qpos, d->qvel, m->timestep);
+  d->time[0] += m->timestep;
+}
+
+static int check_bad(const double *x, int n) {
+  for (int i = 0; i < n; i++) if (isbad(x[i])) return 1;
+  return 0;
+}
+
+/* mj_step: checkPos, checkVel, forward, checkAcc, Euler [ext] */
+void ref_step(const mgx_model_desc *m, ref_data *d) {
+  if (check_bad(d->qpos, m->nq)) { ref_reset(m, d); d->warning[0]++; }
+  if (check_bad(d->qvel, m->nv)) { ref_reset(m, d); d->warning[0]++; }
+  ref_forward(m, d);
+  if (check_bad(d->qacc, m->nv)) {
+    ref_reset(m, d);
+    d->warning[0]++;
+    ref_forward(m, d);
+  }
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * m->nv);
+  euler(m, d);
+}

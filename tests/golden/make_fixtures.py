@@ -1,0 +1,359 @@
+"""Generate the committed golden fixtures from the reference's own Python code.
+
+Run in the build container only (needs /root/reference):  python tests/golden/make_fixtures.py
+
+The reference's env modules import `mujoco` and `gymnasium`, neither of which is installed
+(SURVEY.md §8c). We import them with tiny stub modules and call the reference's own methods:
+
+1. composed MJCF strings: HumanoidSoccerEnv._load_xml_models (soccer_env.py:120-220),
+   QuadrupedParkourEnv._combine_models (parkour_env.py:105-179),
+   BipedalRescueEnv._load_xml_models (rescue_env.py:121-277),
+   HumanoidDancingEnv._load_xml_models (dancing_env.py:156-678); the construction,
+   martial-arts and assembly XML are the reference's on-disk assets (byte-identical to
+   their generators per SURVEY.md §8c).
+2. soccer reset randomisation (soccer_env.py:454-504) for a list of seeds.
+3. soccer env-logic vectors: _update_goalkeeper, _apply_environmental_effects,
+   _get_observation, _calculate_reward, _check_termination (soccer_env.py:506-716) on
+   synthetic MjData-like state with contact lists.
+
+Only data (inputs -> outputs) is written; nothing from the reference is copied into the repo.
+The fake MjModel/MjData fields come from our own MJCF compiler (name tables, jnt_* arrays).
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from mujoco_gymnasium_environments_amd import mjcf  # noqa: E402
+
+
+# ------------------------------------------------------------------------------- stubs
+class _Box:
+    def __init__(self, low, high, shape=None, dtype=np.float32):
+        dtype = np.dtype(dtype)
+        if shape is not None:
+            self.low = np.full(shape, low, dtype=dtype)
+            self.high = np.full(shape, high, dtype=dtype)
+        else:
+            self.low = np.asarray(low, dtype=dtype)
+            self.high = np.asarray(high, dtype=dtype)
+        self.shape = self.low.shape
+        self.dtype = dtype
+
+
+def _np_random(seed=None):
+    ss = np.random.SeedSequence(seed)
+    return np.random.Generator(np.random.PCG64(ss)), ss.entropy
+
+
+class _ObjT:
+    mjOBJ_BODY, mjOBJ_JOINT, mjOBJ_GEOM, mjOBJ_SITE, mjOBJ_ACTUATOR, mjOBJ_SENSOR = range(6)
+
+
+_KIND = {0: "body", 1: "joint", 2: "geom", 3: "site", 4: "actuator"}
+CURRENT_MODEL: dict = {}
+
+
+def _quat2mat(res, quat):
+    w, x, y, z = quat
+    R = mjcf.quat2mat(np.array([w, x, y, z], dtype=np.float64) /
+                      max(1e-15, float(np.linalg.norm(quat))))
+    res[:] = R.reshape(-1)
+
+
+def install_stubs():
+    mj = types.ModuleType("mujoco")
+    mj.mjtObj = _ObjT
+    mj.mj_name2id = lambda m, t, n: m._c.name2id(_KIND[t], n) if t in _KIND else -1
+    mj.mj_id2name = lambda m, t, i: m._c.id2name(_KIND[t], i)
+    mj.mju_quat2Mat = _quat2mat
+    mj.mj_step = lambda m, d: setattr(d, "nstep", getattr(d, "nstep", 0) + 1)
+    mj.mj_resetData = lambda m, d: d.reset()
+    mj.mj_forward = lambda m, d: None
+
+    class MjModel:
+        @staticmethod
+        def from_xml_string(xml):
+            return FakeModel(mjcf.compile_xml(xml))
+    mj.MjModel = MjModel
+    mj.MjData = lambda m: FakeData(m)
+    viewer = types.ModuleType("mujoco.viewer")
+    mj.viewer = viewer
+    sys.modules["mujoco"] = mj
+    sys.modules["mujoco.viewer"] = viewer
+
+    gym = types.ModuleType("gymnasium")
+    gym.Env = object
+    spaces = types.ModuleType("gymnasium.spaces")
+    spaces.Box = _Box
+    spaces.Dict = dict
+    spaces.Discrete = lambda n: n
+    gym.spaces = spaces
+    utils = types.ModuleType("gymnasium.utils")
+    seeding = types.ModuleType("gymnasium.utils.seeding")
+    seeding.np_random = _np_random
+    utils.seeding = seeding
+    gym.utils = utils
+    gym.register = lambda *a, **k: None
+    err = types.ModuleType("gymnasium.error")
+    err.Error = Exception
+    gym.error = err
+    envs = types.ModuleType("gymnasium.envs")
+    reg = types.ModuleType("gymnasium.envs.registration")
+    reg.register = lambda *a, **k: None
+    envs.registration = reg
+    gym.envs = envs
+    for k, v in {"gymnasium": gym, "gymnasium.spaces": spaces, "gymnasium.utils": utils,
+                 "gymnasium.utils.seeding": seeding, "gymnasium.error": err,
+                 "gymnasium.envs": envs, "gymnasium.envs.registration": reg}.items():
+        sys.modules[k] = v
+
+
+class FakeModel:
+    def __init__(self, c: mjcf.Model):
+        self._c = c
+        self.nu, self.nq, self.nv, self.nbody, self.ngeom = c.nu, c.nq, c.nv, c.nbody, c.ngeom
+        self.jnt_qposadr = c.jnt_qposadr.copy()
+        self.jnt_dofadr = c.jnt_dofadr.copy()
+        self.jnt_range = c.jnt_range.copy()
+        self.qpos0 = c.qpos0.copy()
+
+
+class FakeContact:
+    def __init__(self, g1, g2, dist, friction):
+        self.geom1, self.geom2, self.dist = int(g1), int(g2), float(dist)
+        self.friction = np.asarray(friction, dtype=np.float64)
+
+
+class FakeData:
+    def __init__(self, m: FakeModel):
+        self.m = m
+        self.reset()
+
+    def reset(self):
+        c = self.m._c
+        self.qpos = c.qpos0.copy()
+        self.qvel = np.zeros(c.nv)
+        self.ctrl = np.zeros(c.nu)
+        self.qfrc_applied = np.zeros(c.nv)
+        self.xfrc_applied = np.zeros((c.nbody, 6))
+        self.xpos = np.zeros((c.nbody, 3))
+        self.xquat = np.tile([1.0, 0, 0, 0], (c.nbody, 1))
+        self.subtree_com = np.zeros((c.nbody, 3))
+        self.contact = []
+        self.ncon = 0
+        self.time = 0.0
+
+
+def load_module(path, name):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# ------------------------------------------------------------------------------- XML
+def dump_xml():
+    out = {}
+    soccer = load_module(f"{REF}/humanoid_soccer_env/soccer_env.py", "ref_soccer_env")
+    o = object.__new__(soccer.HumanoidSoccerEnv)
+    o.dt = 0.02
+    soccer.HumanoidSoccerEnv._load_xml_models(o)
+    out["humanoid_soccer"] = o.xml_string
+
+    parkour = load_module(f"{REF}/quadruped_parkour_env/parkour_env.py", "ref_parkour_env")
+    o = object.__new__(parkour.QuadrupedParkourEnv)
+    a = f"{REF}/quadruped_parkour_env/assets"
+    out["quadruped_parkour"] = parkour.QuadrupedParkourEnv._combine_models(
+        o, f"{a}/quadruped.xml", f"{a}/parkour_course.xml", f"{a}/terrain_variations.xml")
+
+    for key, path, modname, cls in [
+        ("bipedal_rescue", "bipedal_rescue_env/rescue_env.py", "ref_rescue_env", "BipedalRescueEnv"),
+        ("humanoid_dancing", "humanoid_dancing_env/dancing_env.py", "ref_dancing_env", "HumanoidDancingEnv"),
+    ]:
+        try:
+            mod = load_module(f"{REF}/{path}", modname)
+            o = object.__new__(getattr(mod, cls))
+            o.dt = getattr(o, "dt", 0.02)
+            getattr(mod, cls)._load_xml_models(o)
+            out[key] = o.xml_string
+        except Exception as e:  # noqa: BLE001 - record and continue; later rounds widen
+            print(f"[fixtures] {key}: composition failed: {e!r}")
+    for key, path in [("humanoid_construction", "humanoid_construction_env/assets/construction_site.xml"),
+                      ("humanoid_martial_arts", "humanoid_martial_arts_env/assets/martial_arts_scene.xml"),
+                      ("robotic_arm_assembly", "robotic_arm_assembly_env/assets/complete_model.xml")]:
+        with open(f"{REF}/{path}") as f:
+            out[key] = f.read()
+    os.makedirs(f"{HERE}/xml", exist_ok=True)
+    for k, v in out.items():
+        with open(f"{HERE}/xml/{k}.xml", "w") as f:
+            f.write(v)
+    # the package ships the composed soccer / parkour models it simulates
+    pkg_assets = f"{REPO}/mujoco_gymnasium_environments_amd/assets"
+    os.makedirs(pkg_assets, exist_ok=True)
+    for k in ("humanoid_soccer", "quadruped_parkour"):
+        with open(f"{pkg_assets}/{k}.xml", "w") as f:
+            f.write(out[k])
+    return out
+
+
+# ------------------------------------------------------------------------------- soccer
+def soccer_env():
+    install_stubs()
+    soccer = load_module(f"{REF}/humanoid_soccer_env/soccer_env.py", "ref_soccer_env2")
+    env = soccer.HumanoidSoccerEnv(render_mode=None)
+    return env
+
+
+def soccer_reset_vectors(env, seeds):
+    rows = []
+    for s in seeds:
+        env.seed(int(s))
+        env.data.reset()
+        env._randomize_initial_state()
+        env._update_environmental_factors()
+        rows.append(dict(qpos=env.data.qpos.copy(), wind_strength=env.wind_strength,
+                         wind_direction=env.wind_direction.copy(),
+                         friction_var=env.field_friction_variation))
+    return dict(seeds=np.asarray(seeds, np.int64),
+                qpos=np.stack([r["qpos"] for r in rows]),
+                wind_strength=np.array([r["wind_strength"] for r in rows]),
+                wind_direction=np.stack([r["wind_direction"] for r in rows]),
+                friction_var=np.array([r["friction_var"] for r in rows]))
+
+
+def soccer_envlogic_vectors(env, n, seed=1234, max_contacts=12):
+    """Random synthetic states -> reference env-logic outputs."""
+    c = env.model._c
+    rng = np.random.default_rng(seed)
+    torso, ball, gk = env.torso_id, env.ball_id, env.goalkeeper_id
+    cand = c.pair_geom
+    nb, nq, nv = c.nbody, c.nq, c.nv
+    keys = ["qpos", "qvel", "xpos", "xquat", "subtree_com", "ncon", "con_geom", "con_dist",
+            "con_friction", "prev_ball_pos", "prev_robot_pos", "current_step", "goal_scored_in",
+            "wind_strength", "wind_direction", "qfrc_applied_in", "xfrc_applied_in", "action",
+            # outputs
+            "qfrc_applied_out", "xfrc_applied_out", "obs", "reward", "terminated", "truncated",
+            "goal_scored_out", "ball_contact", "upright"]
+    out = {k: [] for k in keys}
+    for i in range(n):
+        d = env.data
+        d.reset()
+        lo, hi = c.jnt_range[:, 0], c.jnt_range[:, 1]
+        qpos = c.qpos0.copy()
+        for j in range(c.njnt):
+            a = c.jnt_qposadr[j]
+            if c.jnt_type[j] == mjcf.JNT_FREE:
+                qpos[a:a + 3] = rng.uniform(-20, 20, 3)
+                q = rng.normal(size=4)
+                qpos[a + 3:a + 7] = q / np.linalg.norm(q)
+            else:
+                span = hi[j] - lo[j]
+                qpos[a] = rng.uniform(lo[j] - 0.2 * span, hi[j] + 0.2 * span)
+        d.qpos[:] = qpos
+        d.qvel[:] = rng.normal(scale=rng.choice([0.5, 5.0, 30.0]), size=nv)
+        xpos = rng.uniform(-5, 5, (nb, 3))
+        scen = i % 8
+        xpos[torso] = [rng.uniform(-32, 32), rng.uniform(-22, 22), rng.uniform(-0.5, 5.5)]
+        xpos[ball] = [rng.uniform(-32, 32), rng.uniform(-22, 22), rng.uniform(-1.5, 11)]
+        if scen == 0:   # goal zone
+            xpos[ball] = [rng.uniform(24.0, 26), rng.uniform(-3.6, 3.6), rng.uniform(0, 2.4)]
+        elif scen == 1:  # ball deep in own half -> goalkeeper reacts
+            xpos[ball] = [rng.uniform(-25, -10.01), rng.uniform(-6, 6), rng.uniform(0.1, 1.5)]
+        elif scen == 2:  # in bounds, calm
+            xpos[torso] = [rng.uniform(-20, 20), rng.uniform(-10, 10), rng.uniform(0.5, 2)]
+            xpos[ball] = [rng.uniform(-20, 20), rng.uniform(-10, 10), rng.uniform(0.1, 3)]
+        xpos[gk] = [-23.0, rng.uniform(-3.7, 3.7), 0.9]
+        d.xpos[:] = xpos
+        q = rng.normal(size=(nb, 4))
+        if scen in (2, 3):
+            q[torso] = [1, rng.normal(scale=0.2), rng.normal(scale=0.2), rng.normal()]
+        d.xquat[:] = q / np.linalg.norm(q, axis=1, keepdims=True)
+        d.subtree_com[:] = rng.uniform(-40, 40, (nb, 3))
+        ncon = int(rng.integers(0, max_contacts + 1))
+        picks = rng.integers(0, len(cand), ncon)
+        geoms = cand[picks].copy()
+        # force foot-ground and ball-limb contacts into some cases
+        if scen in (4, 5) and ncon >= 2:
+            geoms[0] = [0, env.right_foot_id]
+            geoms[-1] = [env.left_foot_id, 0] if scen == 4 else [0, env.left_foot_id]
+        if scen in (5, 6) and ncon >= 3:
+            geoms[1] = [env.ball_geom_id, int(rng.integers(31, 45))]
+        dist = rng.uniform(-0.05, 0.01, ncon)
+        fric = np.tile([1.0, 1.0, 0.5, 0.5, 0.5], (ncon, 1)) * rng.uniform(0.5, 1.5, (ncon, 1))
+        d.contact = [soccer_contact(g[0], g[1], dd, ff) for g, dd, ff in zip(geoms, dist, fric)]
+        d.ncon = ncon
+        env.prev_ball_pos = xpos[ball] + rng.normal(scale=0.3, size=3)
+        env.prev_robot_pos = xpos[torso] + rng.normal(scale=0.3, size=3)
+        env.current_step = int(rng.choice([0, 50, 100, 101, 2000, 4999, 5000, int(rng.integers(0, 6000))]))
+        env.goal_scored = bool(rng.random() < 0.15)
+        goal_in = env.goal_scored
+        env.wind_strength = float(rng.uniform(0, 2))
+        ang = float(rng.uniform(0, 2 * np.pi))
+        env.wind_direction = np.array([np.cos(ang), np.sin(ang)])
+        d.qfrc_applied[:] = 0
+        d.qfrc_applied[0] = rng.uniform(-100, 100)
+        d.xfrc_applied[:] = 0
+        d.xfrc_applied[ball, :2] = rng.normal(size=2)
+        qfrc_in = d.qfrc_applied[0]
+        xfrc_in = d.xfrc_applied[ball, :2].copy()
+        action = rng.uniform(-200, 200, c.nu).astype(np.float32)
+        action = np.clip(action, env.action_space.low, env.action_space.high)
+        # pre-physics env logic (soccer_env.py:408-411)
+        env._update_goalkeeper()
+        env._apply_environmental_effects()
+        # post-physics (soccer_env.py:420-427); physics is not run: state is synthetic
+        obs = env._get_observation()
+        reward = env._calculate_reward(action)
+        term = env._check_termination()
+        trunc = env.current_step >= env.max_episode_steps
+        vals = dict(qpos=qpos, qvel=d.qvel.copy(), xpos=xpos, xquat=d.xquat.copy(),
+                    subtree_com=d.subtree_com.copy(), ncon=ncon,
+                    con_geom=_pad(geoms, max_contacts, 2, -1), con_dist=_pad(dist, max_contacts),
+                    con_friction=_pad(fric, max_contacts, 5), prev_ball_pos=env.prev_ball_pos,
+                    prev_robot_pos=env.prev_robot_pos, current_step=env.current_step,
+                    goal_scored_in=goal_in, wind_strength=env.wind_strength,
+                    wind_direction=env.wind_direction, qfrc_applied_in=qfrc_in,
+                    xfrc_applied_in=xfrc_in, action=action,
+                    qfrc_applied_out=d.qfrc_applied[0], xfrc_applied_out=d.xfrc_applied[ball, :2].copy(),
+                    obs=obs, reward=float(reward), terminated=bool(term), truncated=bool(trunc),
+                    goal_scored_out=bool(env.goal_scored), ball_contact=bool(env._check_ball_contact()),
+                    upright=bool(env._is_robot_upright()))
+        for k in keys:
+            out[k].append(vals[k])
+    return {k: np.asarray(v) for k, v in out.items()}
+
+
+def soccer_contact(g1, g2, dist, fr):
+    return FakeContact(g1, g2, dist, fr)
+
+
+def _pad(a, n, w=None, fill=0.0):
+    a = np.asarray(a, dtype=np.float64)
+    shape = (n,) if w is None else (n, w)
+    out = np.full(shape, fill, dtype=np.float64)
+    if len(a):
+        out[:len(a)] = a
+    return out
+
+
+def main():
+    install_stubs()
+    dump_xml()
+    env = soccer_env()
+    np.savez_compressed(f"{HERE}/soccer_reset.npz", **soccer_reset_vectors(env, list(range(0, 40)) + [12345, 2**31 - 1]))
+    np.savez_compressed(f"{HERE}/soccer_envlogic.npz", **soccer_envlogic_vectors(env, 400))
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
