@@ -188,11 +188,8 @@ def dump_xml():
             out[key] = o.xml_string
         except Exception as e:  # noqa: BLE001 - record and continue; later rounds widen
             print(f"[fixtures] {key}: composition failed: {e!r}")
-    for key, path in [("humanoid_construction", "humanoid_construction_env/assets/construction_site.xml"),
-                      ("humanoid_martial_arts", "humanoid_martial_arts_env/assets/martial_arts_scene.xml"),
-                      ("robotic_arm_assembly", "robotic_arm_assembly_env/assets/complete_model.xml")]:
-        with open(f"{REF}/{path}") as f:
-            out[key] = f.read()
+    # construction / martial arts / assembly load their on-disk assets unchanged; those files
+    # are read from /root/reference by the tests that need them, never copied into the repo.
     os.makedirs(f"{HERE}/xml", exist_ok=True)
     for k, v in out.items():
         with open(f"{HERE}/xml/{k}.xml", "w") as f:
