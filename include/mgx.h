@@ -142,6 +142,10 @@ typedef struct mgx_soccer_env {
   int32_t *step;         /* [N]     current_step */
   uint8_t *goal_scored;  /* [N]     latched flag (soccer_env.py:641) */
   void *stats;           /* [N][5]  goals, contacts, distance, time_upright, max_ball_speed */
+  int32_t *episode;      /* [N]     episodes started (keys the device reset draws); nullable
+                                    when every reset passes host draws */
+  uint8_t *flags;        /* [N][2]  ball_contact, robot_upright of the last step (info dict,
+                                    soccer_env.py:438-439); nullable */
 } mgx_soccer_env;
 
 typedef struct mgx_soccer_ids {
@@ -160,16 +164,39 @@ int mgx_soccer_configure_reset(mgx_model *m, int root_qposadr, int n_noise, cons
                                const double *noise_range);
 
 /* One env step for N envs (soccer_env.py:398-452): action clip, goalkeeper, wind, mj_step,
- * observation [N][80] (float32), reward [N] (float64), terminated/truncated [N] (uint8). */
+ * observation [N][80] (float32), reward [N] (float64), terminated/truncated [N] (uint8).
+ * autoreset != 0: envs that end are reset in the same launch (gymnasium same-step autoreset):
+ * obs then holds the reset observation and final_obs (nullable) the last one; reset draws
+ * come from Philox keyed by (seed, env_offset + env index, episode). */
 int mgx_soccer_step(const mgx_model *m, const mgx_state *s, const mgx_soccer_env *e,
                     const float *action, float *obs, double *reward, uint8_t *terminated,
-                    uint8_t *truncated, int n_env, const uint8_t *env_mask, void *stream);
+                    uint8_t *truncated, float *final_obs, int autoreset, uint64_t seed, int env_offset,
+                    int n_env, const uint8_t *env_mask, void *stream);
 
-/* reset(seed) for masked envs (soccer_env.py:347-396): mj_resetData, apply the 36 uniform
- * draws per env (`draws` [N][36] real, in reference order), 10 settle mj_step's, obs. */
+/* reset() for masked envs (soccer_env.py:347-396): mj_resetData, the 36 randomisation draws
+ * (`draws` [N][36] real in reference order, e.g. from numpy PCG64 for exact gymnasium
+ * seeding; NULL = device Philox draws keyed like mgx_soccer_step), 10 settle mj_step's, obs. */
 int mgx_soccer_reset(const mgx_model *m, const mgx_state *s, const mgx_soccer_env *e,
-                     const void *draws, float *obs, int n_env, const uint8_t *env_mask,
-                     void *stream);
+                     const void *draws, float *obs, uint64_t seed, int env_offset, int n_env,
+                     const uint8_t *env_mask, void *stream);
+
+/* Test hook: env logic only, on caller-supplied frames and contact lists (no physics). */
+typedef struct mgx_soccer_logic_io {
+  const void *qpos, *qvel, *xpos, *xquat, *subtree_com; /* [N][nq] [N][nv] [N][nbody][3|4|3] */
+  const int32_t *ncon, *con_geom;                       /* [N], [N][max_contacts][2] */
+  const void *con_dist, *con_mu;                        /* [N][max_contacts] */
+  int32_t max_contacts;
+  int32_t pad0;
+  void *prev_ball_pos, *prev_robot_pos, *wind, *stats;  /* in/out like mgx_soccer_env */
+  int32_t *step;
+  uint8_t *goal_scored;
+  void *qfrc_applied, *xfrc_applied;                    /* in/out [N][nv], [N][nbody][6] */
+  const float *action;                                  /* [N][nu] */
+  float *obs;                                           /* [N][80] */
+  double *reward;
+  uint8_t *terminated, *truncated, *flags;              /* flags [N][2]: ball_contact, upright */
+} mgx_soccer_logic_io;
+int mgx_soccer_logic_test(const mgx_model *m, const mgx_soccer_logic_io *io, int n_env, void *stream);
 
 #ifdef __cplusplus
 }

@@ -71,7 +71,19 @@ class MgxFrames(C.Structure):
 
 class MgxSoccerEnv(C.Structure):
     _fields_ = [("prev_ball_pos", C.c_void_p), ("prev_robot_pos", C.c_void_p), ("wind", C.c_void_p),
-                ("step", C.c_void_p), ("goal_scored", C.c_void_p), ("stats", C.c_void_p)]
+                ("step", C.c_void_p), ("goal_scored", C.c_void_p), ("stats", C.c_void_p),
+                ("episode", C.c_void_p), ("flags", C.c_void_p)]
+
+
+class MgxSoccerLogicIO(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("xpos", C.c_void_p), ("xquat", C.c_void_p),
+                ("subtree_com", C.c_void_p), ("ncon", C.c_void_p), ("con_geom", C.c_void_p),
+                ("con_dist", C.c_void_p), ("con_mu", C.c_void_p), ("max_contacts", C.c_int32),
+                ("pad0", C.c_int32), ("prev_ball_pos", C.c_void_p), ("prev_robot_pos", C.c_void_p),
+                ("wind", C.c_void_p), ("stats", C.c_void_p), ("step", C.c_void_p), ("goal_scored", C.c_void_p),
+                ("qfrc_applied", C.c_void_p), ("xfrc_applied", C.c_void_p), ("action", C.c_void_p),
+                ("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p),
+                ("truncated", C.c_void_p), ("flags", C.c_void_p)]
 
 
 class MgxSoccerIds(C.Structure):

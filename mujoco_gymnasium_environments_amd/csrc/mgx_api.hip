@@ -162,11 +162,29 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   }
 }
 
-// soccer: mode 0 = step, 1 = reset
+// soccer reset body shared by the explicit-reset and autoreset paths: draws (36 values in
+// reference order, from the host or from Philox) -> randomised qpos, 10 settle mj_steps, obs.
+template <typename T>
+__device__ int soccer_reset_body(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const T* draws, T* wind,
+                                 T* prev_ball, T* prev_robot, T* stats, int* step, uint8_t* goal, float* obs) {
+  soccer_apply_reset(m, e, ids, draws, wind);
+  int warn = 0;
+  for (int k = 0; k < 10; k++) warn += mj_step_env(m, e);  // soccer_env.py:378-379
+  soccer_obs(m, e, ids, 0, obs);
+  wsync();
+  int l = lane_id();
+  if (l < 3) { prev_ball[l] = e.xpos[3 * ids.ball + l]; prev_robot[l] = e.xpos[3 * ids.torso + l]; }
+  if (l < 5) stats[l] = 0;
+  if (l == 0) { *step = 0; *goal = 0; }
+  return warn;
+}
+
+// soccer: MODE 0 = step (+ optional same-step autoreset), MODE 1 = reset
 template <typename T, int MODE>
 __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
                                                const float* action, const T* draws, float* obs, double* reward,
-                                               uint8_t* terminated, uint8_t* truncated, int n_env,
+                                               uint8_t* terminated, uint8_t* truncated, float* final_obs,
+                                               int autoreset, uint64_t seed, int env_offset, int n_env,
                                                const uint8_t* mask) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int env = blockIdx.x;
@@ -181,26 +199,78 @@ __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, 
   T* prev_robot = (T*)ev.prev_robot_pos + 3 * (size_t)env;
   T* wind = (T*)ev.wind + 3 * (size_t)env;
   T* stats = (T*)ev.stats + 5 * (size_t)env;
+  float* o = obs + (size_t)env * 80;
   int l = lane_id();
   int warn = 0;
+  bool do_reset = MODE == 1;
   if (MODE == 0) {
     const float* a = action + (size_t)env * m.nu;
     soccer_pre(m, e, ids, a, prev_ball, wind);
     warn += mj_step_env(m, e);
-    store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball, prev_robot, stats,
-                obs + (size_t)env * 80, reward + env, terminated + env, truncated + env);
-  } else {
-    soccer_apply_reset(m, e, ids, draws + (size_t)env * 36, wind);
-    for (int k = 0; k < 10; k++) warn += mj_step_env(m, e);
-    store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    soccer_obs(m, e, ids, 0, obs + (size_t)env * 80);
-    wsync();
-    if (l < 3) { prev_ball[l] = e.xpos[3 * ids.ball + l]; prev_robot[l] = e.xpos[3 * ids.torso + l]; }
-    if (l < 5) stats[l] = 0;
-    if (l == 0) { ev.step[env] = 0; ev.goal_scored[env] = 0; }
+    bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball, prev_robot, stats, o,
+                            reward + env, terminated + env, truncated + env,
+                            ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
+    if (done && autoreset) {
+      if (final_obs)
+        for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];
+      do_reset = true;
+    }
   }
+  if (do_reset) {
+    const T* d = draws ? draws + (size_t)env * 36 : nullptr;
+    if (!d) {  // counter-based draws for this env's next episode
+      soccer_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)ev.episode[env], ids.n_noise, e.vec1);
+      wsync();
+      d = e.vec1;
+    }
+    warn += soccer_reset_body(m, e, ids, d, wind, prev_ball, prev_robot, stats, ev.step + env,
+                              ev.goal_scored + env, o);
+    if (l == 0) ev.episode[env] += 1;
+  }
+  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+}
+
+// Env-logic-only test hook: frames/contacts come from the caller (golden vectors generated
+// from the reference's own Python), no physics is run.
+template <typename T>
+__global__ void __launch_bounds__(64) k_soccer_logic(DevModel<T> m, SoccerIds<T> ids, mgx_soccer_logic_io io,
+                                                     int n_env) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int env = blockIdx.x;
+  if (env >= n_env) return;
+  Env<T> e;
+  env_bind(m, e, smem);
+  int l = lane_id();
+  const T* qpos = (const T*)io.qpos + (size_t)env * m.nq;
+  const T* qvel = (const T*)io.qvel + (size_t)env * m.nv;
+  for (int k = l; k < m.nq; k += 64) e.qpos[k] = qpos[k];
+  for (int k = l; k < m.nv; k += 64) e.qvel[k] = qvel[k];
+  for (int k = l; k < 3 * m.nbody; k += 64) {
+    e.xpos[k] = ((const T*)io.xpos)[(size_t)env * 3 * m.nbody + k];
+    e.subtree_com[k] = ((const T*)io.subtree_com)[(size_t)env * 3 * m.nbody + k];
+  }
+  for (int k = l; k < 4 * m.nbody; k += 64) e.xquat[k] = ((const T*)io.xquat)[(size_t)env * 4 * m.nbody + k];
+  for (int k = l; k < 6 * m.nbody; k += 64) e.xfrc[k] = ((T*)io.xfrc_applied)[(size_t)env * 6 * m.nbody + k];
+  e.qfrc_applied = l < m.nv ? ((T*)io.qfrc_applied)[(size_t)env * m.nv + l] : (T)0;
+  int nc = io.ncon[env];
+  e.ncon = nc;
+  for (int c = l; c < nc; c += 64) {
+    e.con_geom[2 * c] = io.con_geom[((size_t)env * io.max_contacts + c) * 2];
+    e.con_geom[2 * c + 1] = io.con_geom[((size_t)env * io.max_contacts + c) * 2 + 1];
+    e.con_dist[c] = ((const T*)io.con_dist)[(size_t)env * io.max_contacts + c];
+    e.con_mu[c] = ((const T*)io.con_mu)[(size_t)env * io.max_contacts + c];
+  }
+  wsync();
+  const T* stale = (const T*)io.xpos + (size_t)env * 3 * m.nbody + 3 * ids.ball;
+  const float* a = io.action + (size_t)env * m.nu;
+  soccer_pre(m, e, ids, a, stale, (const T*)io.wind + 3 * (size_t)env);
+  soccer_post(m, e, ids, a, io.step + env, io.goal_scored + env, (T*)io.prev_ball_pos + 3 * (size_t)env,
+              (T*)io.prev_robot_pos + 3 * (size_t)env, (T*)io.stats + 5 * (size_t)env, io.obs + (size_t)env * 80,
+              io.reward + env, io.terminated + env, io.truncated + env, io.flags + 2 * (size_t)env);
+  wsync();
+  if (l < m.nv) ((T*)io.qfrc_applied)[(size_t)env * m.nv + l] = e.qfrc_applied;
+  for (int k = l; k < 6 * m.nbody; k += 64) ((T*)io.xfrc_applied)[(size_t)env * 6 * m.nbody + k] = e.xfrc[k];
 }
 
 // ------------------------------------------------------------------------- host side
@@ -222,7 +292,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.cdof = take(6 * nv); L.cdof_dot = take(6 * nv); L.qLD = take(d->nM); L.qMH = take(d->nM);
   L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
   L.act_force = take(d->nu); L.con_dist = take(max_ncon); L.con_pos = take(3 * max_ncon);
-  L.con_frame = take(9 * max_ncon); L.efc_pos = take(max_nefc); L.efc_margin = take(max_nefc);
+  L.con_frame = take(9 * max_ncon); L.con_mu = take(max_ncon); L.efc_pos = take(max_nefc); L.efc_margin = take(max_nefc);
   L.efc_diag = take(max_nefc); L.efc_K = take(max_nefc); L.efc_B = take(max_nefc); L.efc_imp = take(max_nefc);
   L.efc_R = take(max_nefc); L.efc_aref = take(max_nefc); L.efc_b = take(max_nefc); L.efc_f = take(max_nefc);
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
@@ -396,9 +466,11 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   if (m->L.bytes > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "per-env LDS exceeds 160 KiB"); }
   int r2 = precision == MGX_F32
                ? (set_lds(k_step<float>, m->L.bytes) | set_lds(k_debug_forward<float>, m->L.bytes) |
-                  set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes))
+                  set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes) |
+                  set_lds(k_soccer_logic<float>, m->L.bytes))
                : (set_lds(k_step<double>, m->L.bytes) | set_lds(k_debug_forward<double>, m->L.bytes) |
-                  set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes));
+                  set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes) |
+                  set_lds(k_soccer_logic<double>, m->L.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
   *out = m;
   return MGX_OK;
@@ -509,28 +581,32 @@ int mgx_soccer_configure_reset(mgx_model* m, int root_qposadr, int n_noise, cons
 }
 
 int mgx_soccer_step(const mgx_model* m, const mgx_state* s, const mgx_soccer_env* e, const float* action, float* obs,
-                    double* reward, uint8_t* terminated, uint8_t* truncated, int n_env, const uint8_t* mask,
-                    void* stream) {
+                    double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
+                    uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
   if (!m->soccer_ok) return fail(MGX_E_ARG, "mgx_soccer_configure not called");
+  if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   int rc = check_state(s);
   if (rc) return rc;
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
   if (m->precision == MGX_F32)
     hipLaunchKernelGGL((k_soccer<float, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e, action,
-                       (const float*)nullptr, obs, reward, terminated, truncated, n_env, mask);
+                       (const float*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
+                       env_offset, n_env, mask);
   else
     hipLaunchKernelGGL((k_soccer<double, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e, action,
-                       (const double*)nullptr, obs, reward, terminated, truncated, n_env, mask);
+                       (const double*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
+                       env_offset, n_env, mask);
   HIPCHK(hipGetLastError());
   return MGX_OK;
 }
 
 int mgx_soccer_reset(const mgx_model* m, const mgx_state* s, const mgx_soccer_env* e, const void* draws, float* obs,
-                     int n_env, const uint8_t* mask, void* stream) {
-  if (!m || !e || !draws || !obs) return fail(MGX_E_ARG, "null argument");
+                     uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
+  if (!m || !e || !obs) return fail(MGX_E_ARG, "null argument");
   if (!m->soccer_ok) return fail(MGX_E_ARG, "mgx_soccer_configure not called");
+  if (!draws && !e->episode) return fail(MGX_E_ARG, "device draws need the episode counter buffer");
   int rc = check_state(s);
   if (rc) return rc;
   if (n_env <= 0) return MGX_OK;
@@ -538,11 +614,25 @@ int mgx_soccer_reset(const mgx_model* m, const mgx_state* s, const mgx_soccer_en
   if (m->precision == MGX_F32)
     hipLaunchKernelGGL((k_soccer<float, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e,
                        (const float*)nullptr, (const float*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
-                       (uint8_t*)nullptr, n_env, mask);
+                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
   else
     hipLaunchKernelGGL((k_soccer<double, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e,
                        (const float*)nullptr, (const double*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
-                       (uint8_t*)nullptr, n_env, mask);
+                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+int mgx_soccer_logic_test(const mgx_model* m, const mgx_soccer_logic_io* io, int n_env, void* stream) {
+  if (!m || !io) return fail(MGX_E_ARG, "null argument");
+  if (!m->soccer_ok) return fail(MGX_E_ARG, "mgx_soccer_configure not called");
+  if (io->max_contacts > m->L.max_ncon) return fail(MGX_E_CAPACITY, "max_contacts exceeds the contact capacity");
+  if (n_env <= 0) return MGX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (m->precision == MGX_F32)
+    hipLaunchKernelGGL(k_soccer_logic<float>, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *io, n_env);
+  else
+    hipLaunchKernelGGL(k_soccer_logic<double>, dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *io, n_env);
   HIPCHK(hipGetLastError());
   return MGX_OK;
 }

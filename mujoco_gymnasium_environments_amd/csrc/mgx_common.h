@@ -26,7 +26,7 @@ enum { C_LIMIT_JOINT = 3, C_CONTACT_FRICTIONLESS = 5, C_CONTACT_PYRAMIDAL = 6 };
 struct Layout {
   int qpos, qvel, ctrl, xfrc, xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cfrc;
   int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, geom_xpos, geom_xmat, act_force;
-  int con_dist, con_pos, con_frame;
+  int con_dist, con_pos, con_frame, con_mu;
   int efc_pos, efc_margin, efc_diag, efc_K, efc_B, efc_imp, efc_R, efc_aref, efc_b, efc_f;
   int Bmat, Bstride;
   int reals;  // total reals

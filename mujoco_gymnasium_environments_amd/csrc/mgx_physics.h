@@ -20,7 +20,7 @@ template <typename T>
 struct Env {
   T *qpos, *qvel, *ctrl, *xfrc, *xpos, *xquat, *xmat, *xipos, *ximat, *subtree_com, *cinert, *crb, *cvel, *cfrc;
   T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *geom_xpos, *geom_xmat, *act_force;
-  T *con_dist, *con_pos, *con_frame;
+  T *con_dist, *con_pos, *con_frame, *con_mu;  // con_mu = |friction[0:2]| (soccer obs)
   T *efc_pos, *efc_margin, *efc_diag, *efc_K, *efc_B, *efc_imp, *efc_R, *efc_aref, *efc_b, *efc_f;
   T *Bm;
   int Bs;
@@ -43,7 +43,7 @@ __device__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
   e.cdof = R + L.cdof; e.cdof_dot = R + L.cdof_dot; e.qLD = R + L.qLD; e.qMH = R + L.qMH;
   e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.geom_xpos = R + L.geom_xpos;
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.con_dist = R + L.con_dist;
-  e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.efc_pos = R + L.efc_pos;
+  e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc_pos = R + L.efc_pos;
   e.efc_margin = R + L.efc_margin; e.efc_diag = R + L.efc_diag; e.efc_K = R + L.efc_K;
   e.efc_B = R + L.efc_B; e.efc_imp = R + L.efc_imp; e.efc_R = R + L.efc_R; e.efc_aref = R + L.efc_aref;
   e.efc_b = R + L.efc_b; e.efc_f = R + L.efc_f; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
@@ -418,6 +418,7 @@ __device__ void collision(const DevModel<T>& m, Env<T>& e) {
       for (int q = 0; q < 3; q++) { e.con_pos[3 * k + q] = rc[c].pos[q]; e.con_frame[9 * k + q] = rc[c].n[q]; }
       make_frame(e.con_frame + 9 * k);
       e.con_pair[k] = p;
+      e.con_mu[k] = sqrt(m.pair_friction[5 * p] * m.pair_friction[5 * p] + m.pair_friction[5 * p + 1] * m.pair_friction[5 * p + 1]);
       e.con_geom[2 * k] = m.pair_geom[2 * p];
       e.con_geom[2 * k + 1] = m.pair_geom[2 * p + 1];
     }

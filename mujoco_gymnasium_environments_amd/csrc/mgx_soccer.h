@@ -102,11 +102,7 @@ __device__ void soccer_obs(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& 
       int c = k < 2 ? lastR : lastL;
       T f = 0;
       if (c >= 0) {
-        if ((k & 1) == 0) f = e.con_dist[c];
-        else {
-          const T* fr = m.pair_friction + 5 * e.con_pair[c];
-          f = sqrt(fr[0] * fr[0] + fr[1] * fr[1]);
-        }
+        f = (k & 1) == 0 ? e.con_dist[c] : e.con_mu[c];
       }
       v = clip1(f / (T)1000);
     } else if (i < 76) {
@@ -150,9 +146,9 @@ __device__ bool soccer_upright(const Env<T>& e, const SoccerIds<T>& ids) {
 
 // Post-physics: step count, obs, reward, termination, stats, prev snapshots
 template <typename T>
-__device__ void soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
+__device__ bool soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
                             uint8_t* goal_scored, T* prev_ball, T* prev_robot, T* stats, float* obs, double* reward,
-                            uint8_t* terminated, uint8_t* truncated) {
+                            uint8_t* terminated, uint8_t* truncated, uint8_t* flags = nullptr) {
   int l = lane_id();
   int st = *step + 1;
   soccer_obs(m, e, ids, st, obs);
@@ -204,8 +200,46 @@ __device__ void soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>&
     *truncated = trunc;
     *goal_scored = gs;
     *step = st;
+    if (flags) { flags[0] = ball_contact; flags[1] = upright; }
   }
   if (l < 3) { prev_ball[l] = bp[l]; prev_robot[l] = tx[l]; }
+  return term || trunc;
+}
+
+// Counter-based reset draws for the vector env: Philox4x32-10 keyed by (seed, global env
+// index), counter = (episode, word). Independent of how envs are sharded over GPUs.
+__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+// the reference's ranges, in draw order (soccer_env.py:458-504)
+__device__ __forceinline__ void soccer_draw_ranges(int j, int n_noise, double* lo, double* hi) {
+  if (j == 0) { *lo = -15; *hi = -5; }
+  else if (j == 1) { *lo = -10; *hi = 10; }
+  else if (j == 2) { *lo = -0.5; *hi = 0.5; }
+  else if (j < 3 + n_noise) { *lo = -0.1; *hi = 0.1; }
+  else if (j == 3 + n_noise) { *lo = -2; *hi = 2; }
+  else if (j == 4 + n_noise) { *lo = 0; *hi = 2; }
+  else if (j == 5 + n_noise) { *lo = 0; *hi = 6.283185307179586; }
+  else { *lo = 0.05; *hi = 0.15; }
+}
+// lane j < 36 produces draw j of episode `episode` for global env `genv` into `out` (LDS/global)
+template <typename T>
+__device__ void soccer_philox_draws(uint64_t seed, uint32_t genv, uint32_t episode, int n_noise, T* out) {
+  int j = lane_id();
+  if (j < 36) {
+    uint32_t c[4] = {episode, (uint32_t)j, 0x50C3Eu, 0u};
+    philox4x32(c, (uint32_t)seed ^ genv, (uint32_t)(seed >> 32));
+    double u = ((double)(c[0] >> 5) * 67108864.0 + (double)(c[1] >> 6)) * (1.0 / 9007199254740992.0);
+    double lo, hi;
+    soccer_draw_ranges(j, n_noise, &lo, &hi);
+    out[j] = (T)(lo + (hi - lo) * u);
+  }
 }
 
 // Reset: mj_resetData + the reference's randomisation (draws in reference order), with the

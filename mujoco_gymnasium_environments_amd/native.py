@@ -61,9 +61,10 @@ _SIGS = {
     "mgx_soccer_configure": ([_VP, C.POINTER(cabi.MgxSoccerIds)], C.c_int),
     "mgx_soccer_configure_reset": ([_VP, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double)], C.c_int),
     "mgx_soccer_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, _VP, _VP, _VP,
-                         C.c_int, _VP, _VP], C.c_int),
-    "mgx_soccer_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, C.c_int, _VP, _VP],
-                         C.c_int),
+                         _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_soccer_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, C.c_uint64,
+                          C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_soccer_logic_test": ([_VP, C.POINTER(cabi.MgxSoccerLogicIO), C.c_int, _VP], C.c_int),
 }
 EXPORTS = tuple(_SIGS)
 
