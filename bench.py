@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env steps/sec (whole node), humanoid_soccer, 4096 envs per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One "step" = one SoccerVectorEnv.step over all envs of a rank: action clip, goalkeeper, wind,
+mj_step (kinematics .. PGS .. Euler) and observation/reward/termination for every env, with
+same-step autoreset — one fused HIP kernel launch (mgx_soccer_step). Actions are synthetic
+U(-150, 150)^33 float32 drawn before the timed region and resident in HBM.
+Ranks shard envs (global index = rank * envs + i); the only collective is the end-of-rollout
+metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+# algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
+# qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
+# scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
+ALG_BYTES_PER_ENV_STEP = 4 * (2 * 121 + 33 + 2 * 3 + 2 * 11 + 80) + 8 + 2
+
+
+def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
+    """Oracle port on one host core: mjref (C, fp64) physics + numpy env logic."""
+    from mujoco_gymnasium_environments_amd import cabi
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerTables, soccer_model
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.mjref import RefSim
+    from oracle.soccer_logic import SoccerLogic
+    m = soccer_model()
+    pk = cabi.pack_model(m)
+    tb = SoccerTables(m)
+    L = SoccerLogic(tb)
+    rng = np.random.default_rng(seed)
+    acts = rng.uniform(-150, 150, (64, m.nu)).astype(np.float32)
+    total = 0
+    t0 = time.perf_counter()
+    for e in range(n_envs):
+        sim = RefSim(pk)
+        draws = tb.reset_draws(np_random(seed + e)[0])
+
+        def reset():
+            sim.reset()
+            q = sim.qpos
+            a0 = tb.root_qposadr
+            q[a0:a0 + 3] = [draws[0], draws[1], 1.4]
+            q[a0 + 3:a0 + 7] = [np.cos(draws[2] / 2), 0, 0, np.sin(draws[2] / 2)]
+            q[tb.ball_qposadr:tb.ball_qposadr + 3] = [draws[0] + 2, draws[1], 0.15]
+            for k, j in enumerate(tb.noise_joints):
+                lo, hi = m.jnt_range[j]
+                q[m.jnt_qposadr[j]] = np.clip((lo + hi) / 2 + draws[3 + k], lo, hi)
+            q[tb.gk_qposadr] = draws[3 + len(tb.noise_joints)]
+            sim.step(10)
+        reset()
+        nn = len(tb.noise_joints)
+        s = dict(wind_strength=draws[4 + nn], wind_direction=np.array([np.cos(draws[5 + nn]), np.sin(draws[5 + nn])]),
+                 goal_scored=False, stats=np.zeros(5))
+
+        def view():
+            c = sim.contacts()
+            s.update(qpos=sim.qpos, qvel=sim.qvel, xpos=sim.xpos.reshape(-1, 3), xquat=sim.xquat.reshape(-1, 4),
+                     subtree_com=sim.subtree_com.reshape(-1, 3), con_geom=c["geom"], con_dist=c["dist"],
+                     con_mu=np.array([np.linalg.norm(m.pair_friction[p][:2]) for p in c["pair"]]), ctrl=sim.ctrl,
+                     qfrc_applied=sim.qfrc_applied, xfrc_applied=sim.xfrc_applied.reshape(-1, 6))
+        view()
+        s["prev_ball_pos"], s["prev_robot_pos"] = s["xpos"][tb.ball].copy(), s["xpos"][tb.torso].copy()
+        step = 0
+        for k in range(n_steps):
+            a = L.pre(s, acts[k % 64])
+            sim.step()
+            view()
+            step += 1
+            _, _, term, trunc, _, _ = L.post(s, a, step)
+            total += 1
+            if term or trunc:
+                reset()
+                view()
+                s.update(goal_scored=False, stats=np.zeros(5), prev_ball_pos=s["xpos"][tb.ball].copy(),
+                         prev_robot_pos=s["xpos"][tb.torso].copy())
+                step = 0
+    dt = time.perf_counter() - t0
+    return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of humanoid_soccer, U(-150,150) actions, "
+                      f"oracle/mjref.c fp64 physics + oracle/soccer_logic.py; CPU MuJoCo unavailable (not installed)",
+            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--cpu-envs", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=800)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    N = args.envs
+    env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=rank * N)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]
+    env.reset()
+    for k in range(args.warmup):
+        env.step(pool[k % len(pool)])
+    torch.cuda.synchronize(dev)
+    # metric accumulators live on device; read once after the timed region
+    acc = torch.zeros(6, dtype=torch.float64, device=dev)  # env_steps, episodes, reward, term, trunc, bad
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        obs, rew, term, trunc, _ = env.step(pool[k % len(pool)])
+        ev[k][1].record()
+        acc[2] += rew.sum()
+        acc[3] += term.sum()
+        acc[4] += trunc.sum()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    acc[0] = float(N * args.steps)
+    acc[1] = float(env.episode.sum().item())
+    acc[5] = float(env.batch.warning.sum().item())
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(acc)                                # end-of-rollout metric all-reduce (RCCL)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_steps = acc[0].item()
+    value = total_steps / elapsed
+    if rank == 0:
+        bytes_per_launch = ALG_BYTES_PER_ENV_STEP * N
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "r01_pmc.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    p = json.load(f)
+                if p.get("envs") == N and p.get("precision") == args.precision:
+                    traffic = p.get("hbm_bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                traffic = None
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (U(-150,150) actions, Philox reset draws)",
+            "config": {"workload": "humanoid_soccer_env, 4096 envs/GPU (BASELINE configs[2])",
+                       "envs_per_gpu": N, "global_batch": N * world, "parallelism": f"dp{world} (env shards)",
+                       "autoreset": "same-step", "episodes_total": int(acc[1].item()),
+                       "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "mean_reward": round(acc[2].item() / total_steps, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_soccer<float,0> (mgx_soccer_step)",
+                         "alg_bytes_per_launch": bytes_per_launch, "launch_ms": round(launch_ms, 4)},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_steps)
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

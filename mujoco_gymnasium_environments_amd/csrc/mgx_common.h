@@ -68,6 +68,25 @@ struct DevModel {
   Layout L;
 };
 
+// ------------------------------------------------------------------ diagnostic stamps
+// Built only with -DMGX_PROFILE (libmgx_prof.so, never the shipped library): per-env cycle
+// sums per stage, read back by tools/stage_profile.py. Stamps never feed any output.
+#ifdef MGX_PROFILE
+extern __device__ unsigned long long* g_mgx_prof;
+#define MGX_STAMP_DECL unsigned long long _mgx_t0 = __builtin_amdgcn_s_memtime();
+#define MGX_STAMP(slot)                                                                 \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                               \
+    if (g_mgx_prof && threadIdx.x == 0) g_mgx_prof[blockIdx.x * 32 + (slot)] += _t - _mgx_t0; \
+    _mgx_t0 = _t;                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+  } while (0)
+#else
+#define MGX_STAMP_DECL
+#define MGX_STAMP(slot) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------ wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 __device__ __forceinline__ void wsync() { __syncthreads(); }

@@ -864,18 +864,28 @@ __device__ void euler(const DevModel<T>& m, Env<T>& e) {
 // ---------------------------------------------------------------- forward + step
 template <typename T>
 __device__ void forward(const DevModel<T>& m, Env<T>& e) {
+  MGX_STAMP_DECL
   kinematics(m, e);
+  MGX_STAMP(0);
   com_crb(m, e);
+  MGX_STAMP(1);
   e.diaginv = factor_ld(m, e.qLD);
+  MGX_STAMP(2);
   collision(m, e);
+  MGX_STAMP(3);
   make_constraint(m, e);
+  MGX_STAMP(4);
   // D^-1/2 per dof for the row transform
   if (lane_id() < m.nv) e.vec0[lane_id()] = sqrt(e.diaginv);
   wsync();
   transform_rows(m, e);
+  MGX_STAMP(5);
   velocity(m, e);
+  MGX_STAMP(6);
   e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
+  MGX_STAMP(7);
   pgs(m, e);
+  MGX_STAMP(8);
 }
 
 // returns the number of bad-state resets performed (0..3)
@@ -891,7 +901,9 @@ __device__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
     forward(m, e);
   }
   e.qacc_ws = e.qacc;
+  MGX_STAMP_DECL
   euler(m, e);
+  MGX_STAMP(9);
   return warn;
 }
 
