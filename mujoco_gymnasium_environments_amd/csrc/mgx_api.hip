@@ -136,22 +136,29 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   wsync();
   e.diaginv = factor_ld(m, e.qLD);
   for (int k = l; k < m.nM; k += 64) D[o.qLD + k] = e.qLD[k];
+  velocity(m, e);
+  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
   collision(m, e);
+  wsync();
+  for (int k = l; k < 3 * m.nbody; k += 64) D[o.xipos + k] = e.xipos[k];
+  for (int k = l; k < 10 * m.nbody; k += 64) D[o.cinert + k] = e.cinert[k];
+  for (int k = l; k < 6 * m.nv; k += 64) D[o.cdof_dot + k] = e.cdof_dot[k];
+  for (int k = l; k < 6 * m.nbody; k += 64) D[o.cvel + k] = e.cvel[k];
+  for (int k = l; k < 3 * m.ngeom; k += 64) D[o.geom_xpos + k] = e.geom_xpos[k];
+  for (int k = l; k < 9 * m.ngeom; k += 64) D[o.geom_xmat + k] = e.geom_xmat[k];
+  wsync();
   make_constraint(m, e);
   if (l < m.nv) e.vec0[l] = sqrt(e.diaginv);
   wsync();
   transform_rows(m, e);
-  velocity(m, e);
-  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
+  wsync();
+  for (int r = l; r < e.nefc; r += 64)
+    for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];
   pgs(m, e);
   wsync();
-  for (int k = l; k < 3 * m.nbody; k += 64) { D[o.xpos + k] = e.xpos[k]; D[o.xipos + k] = e.xipos[k]; D[o.subtree_com + k] = e.subtree_com[k]; }
+  for (int k = l; k < 3 * m.nbody; k += 64) { D[o.xpos + k] = e.xpos[k]; D[o.subtree_com + k] = e.subtree_com[k]; }
   for (int k = l; k < 4 * m.nbody; k += 64) D[o.xquat + k] = e.xquat[k];
-  for (int k = l; k < 10 * m.nbody; k += 64) D[o.cinert + k] = e.cinert[k];
-  for (int k = l; k < 6 * m.nv; k += 64) { D[o.cdof + k] = e.cdof[k]; D[o.cdof_dot + k] = e.cdof_dot[k]; }
-  for (int k = l; k < 6 * m.nbody; k += 64) D[o.cvel + k] = e.cvel[k];
-  for (int k = l; k < 3 * m.ngeom; k += 64) D[o.geom_xpos + k] = e.geom_xpos[k];
-  for (int k = l; k < 9 * m.ngeom; k += 64) D[o.geom_xmat + k] = e.geom_xmat[k];
+  for (int k = l; k < 6 * m.nv; k += 64) D[o.cdof + k] = e.cdof[k];
   if (l == 0) { D[o.ncon] = (T)e.ncon; D[o.nefc] = (T)e.nefc; D[o.niter] = (T)e.niter; }
   for (int c = l; c < e.ncon; c += 64) {
     D[o.con_dist + c] = e.con_dist[c];
@@ -161,10 +168,9 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
     D[o.con_geom + 2 * c + 1] = (T)e.con_geom[2 * c + 1];
   }
   for (int r = l; r < e.nefc; r += 64) {
-    D[o.efc_type + r] = (T)e.efc_type[r]; D[o.efc_id + r] = (T)e.efc_id[r]; D[o.efc_pos + r] = e.efc_pos[r];
-    D[o.efc_margin + r] = e.efc_margin[r]; D[o.efc_R + r] = e.efc_R[r]; D[o.efc_aref + r] = e.efc_aref[r];
-    D[o.efc_force + r] = e.efc_f[r];
-    for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];
+    D[o.efc_type + r] = (T)e.efc_type[r]; D[o.efc_id + r] = (T)e.efc_id[r]; D[o.efc_pos + r] = e.efc[8 * r + 7];
+    D[o.efc_margin + r] = e.efc_margin[r]; D[o.efc_R + r] = e.efc[8 * r + 2]; D[o.efc_aref + r] = e.efc[8 * r + 5];
+    D[o.efc_force + r] = e.efc[8 * r + 1];
   }
   if (l < m.nv) {
     D[o.qfrc_smooth + l] = e.qfrc_smooth; D[o.qacc_smooth + l] = e.qacc_smooth; D[o.qacc + l] = e.qacc;
@@ -175,7 +181,7 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
 // soccer reset body shared by the explicit-reset and autoreset paths: draws (36 values in
 // reference order, from the host or from Philox) -> randomised qpos, 10 settle mj_steps, obs.
 template <typename T>
-__device__ int soccer_reset_body(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const T* draws, T* wind,
+__device__ __forceinline__ int soccer_reset_body(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const T* draws, T* wind,
                                  T* prev_ball, T* prev_robot, T* stats, int* step, uint8_t* goal, float* obs) {
   soccer_apply_reset(m, e, ids, draws, wind);
   int warn = 0;
@@ -295,19 +301,24 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   auto take = [&](int n) { int r = p; p = align_up(p + (n > 0 ? n : 1), al); return r; };
   int nb = d->nbody, nv = d->nv, nj = d->njnt, ng = d->ngeom;
   L.max_ncon = max_ncon; L.max_nefc = max_nefc; L.max_active = max_active;
+  // persistent for the whole step (state, frames read by env logic, factors, contacts, rows)
   L.qpos = take(d->nq); L.qvel = take(nv); L.ctrl = take(d->nu); L.xfrc = take(6 * nb);
-  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
-  L.ximat = take(9 * nb); L.subtree_com = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb);
-  L.cvel = take(6 * nb); L.cfrc = take(6 * nb); L.xaxis = take(3 * nj); L.xanchor = take(3 * nj);
-  L.cdof = take(6 * nv); L.cdof_dot = take(6 * nv); L.qLD = take(d->nM); L.qMH = take(d->nM);
-  L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
-  L.act_force = take(d->nu); L.con_dist = take(max_ncon); L.con_pos = take(3 * max_ncon);
-  L.con_frame = take(9 * max_ncon); L.con_mu = take(max_ncon); L.efc_pos = take(max_nefc); L.efc_margin = take(max_nefc);
-  L.efc_diag = take(max_nefc); L.efc_K = take(max_nefc); L.efc_B = take(max_nefc); L.efc_imp = take(max_nefc);
-  L.efc_R = take(max_nefc); L.efc_aref = take(max_nefc); L.efc_b = take(max_nefc); L.efc_f = take(max_nefc);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb); L.cdof = take(6 * nv);
+  L.qLD = take(d->nM); L.qMH = take(d->nM); L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64);
+  L.con_dist = take(max_ncon); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
+  L.con_mu = take(max_ncon);
+  L.efc = take(8 * max_nefc); L.efc_margin = take(max_nefc);
+  // union: phase A (kinematics .. collision) arrays, then the B matrix of phase B on top
+  int u0 = p;
+  L.xmat = take(9 * nb); L.xipos = take(3 * nb); L.ximat = take(9 * nb); L.cinert = take(10 * nb);
+  L.crb = take(10 * nb); L.cvel = take(6 * nb); L.cfrc = take(6 * nb); L.cdof_dot = take(6 * nv);
+  L.xaxis = take(3 * nj); L.xanchor = take(3 * nj); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
+  L.act_force = take(d->nu);
+  int endA = p;
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
-  L.Bmat = take(max_nefc * L.Bstride);
-  L.reals = p;
+  L.Bmat = u0;
+  int endB = align_up(u0 + max_nefc * L.Bstride, al);
+  L.reals = endA > endB ? endA : endB;
   int q = 0;
   auto takei = [&](int n) { int r = q; q = align_up(q + (n > 0 ? n : 1), 4); return r; };
   L.con_geom = takei(2 * max_ncon); L.con_pair = takei(max_ncon); L.act_list = takei(max_active);

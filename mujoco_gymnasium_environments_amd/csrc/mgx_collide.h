@@ -32,7 +32,7 @@ __device__ __forceinline__ void seg_ends(const T* pos, const T* mat, T hl, T* a,
 }
 
 template <typename T>
-__device__ void seg_seg(const T* p1, const T* q1, const T* p2, const T* q2, T* s, T* t) {
+__device__ __forceinline__ void seg_seg(const T* p1, const T* q1, const T* p2, const T* q2, T* s, T* t) {
   T d1[3], d2[3], r[3];
   for (int k = 0; k < 3; k++) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
   T a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
@@ -74,7 +74,7 @@ __device__ __forceinline__ T box_sd(const T* p, const T* h, T* e) {
 }
 
 template <typename T>
-__device__ int sphere_box_core(const T* c, T r, const T* bp, const T* bm, const T* h, T margin, Con<T>* out) {
+__device__ __forceinline__ int sphere_box_core(const T* c, T r, const T* bp, const T* bm, const T* h, T margin, Con<T>* out) {
   T tmp[3] = {c[0] - bp[0], c[1] - bp[1], c[2] - bp[2]}, pl[3], e[3], ew[3];
   mulmatTvec3(pl, bm, tmp);
   T sd = box_sd(pl, h, e);
@@ -87,7 +87,7 @@ __device__ int sphere_box_core(const T* c, T r, const T* bp, const T* bm, const 
 }
 
 template <typename T>
-__device__ int capsule_box(const T* cp, const T* cm, const T* cs, const T* bp, const T* bm, const T* h, T margin,
+__device__ __forceinline__ int capsule_box(const T* cp, const T* cm, const T* cs, const T* bp, const T* bm, const T* h, T margin,
                            Con<T>* out) {
   T a[3], b[3], al[3], bl[3], tmp[3], e[3], p[3];
   T r = cs[0];
@@ -130,7 +130,7 @@ __device__ int capsule_box(const T* cp, const T* cm, const T* cs, const T* bp, c
 }
 
 template <typename T>
-__device__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T (*out)[2]) {
+__device__ __forceinline__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T (*out)[2]) {
   int m = 0;
   for (int i = 0; i < n; i++) {
     T* P = in[i];
@@ -148,7 +148,7 @@ __device__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T (*out)[2])
 }
 
 template <typename T>
-__device__ int box_box(const T* pa, const T* Ra, const T* ha, const T* pb, const T* Rb, const T* hb, T margin,
+__device__ __forceinline__ int box_box(const T* pa, const T* Ra, const T* ha, const T* pb, const T* Rb, const T* hb, T margin,
                        Con<T>* out) {
   T d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
   T A[3][3], B[3][3];
@@ -265,7 +265,7 @@ __device__ __forceinline__ int plane_sphere(const T* pp, const T* pm, const T* c
 }
 
 template <typename T>
-__device__ int plane_box(const T* pp, const T* pm, const T* bp, const T* bm, const T* h, T margin, Con<T>* out) {
+__device__ __forceinline__ int plane_box(const T* pp, const T* pm, const T* bp, const T* bm, const T* h, T margin, Con<T>* out) {
   T n[3] = {pm[2], pm[5], pm[8]};
   int cnt = 0;
   for (int c = 0; c < 8 && cnt < 4; c++) {
@@ -284,7 +284,7 @@ __device__ int plane_box(const T* pp, const T* pm, const T* bp, const T* bm, con
 
 // Dispatch one candidate pair. Geom frames come from LDS.
 template <typename T>
-__device__ int collide_pair(int t1, int t2, const T* p1, const T* m1, const T* s1, const T* p2, const T* m2,
+__device__ __forceinline__ int collide_pair(int t1, int t2, const T* p1, const T* m1, const T* s1, const T* p2, const T* m2,
                             const T* s2, T margin, Con<T>* out) {
   if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph(p1, s1[0], p2, s2[0], margin, out);
   if (t1 == GSPHERE && t2 == GCAPSULE) {

@@ -27,7 +27,7 @@ struct Layout {
   int qpos, qvel, ctrl, xfrc, xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cfrc;
   int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, geom_xpos, geom_xmat, act_force;
   int con_dist, con_pos, con_frame, con_mu;
-  int efc_pos, efc_margin, efc_diag, efc_K, efc_B, efc_imp, efc_R, efc_aref, efc_b, efc_f;
+  int efc, efc_margin;
   int Bmat, Bstride;
   int reals;  // total reals
   // int region (after reals)
@@ -124,6 +124,23 @@ __device__ __forceinline__ float wave_sum_dpp(float x) {
 }
 __device__ __forceinline__ double wave_sum_dpp(double x) { return wave_sum(x); }
 
+// full-wave sum, 6 DPP steps + one readlane: quad_perm x2, row_half_mirror, row_mirror (row
+// totals in every lane), row_bcast:15 / row_bcast:31 (gfx9 DPP) -> total in lane 63
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_upd(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum_fast(float x) {
+  x += dpp_f<0xB1>(x);
+  x += dpp_f<0x4E>(x);
+  x += dpp_f<0x141>(x);
+  x += dpp_f<0x140>(x);
+  x += dpp_upd<0x142, 0xa>(x);
+  x += dpp_upd<0x143, 0xc>(x);
+  return readlane(x, 63);
+}
+__device__ __forceinline__ double wave_sum_fast(double x) { return wave_sum(x); }
+
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int prefix_count(unsigned long long mask) {  // set bits below this lane
   return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
@@ -138,7 +155,7 @@ __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
     int y = __shfl_up(x, o);
     if (lane_id() >= o) x += y;
   }
-  *total = __shfl(x, 63);
+  *total = __builtin_amdgcn_readfirstlane(__shfl(x, 63));  // uniform
   return x - v;
 }
 

@@ -21,7 +21,10 @@ struct Env {
   T *qpos, *qvel, *ctrl, *xfrc, *xpos, *xquat, *xmat, *xipos, *ximat, *subtree_com, *cinert, *crb, *cvel, *cfrc;
   T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *geom_xpos, *geom_xmat, *act_force;
   T *con_dist, *con_pos, *con_frame, *con_mu;  // con_mu = |friction[0:2]| (soccer obs)
-  T *efc_pos, *efc_margin, *efc_diag, *efc_K, *efc_B, *efc_imp, *efc_R, *efc_aref, *efc_b, *efc_f;
+  // per-row constraint data, AoS with stride 8 so the solver fetches a row's scalars with one
+  // 16-byte LDS read: [0] b, [1] f, [2] R (diagApprox until impedance), [3] 1/AR_rr,
+  // [4] AR_rr, [5] aref (K*imp*(pos-margin) until the solver), [6] B damping, [7] pos
+  T *efc, *efc_margin;
   T *Bm;
   int Bs;
   int *con_geom, *con_pair, *act_list, *efc_type, *efc_id;
@@ -33,7 +36,7 @@ struct Env {
 };
 
 template <typename T>
-__device__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
+__device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
   T* R = reinterpret_cast<T*>(smem);
   const Layout& L = m.L;
   e.qpos = R + L.qpos; e.qvel = R + L.qvel; e.ctrl = R + L.ctrl; e.xfrc = R + L.xfrc;
@@ -43,10 +46,8 @@ __device__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
   e.cdof = R + L.cdof; e.cdof_dot = R + L.cdof_dot; e.qLD = R + L.qLD; e.qMH = R + L.qMH;
   e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.geom_xpos = R + L.geom_xpos;
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.con_dist = R + L.con_dist;
-  e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc_pos = R + L.efc_pos;
-  e.efc_margin = R + L.efc_margin; e.efc_diag = R + L.efc_diag; e.efc_K = R + L.efc_K;
-  e.efc_B = R + L.efc_B; e.efc_imp = R + L.efc_imp; e.efc_R = R + L.efc_R; e.efc_aref = R + L.efc_aref;
-  e.efc_b = R + L.efc_b; e.efc_f = R + L.efc_f; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
+  e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
+  e.efc_margin = R + L.efc_margin; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
   int* I = reinterpret_cast<int*>(R + L.reals);
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
   e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id;
@@ -58,7 +59,7 @@ __device__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
 
 // ---------------------------------------------------------------- state load / store / reset
 template <typename T>
-__device__ void load_state(const DevModel<T>& m, Env<T>& e, const T* gqpos, const T* gqvel, const T* gqacc,
+__device__ __forceinline__ void load_state(const DevModel<T>& m, Env<T>& e, const T* gqpos, const T* gqvel, const T* gqacc,
                            const T* gctrl, const T* gqfrc, const T* gxfrc, const T* gtime, int env) {
   int l = lane_id();
   for (int k = l; k < m.nq; k += 64) e.qpos[k] = gqpos[(size_t)env * m.nq + k];
@@ -72,7 +73,7 @@ __device__ void load_state(const DevModel<T>& m, Env<T>& e, const T* gqpos, cons
 }
 
 template <typename T>
-__device__ void store_state(const DevModel<T>& m, Env<T>& e, T* gqpos, T* gqvel, T* gqacc, T* gctrl, T* gqfrc,
+__device__ __forceinline__ void store_state(const DevModel<T>& m, Env<T>& e, T* gqpos, T* gqvel, T* gqacc, T* gctrl, T* gqfrc,
                             T* gxfrc, T* gtime, int env) {
   wsync();
   int l = lane_id();
@@ -86,7 +87,7 @@ __device__ void store_state(const DevModel<T>& m, Env<T>& e, T* gqpos, T* gqvel,
 
 // mj_resetData on the LDS copy (soccer_env.py:354 reaches it; also the bad-state reset)
 template <typename T>
-__device__ void reset_env(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void reset_env(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   wsync();
   for (int k = l; k < m.nq; k += 64) e.qpos[k] = m.qpos0[k];
@@ -100,7 +101,7 @@ __device__ void reset_env(const DevModel<T>& m, Env<T>& e) {
 }
 
 template <typename T>
-__device__ bool any_bad(const T* x, int n) {
+__device__ __forceinline__ bool any_bad(const T* x, int n) {
   bool b = false;
   for (int k = lane_id(); k < n; k += 64) b |= isbad(x[k]);
   return ballot(b) != 0ull;
@@ -109,7 +110,7 @@ __device__ bool any_bad(const T* x, int n) {
 // ---------------------------------------------------------------- kinematics (mj_kinematics)
 // Lane b recomputes the chain root..b, so no level-by-level barriers are needed.
 template <typename T>
-__device__ void body_pose_step(const DevModel<T>& m, Env<T>& e, int i, T* pos, T* quat, T* mat, bool store_joints) {
+__device__ __forceinline__ void body_pose_step(const DevModel<T>& m, Env<T>& e, int i, T* pos, T* quat, T* mat, bool store_joints) {
   int ja = m.body_jntadr[i], jn = m.body_jntnum[i];
   if (jn == 1 && m.jnt_type[ja] == JFREE) {
     int a = m.jnt_qposadr[ja];
@@ -152,7 +153,7 @@ __device__ void body_pose_step(const DevModel<T>& m, Env<T>& e, int i, T* pos, T
 }
 
 template <typename T>
-__device__ void kinematics(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void kinematics(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   for (int b = l; b < m.nbody; b += 64) {
     T pos[3] = {0, 0, 0}, quat[4] = {1, 0, 0, 0}, mat[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
@@ -185,7 +186,7 @@ __device__ void kinematics(const DevModel<T>& m, Env<T>& e) {
 
 // ---------------------------------------------------------------- comPos, CRB, M
 template <typename T>
-__device__ void inertcom(T* res, const T* inert, const T* mat, const T* dif, T mass) {
+__device__ __forceinline__ void inertcom(T* res, const T* inert, const T* mat, const T* dif, T mass) {
   T tmp[9] = {mat[0] * inert[0], mat[3] * inert[0], mat[6] * inert[0],
               mat[1] * inert[1], mat[4] * inert[1], mat[7] * inert[1],
               mat[2] * inert[2], mat[5] * inert[2], mat[8] * inert[2]};
@@ -206,7 +207,7 @@ __device__ void inertcom(T* res, const T* inert, const T* mat, const T* dif, T m
 }
 
 template <typename T>
-__device__ void com_crb(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void com_crb(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   // subtree com: lane b sums its DFS-contiguous subtree
   for (int b = l; b < m.nbody; b += 64) {
@@ -283,7 +284,7 @@ __device__ void com_crb(const DevModel<T>& m, Env<T>& e) {
 
 // mj_factorI on an LDS tree-sparse matrix: M = L' D L in place; returns diaginv in a register
 template <typename T>
-__device__ T factor_ld(const DevModel<T>& m, T* LD) {
+__device__ __forceinline__ T factor_ld(const DevModel<T>& m, T* LD) {
   int l = lane_id();
   for (int k = m.nv - 1; k >= 0; k--) {
     int akk = m.dof_Madr[k];
@@ -312,7 +313,7 @@ __device__ T factor_ld(const DevModel<T>& m, T* LD) {
 
 // x <- L'^-1 x (lane-distributed vector)
 template <typename T>
-__device__ T solve_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
+__device__ __forceinline__ T solve_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
   int l = lane_id();
   for (int k = m.nv - 1; k >= 0; k--) {
     T xk = readlane(x, k);
@@ -323,7 +324,7 @@ __device__ T solve_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
 }
 // x <- L^-1 x
 template <typename T>
-__device__ T solve_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
+__device__ __forceinline__ T solve_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
   int l = lane_id();
   int madr = l < m.nv ? m.dof_Madr[l] : 0;
   for (int i = 0; i < m.nv; i++) {
@@ -334,7 +335,7 @@ __device__ T solve_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
 }
 // y = L x
 template <typename T>
-__device__ T mul_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
+__device__ __forceinline__ T mul_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
   int l = lane_id();
   int madr = l < m.nv ? m.dof_Madr[l] : 0;
   T y = x;
@@ -346,7 +347,7 @@ __device__ T mul_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
 }
 // y = L' u
 template <typename T>
-__device__ T mul_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T u) {
+__device__ __forceinline__ T mul_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T u) {
   int l = lane_id();
   T y = u;
   for (int k = 0; k < m.nv; k++) {
@@ -358,7 +359,7 @@ __device__ T mul_LT(const DevModel<T>& m, const Env<T>& e, const T* LD, T u) {
 }
 // x = M^-1 y
 template <typename T>
-__device__ T solve_M(const DevModel<T>& m, const Env<T>& e, const T* LD, T diaginv, T y) {
+__device__ __forceinline__ T solve_M(const DevModel<T>& m, const Env<T>& e, const T* LD, T diaginv, T y) {
   T x = solve_LT(m, e, LD, y);
   x *= diaginv;
   return solve_L(m, e, LD, x);
@@ -366,7 +367,7 @@ __device__ T solve_M(const DevModel<T>& m, const Env<T>& e, const T* LD, T diagi
 
 // ---------------------------------------------------------------- collision (mj_collision)
 template <typename T>
-__device__ void collision(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void collision(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   const Layout& L = m.L;
   // broadphase: bounding spheres (planes always pass); compact survivors in pair order
@@ -425,7 +426,7 @@ __device__ void collision(const DevModel<T>& m, Env<T>& e) {
     ncon += total;
   }
   if (ncon > L.max_ncon) { ncon = L.max_ncon; e.overflow |= 2; }
-  e.ncon = ncon;
+  e.ncon = __builtin_amdgcn_readfirstlane(ncon);
   wsync();
 }
 
@@ -436,7 +437,7 @@ __device__ __forceinline__ bool body_has_dof(const DevModel<T>& m, int b, int d)
 }
 
 template <typename T>
-__device__ T impedance(const T* solimp, T pos, T margin) {
+__device__ __forceinline__ T impedance(const T* solimp, T pos, T margin) {
   T d0 = clampv(solimp[0], (T)0.0001, (T)0.9999), d1 = clampv(solimp[1], (T)0.0001, (T)0.9999);
   T width = solimp[2], mid = solimp[3], power = solimp[4];
   if (d0 == d1 || width <= minval<T>()) return (T)0.5 * (d0 + d1);
@@ -452,7 +453,7 @@ __device__ T impedance(const T* solimp, T pos, T margin) {
 
 // joint limits then pyramidal contacts; rows are written as J and transformed in place
 template <typename T>
-__device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   const Layout& L = m.L;
   int nefc = 0;
@@ -478,10 +479,10 @@ __device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
       if (!on) continue;
       if (r < L.max_nefc) {
         e.efc_type[r] = C_LIMIT_JOINT; e.efc_id[r] = j;
-        e.efc_pos[r] = side == 0 ? dl : du;
+        e.efc[8 * r + 7] = side == 0 ? dl : du;
         e.efc_margin[r] = m.jnt_margin[j];
-        e.efc_diag[r] = m.dof_invweight0[m.jnt_dofadr[j]];
-        e.efc_f[r] = side == 0 ? (T)1 : (T)-1;  // J entry, scattered below
+        e.efc[8 * r + 2] = m.dof_invweight0[m.jnt_dofadr[j]];
+        e.efc[8 * r + 1] = side == 0 ? (T)1 : (T)-1;  // J entry, scattered below
       }
       r++;
     }
@@ -493,7 +494,7 @@ __device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
   for (int r = l; r < nefc; r += 64) {
     T* row = e.Bm + r * e.Bs;
     for (int k = 0; k < m.nv; k++) row[k] = 0;
-    row[m.jnt_dofadr[e.efc_id[r]]] = e.efc_f[r];
+    row[m.jnt_dofadr[e.efc_id[r]]] = e.efc[8 * r + 1];
   }
   // ---- contacts: 2*(condim-1) pyramid rows (condim 3) or 1 row (condim 1); lane = dof
   for (int c = 0; c < e.ncon; c++) {
@@ -540,13 +541,13 @@ __device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
       T f = dim == 1 ? (T)0 : m.pair_friction[5 * p + (l >> 1)];
       e.efc_type[r] = dim == 1 ? C_CONTACT_FRICTIONLESS : C_CONTACT_PYRAMIDAL;
       e.efc_id[r] = c;
-      e.efc_pos[r] = e.con_dist[c];
+      e.efc[8 * r + 7] = e.con_dist[c];
       e.efc_margin[r] = m.pair_margin[p] - m.pair_gap[p];
-      e.efc_diag[r] = tran + f * f * tran;
+      e.efc[8 * r + 2] = tran + f * f * tran;
     }
     nefc += nrow;
   }
-  e.nefc = nefc;
+  e.nefc = __builtin_amdgcn_readfirstlane(nefc);
   wsync();
   // impedance, K, B, R per row (lane per row)
   for (int r = l; r < nefc; r += 64) {
@@ -559,7 +560,8 @@ __device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
       solref = m.pair_solref + 2 * p;
       solimp = m.pair_solimp + 5 * p;
     }
-    T imp = impedance(solimp, e.efc_pos[r], e.efc_margin[r]);
+    T pos = e.efc[8 * r + 7];
+    T imp = impedance(solimp, pos, e.efc_margin[r]);
     T dmax = clampv(solimp[1], (T)0.0001, (T)0.9999), K, B;
     if (solref[0] > 0) {
       T tc = solref[0], dr = solref[1];
@@ -570,16 +572,17 @@ __device__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
       K = -solref[0] / (dmax * dmax);
       B = -solref[1] / dmax;
     }
-    T R = ((T)1 - imp) * e.efc_diag[r] / imp;
-    e.efc_K[r] = K; e.efc_B[r] = B; e.efc_imp[r] = imp;
-    e.efc_R[r] = R > minval<T>() ? R : minval<T>();
+    T R = ((T)1 - imp) * e.efc[8 * r + 2] / imp;
+    e.efc[8 * r + 6] = B;
+    e.efc[8 * r + 5] = K * imp * (pos - e.efc_margin[r]);
+    e.efc[8 * r + 2] = R > minval<T>() ? R : minval<T>();
   }
   wsync();
 }
 
 // B_r = D^-1/2 L'^-1 J_r' in place (lane per row), sqrtdi in vec0
 template <typename T>
-__device__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   for (int r = l; r < e.nefc; r += 64) {
     T* x = e.Bm + r * e.Bs;
@@ -596,7 +599,7 @@ __device__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
 
 // ---------------------------------------------------------------- velocity stage
 template <typename T>
-__device__ void velocity(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void velocity(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   // comVel: lane b walks its chain; cdof_dot for the body's own dofs
   for (int b = l; b < m.nbody; b += 64) {
@@ -708,11 +711,17 @@ __device__ void velocity(const DevModel<T>& m, Env<T>& e) {
 }
 
 // ---------------------------------------------------------------- constraint solver (PGS)
+// mj_fwdConstraint + mj_solPGS [ext]. Rows are swept in order (Gauss-Seidel, MuJoCo's order);
+// per row: one LDS read of B_r (lane = dof), one wave reduction for B_r.v, scalar update,
+// v += delta * B_r. Row scalars live in LDS and the next row is prefetched while the current
+// reduction runs; 1/AR_rr is precomputed so the sweep has no division.
 template <typename T>
-__device__ void pgs(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
-  int ne = e.nefc;
-  T sqrtD = l < m.nv ? sqrt(e.qLD[m.dof_Madr[l]]) : (T)0;
+  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);  // uniform: keeps the sweep a scalar loop
+  const int nv = m.nv;
+  const bool dl = l < nv;
+  T sqrtD = dl ? sqrt(e.qLD[m.dof_Madr[l]]) : (T)0;
   if (ne == 0) {
     e.qacc = e.qacc_smooth;
     e.qfrc_constraint = 0;
@@ -720,102 +729,97 @@ __device__ void pgs(const DevModel<T>& m, Env<T>& e) {
     return;
   }
   // w vectors: D^1/2 L x for qvel, qacc_smooth, qacc_warmstart -> vec0 / vec1 / vec2
-  T qv = l < m.nv ? e.qvel[l] : (T)0;
+  T qv = dl ? e.qvel[l] : (T)0;
   T wv = sqrtD * mul_L(m, e, e.qLD, qv);
   T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
   T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
   wsync();
-  if (l < m.nv) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww; }
+  if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww; }
   wsync();
-  // per-row: vel, aref, b, warmstart force, AR diag (lane per row; registers by slot)
-  T f[MGX_EFC_SLOTS], bb[MGX_EFC_SLOTS], RR[MGX_EFC_SLOTS], AD[MGX_EFC_SLOTS];
-#pragma unroll
-  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
-    int r = s * 64 + l;
-    f[s] = 0; bb[s] = 0; RR[s] = 0; AD[s] = 1;
-    if (r < ne) {
-      const T* row = e.Bm + r * e.Bs;
-      T dv = 0, ds = 0, dw = 0, nn = 0;
-      for (int k = 0; k < m.nv; k++) {
-        T x = row[k];
-        dv += x * e.vec0[k]; ds += x * e.vec1[k]; dw += x * e.vec2[k]; nn += x * x;
-      }
-      T aref = -e.efc_B[r] * dv - e.efc_K[r] * e.efc_imp[r] * (e.efc_pos[r] - e.efc_margin[r]);
-      e.efc_aref[r] = aref;
-      bb[s] = ds - aref;
-      RR[s] = e.efc_R[r];
-      AD[s] = nn + RR[s];
-      T jar = dw - aref;
-      f[s] = jar < 0 ? -jar / RR[s] : (T)0;
+  T* efc = e.efc;
+  const T* Bm = e.Bm;
+  const int Bs = e.Bs;
+  // per row (lane per row): efc_vel -> aref (mj_referenceConstraint), b = J qacc_smooth - aref,
+  // warmstart force from qacc_warmstart (mj_constraintUpdate), 1/AR_rr and AR_rr
+  for (int r = l; r < ne; r += 64) {
+    const T* row = Bm + r * Bs;
+    T dv = 0, ds = 0, dw = 0, nn = 0;
+    for (int k = 0; k < nv; k++) {
+      T x = row[k];
+      dv += x * e.vec0[k]; ds += x * e.vec1[k]; dw += x * e.vec2[k]; nn += x * x;
     }
+    T* q = efc + 8 * r;
+    T aref = -q[6] * dv - q[5];
+    q[5] = aref;
+    q[0] = ds - aref;
+    T Rr = q[2];
+    T jar = dw - aref;
+    q[1] = jar < 0 ? -jar / Rr : (T)0;
+    T ad = nn + Rr;
+    q[4] = ad;
+    q[3] = (T)1 / ad;
   }
-  // v = B' f (lane = dof) and warmstart cost
+  wsync();
+  // v = B' f (lane = dof), then the warmstart dual cost
+  const int lc = dl ? l : 0;  // clamped column: every lane reads a valid address
   T v = 0;
-#pragma unroll
-  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
-    int cnt = ne - s * 64;
-    if (cnt > 64) cnt = 64;
-    for (int rl = 0; rl < cnt; rl++) {
-      T fr = readlane(f[s], rl);
-      if (l < m.nv) v += fr * e.Bm[(s * 64 + rl) * e.Bs + l];
-    }
+  for (int r = 0; r < ne; r++) {
+    T b = Bm[r * Bs + lc];
+    v += efc[8 * r + 1] * (dl ? b : (T)0);
   }
   wsync();
-  if (l < m.nv) e.vec0[l] = v;
+  if (dl) e.vec0[l] = v;
   wsync();
   T cpart = 0;
-#pragma unroll
-  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
-    int r = s * 64 + l;
-    if (r < ne) {
-      const T* row = e.Bm + r * e.Bs;
-      T bv = 0;
-      for (int k = 0; k < m.nv; k++) bv += row[k] * e.vec0[k];
-      cpart += f[s] * (bb[s] + (T)0.5 * (bv + RR[s] * f[s]));
-    }
+  for (int r = l; r < ne; r += 64) {
+    const T* row = Bm + r * Bs;
+    T bv = 0;
+    for (int k = 0; k < nv; k++) bv += row[k] * e.vec0[k];
+    const T* q = efc + 8 * r;
+    cpart += q[1] * (q[0] + (T)0.5 * (bv + q[2] * q[1]));
   }
   T cost = wave_sum(cpart);
   if (cost > 0) {
-#pragma unroll
-    for (int s = 0; s < MGX_EFC_SLOTS; s++) f[s] = 0;
+    for (int r = l; r < ne; r += 64) efc[8 * r + 1] = 0;
     v = 0;
   }
-  // Gauss-Seidel sweeps
-  T scale = (T)1 / (m.meaninertia * (T)(m.nv > 1 ? m.nv : 1));
+  wsync();
+  // Gauss-Seidel sweeps with early exit on scaled improvement < tolerance
+  const T scale = (T)1 / (m.meaninertia * (T)(nv > 1 ? nv : 1));
+  const T tol = m.tolerance;
+  const int maxit = m.iterations;
   int iter = 0;
-  while (iter < m.iterations) {
+  while (iter < maxit) {
     T improvement = 0;
-#pragma unroll
-    for (int s = 0; s < MGX_EFC_SLOTS; s++) {
-      int cnt = ne - s * 64;
-      if (cnt > 64) cnt = 64;
-      for (int rl = 0; rl < cnt; rl++) {
-        int r = s * 64 + rl;
-        T bv = l < m.nv ? e.Bm[r * e.Bs + l] : (T)0;
-        T dot = wave_sum_dpp(bv * v);
-        T fr = readlane(f[s], rl), br = readlane(bb[s], rl), Rr = readlane(RR[s], rl), Ar = readlane(AD[s], rl);
-        T res = br + dot + Rr * fr;
-        T fn = fr - res / Ar;
-        if (fn < 0) fn = 0;
-        T delta = fn - fr;
-        T change = (T)0.5 * delta * delta * Ar + delta * res;
-        if (change > (T)1e-10) { fn = fr; delta = 0; change = 0; }
-        if (l == rl) f[s] = fn;
-        v += delta * bv;
-        improvement -= change;
-      }
+    T bv_n = Bm[lc];
+    T b_n = efc[0], f_n = efc[1], R_n = efc[2], ai_n = efc[3], ad_n = efc[4];
+    for (int r = 0; r < ne; r++) {
+      T bv = dl ? bv_n : (T)0;
+      T br = b_n, fr = f_n, Rr = R_n, ai = ai_n, ad = ad_n;
+      const int rn = r + 1 < ne ? r + 1 : r;
+      bv_n = Bm[rn * Bs + lc];
+      const T* qn = efc + 8 * rn;
+      b_n = qn[0]; f_n = qn[1]; R_n = qn[2]; ai_n = qn[3]; ad_n = qn[4];
+      T dot = wave_sum_fast(bv * v);
+      T res = br + dot + Rr * fr;
+      T fn = fr - res * ai;
+      fn = fn < 0 ? (T)0 : fn;
+      T delta = fn - fr;
+      T change = (T)0.5 * delta * delta * ad + delta * res;
+      bool keep = change > (T)1e-10;
+      fn = keep ? fr : fn;
+      delta = keep ? (T)0 : delta;
+      change = keep ? (T)0 : change;
+      efc[8 * r + 1] = fn;  // every lane stores the same uniform value
+      v += delta * bv;
+      improvement -= change;
     }
     iter++;
-    if (improvement * scale < m.tolerance) break;
+    if (improvement * scale < tol) break;
   }
   e.niter = iter;
-#pragma unroll
-  for (int s = 0; s < MGX_EFC_SLOTS; s++) {
-    int r = s * 64 + l;
-    if (r < ne) e.efc_f[r] = f[s];
-  }
   // qacc = qacc_smooth + L^-1 D^-1/2 v ; qfrc_constraint = L' D^1/2 v
-  T z = l < m.nv ? v * e.diaginv * sqrtD : (T)0;  // D^-1/2 = diaginv * sqrt(D)
+  T z = dl ? v * e.diaginv * sqrtD : (T)0;  // D^-1/2 = diaginv * sqrt(D)
   z = solve_L(m, e, e.qLD, z);
   e.qacc = e.qacc_smooth + z;
   e.qfrc_constraint = mul_LT(m, e, e.qLD, sqrtD * v);
@@ -824,7 +828,7 @@ __device__ void pgs(const DevModel<T>& m, Env<T>& e) {
 
 // ---------------------------------------------------------------- integration
 template <typename T>
-__device__ void quat_integrate(T* q, const T* w, T h) {
+__device__ __forceinline__ void quat_integrate(T* q, const T* w, T h) {
   T ax[3] = {w[0], w[1], w[2]}, qr[4];
   T ang = h * normalize3(ax);
   axisangle2quat(qr, ax, ang);
@@ -833,7 +837,7 @@ __device__ void quat_integrate(T* q, const T* w, T h) {
 }
 
 template <typename T>
-__device__ void euler(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void euler(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   bool damp = false;
   for (int k = 0; k < m.nv; k++) damp |= m.dof_damping[k] > 0;
@@ -863,7 +867,9 @@ __device__ void euler(const DevModel<T>& m, Env<T>& e) {
 
 // ---------------------------------------------------------------- forward + step
 template <typename T>
-__device__ void forward(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
+  // phase A (kinematics .. velocity) uses the LDS union region; phase B (constraint rows)
+  // overwrites it with the B matrix once collision has consumed the geom frames
   MGX_STAMP_DECL
   kinematics(m, e);
   MGX_STAMP(0);
@@ -871,18 +877,18 @@ __device__ void forward(const DevModel<T>& m, Env<T>& e) {
   MGX_STAMP(1);
   e.diaginv = factor_ld(m, e.qLD);
   MGX_STAMP(2);
-  collision(m, e);
+  velocity(m, e);
   MGX_STAMP(3);
-  make_constraint(m, e);
+  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
   MGX_STAMP(4);
+  collision(m, e);
+  MGX_STAMP(5);
+  make_constraint(m, e);
+  MGX_STAMP(6);
   // D^-1/2 per dof for the row transform
   if (lane_id() < m.nv) e.vec0[lane_id()] = sqrt(e.diaginv);
   wsync();
   transform_rows(m, e);
-  MGX_STAMP(5);
-  velocity(m, e);
-  MGX_STAMP(6);
-  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
   MGX_STAMP(7);
   pgs(m, e);
   MGX_STAMP(8);
@@ -890,7 +896,7 @@ __device__ void forward(const DevModel<T>& m, Env<T>& e) {
 
 // returns the number of bad-state resets performed (0..3)
 template <typename T>
-__device__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
   int warn = 0;
   if (any_bad(e.qpos, m.nq)) { reset_env(m, e); warn++; }
   if (any_bad(e.qvel, m.nv)) { reset_env(m, e); warn++; }

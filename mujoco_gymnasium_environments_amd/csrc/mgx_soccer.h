@@ -30,7 +30,7 @@ struct SoccerIds {
 
 // Pre-physics env logic: action clip -> ctrl, goalkeeper, wind (soccer_env.py:401-411)
 template <typename T>
-__device__ void soccer_pre(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action,
+__device__ __forceinline__ void soccer_pre(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action,
                            const T* prev_ball, const T* wind) {
   int l = lane_id();
   for (int u = l; u < m.nu; u += 64) {
@@ -55,11 +55,11 @@ template <typename T>
 __device__ __forceinline__ T clip1(T x) { return clampv(x, (T)-1, (T)1); }
 
 template <typename T>
-__device__ T norm3v(T a, T b, T c) { return sqrt(a * a + b * b + c * c); }
+__device__ __forceinline__ T norm3v(T a, T b, T c) { return sqrt(a * a + b * b + c * c); }
 
 // Observation (80 floats) from the forward-pass frames + post-integration qpos/qvel.
 template <typename T>
-__device__ void soccer_obs(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, int step, float* obs) {
+__device__ __forceinline__ void soccer_obs(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, int step, float* obs) {
   int l = lane_id();
   // foot "contact forces": last matching contact wins (soccer_env.py:765-785)
   int lastR = -1, lastL = -1;
@@ -120,7 +120,7 @@ __device__ void soccer_obs(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& 
 }
 
 template <typename T>
-__device__ bool soccer_ball_contact(Env<T>& e, const SoccerIds<T>& ids) {
+__device__ __forceinline__ bool soccer_ball_contact(Env<T>& e, const SoccerIds<T>& ids) {
   bool hit = false;
   for (int base = 0; base < e.ncon; base += 64) {
     int c = base + lane_id();
@@ -137,7 +137,7 @@ __device__ bool soccer_ball_contact(Env<T>& e, const SoccerIds<T>& ids) {
 }
 
 template <typename T>
-__device__ bool soccer_upright(const Env<T>& e, const SoccerIds<T>& ids) {
+__device__ __forceinline__ bool soccer_upright(const Env<T>& e, const SoccerIds<T>& ids) {
   T q[4] = {e.xquat[4 * ids.torso], e.xquat[4 * ids.torso + 1], e.xquat[4 * ids.torso + 2], e.xquat[4 * ids.torso + 3]};
   T R[9];
   quat2mat(R, q);
@@ -146,7 +146,7 @@ __device__ bool soccer_upright(const Env<T>& e, const SoccerIds<T>& ids) {
 
 // Post-physics: step count, obs, reward, termination, stats, prev snapshots
 template <typename T>
-__device__ bool soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
+__device__ __forceinline__ bool soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
                             uint8_t* goal_scored, T* prev_ball, T* prev_robot, T* stats, float* obs, double* reward,
                             uint8_t* terminated, uint8_t* truncated, uint8_t* flags = nullptr) {
   int l = lane_id();
@@ -230,7 +230,7 @@ __device__ __forceinline__ void soccer_draw_ranges(int j, int n_noise, double* l
 }
 // lane j < 36 produces draw j of episode `episode` for global env `genv` into `out` (LDS/global)
 template <typename T>
-__device__ void soccer_philox_draws(uint64_t seed, uint32_t genv, uint32_t episode, int n_noise, T* out) {
+__device__ __forceinline__ void soccer_philox_draws(uint64_t seed, uint32_t genv, uint32_t episode, int n_noise, T* out) {
   int j = lane_id();
   if (j < 36) {
     uint32_t c[4] = {episode, (uint32_t)j, 0x50C3Eu, 0u};
@@ -245,7 +245,7 @@ __device__ void soccer_philox_draws(uint64_t seed, uint32_t genv, uint32_t episo
 // Reset: mj_resetData + the reference's randomisation (draws in reference order), with the
 // jnt_qposadr[0] aliasing quirk (the robot pose lands on goalkeeper + ball qpos).
 template <typename T>
-__device__ void soccer_apply_reset(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const T* draws, T* wind) {
+__device__ __forceinline__ void soccer_apply_reset(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const T* draws, T* wind) {
   reset_env(m, e);
   int l = lane_id();
   if (l == 0) {

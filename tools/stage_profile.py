@@ -14,8 +14,8 @@ sys.path.insert(0, ROOT)
 from mujoco_gymnasium_environments_amd import native  # noqa: E402
 
 PROF_LIB = os.path.join(native.PKG, "libmgx_prof.so")
-STAGES = ["kinematics", "com_crb", "factorM", "collision", "make_constraint", "transform_rows", "velocity",
-          "qacc_smooth", "pgs", "euler"]
+STAGES = ["kinematics", "com_crb", "factorM", "velocity", "qacc_smooth", "collision", "make_constraint",
+          "transform_rows", "pgs", "euler"]
 
 
 def build():
@@ -52,7 +52,7 @@ def main():
     print(f"envs={n} steps={steps} mean cycles/env-step (s_memtime units) total={tot:.0f}")
     for i, s in enumerate(STAGES):
         print(f"  {s:16s} {v[:, i].mean():12.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {sorted(v[:, i])[int(0.99 * n)]:.0f}")
-    print(f"  nefc mean {env.batch.nefc.float().mean().item() if env.batch.nefc.any() else 'n/a'}")
+    print(f"  lds bytes per env {env.native.info.lds_bytes_per_env}")
 
 
 if __name__ == "__main__":
