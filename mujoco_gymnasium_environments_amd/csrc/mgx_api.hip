@@ -307,7 +307,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.qLD = take(d->nM); L.qMH = take(d->nM); L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64);
   L.con_dist = take(max_ncon); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
   L.con_mu = take(max_ncon);
-  L.efc = take(8 * max_nefc); L.efc_margin = take(max_nefc);
+  L.efc = take(8 * max_nefc); L.efc_margin = take(max_nefc); L.efc_blk = take(2 * max_nefc);
   // union: phase A (kinematics .. collision) arrays, then the B matrix of phase B on top
   int u0 = p;
   L.xmat = take(9 * nb); L.xipos = take(3 * nb); L.ximat = take(9 * nb); L.cinert = take(10 * nb);

@@ -27,7 +27,7 @@ struct Layout {
   int qpos, qvel, ctrl, xfrc, xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cfrc;
   int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, geom_xpos, geom_xmat, act_force;
   int con_dist, con_pos, con_frame, con_mu;
-  int efc, efc_margin;
+  int efc, efc_margin, efc_blk;
   int Bmat, Bstride;
   int reals;  // total reals
   // int region (after reals)
@@ -140,6 +140,27 @@ __device__ __forceinline__ float wave_sum_fast(float x) {
   return readlane(x, 63);
 }
 __device__ __forceinline__ double wave_sum_fast(double x) { return wave_sum(x); }
+
+// four independent full-wave sums, DPP steps interleaved so the hazard wait states of one
+// chain are filled by the others (same per-chain order as wave_sum_fast)
+__device__ __forceinline__ void wave_sum4(float& a, float& b, float& c, float& d) {
+#define MGX_STEP4(OP) a += OP(a); b += OP(b); c += OP(c); d += OP(d);
+  MGX_STEP4(dpp_f<0xB1>)
+  MGX_STEP4(dpp_f<0x4E>)
+  MGX_STEP4(dpp_f<0x141>)
+  MGX_STEP4(dpp_f<0x140>)
+#define MGX_B15(x) dpp_upd<0x142, 0xa>(x)
+#define MGX_B31(x) dpp_upd<0x143, 0xc>(x)
+  MGX_STEP4(MGX_B15)
+  MGX_STEP4(MGX_B31)
+#undef MGX_B15
+#undef MGX_B31
+#undef MGX_STEP4
+  a = readlane(a, 63); b = readlane(b, 63); c = readlane(c, 63); d = readlane(d, 63);
+}
+__device__ __forceinline__ void wave_sum4(double& a, double& b, double& c, double& d) {
+  a = wave_sum(a); b = wave_sum(b); c = wave_sum(c); d = wave_sum(d);
+}
 
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int prefix_count(unsigned long long mask) {  // set bits below this lane

@@ -24,7 +24,7 @@ struct Env {
   // per-row constraint data, AoS with stride 8 so the solver fetches a row's scalars with one
   // 16-byte LDS read: [0] b, [1] f, [2] R (diagApprox until impedance), [3] 1/AR_rr,
   // [4] AR_rr, [5] aref (K*imp*(pos-margin) until the solver), [6] B damping, [7] pos
-  T *efc, *efc_margin;
+  T *efc, *efc_margin, *efc_blk;
   T *Bm;
   int Bs;
   int *con_geom, *con_pair, *act_list, *efc_type, *efc_id;
@@ -47,7 +47,7 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.geom_xpos = R + L.geom_xpos;
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.con_dist = R + L.con_dist;
   e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
-  e.efc_margin = R + L.efc_margin; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
+  e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
   int* I = reinterpret_cast<int*>(R + L.reals);
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
   e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id;
@@ -784,35 +784,70 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
     v = 0;
   }
   wsync();
-  // Gauss-Seidel sweeps with early exit on scaled improvement < tolerance
+  // Gauss-Seidel sweeps with early exit on scaled improvement < tolerance. Rows go in blocks of
+  // 4: the four dots B_r.v use the pre-block v (4 interleaved reductions), and row i of the
+  // block adds sum_{j<i} A_ij delta_j with A_ij = B_i.B_j precomputed -> the same sequential
+  // Gauss-Seidel update as row-by-row, in a quarter of the reduction latency. Rows ne..ne4-1
+  // are zero padding (B = 0, b = f = 0, R = AR = 1) and never change.
+  const int ne4 = (ne + 3) & ~3;
+  for (int r = ne + l; r < ne4; r += 64) {
+    T* q = efc + 8 * r;
+    q[0] = 0; q[1] = 0; q[2] = 1; q[3] = 1; q[4] = 1;
+  }
+  for (int r = ne; r < ne4; r++)
+    if (dl) e.Bm[r * Bs + l] = 0;
+  wsync();
+  T* blk = e.efc_blk;  // [ne4/4][8]: A_10, A_20, A_21, A_30, A_31, A_32
+  for (int b0 = 4 * l; b0 < ne4; b0 += 256) {
+    const T* r0 = Bm + b0 * Bs;
+    const T* r1 = r0 + Bs;
+    const T* r2 = r1 + Bs;
+    const T* r3 = r2 + Bs;
+    T a10 = 0, a20 = 0, a21 = 0, a30 = 0, a31 = 0, a32 = 0;
+    for (int k = 0; k < nv; k++) {
+      T x0 = r0[k], x1 = r1[k], x2 = r2[k], x3 = r3[k];
+      a10 += x1 * x0; a20 += x2 * x0; a21 += x2 * x1; a30 += x3 * x0; a31 += x3 * x1; a32 += x3 * x2;
+    }
+    T* o = blk + 2 * b0;
+    o[0] = a10; o[1] = a20; o[2] = a21; o[3] = a30; o[4] = a31; o[5] = a32;
+  }
+  wsync();
   const T scale = (T)1 / (m.meaninertia * (T)(nv > 1 ? nv : 1));
   const T tol = m.tolerance;
   const int maxit = m.iterations;
   int iter = 0;
   while (iter < maxit) {
     T improvement = 0;
-    T bv_n = Bm[lc];
-    T b_n = efc[0], f_n = efc[1], R_n = efc[2], ai_n = efc[3], ad_n = efc[4];
-    for (int r = 0; r < ne; r++) {
-      T bv = dl ? bv_n : (T)0;
-      T br = b_n, fr = f_n, Rr = R_n, ai = ai_n, ad = ad_n;
-      const int rn = r + 1 < ne ? r + 1 : r;
-      bv_n = Bm[rn * Bs + lc];
-      const T* qn = efc + 8 * rn;
-      b_n = qn[0]; f_n = qn[1]; R_n = qn[2]; ai_n = qn[3]; ad_n = qn[4];
-      T dot = wave_sum_fast(bv * v);
-      T res = br + dot + Rr * fr;
-      T fn = fr - res * ai;
-      fn = fn < 0 ? (T)0 : fn;
-      T delta = fn - fr;
-      T change = (T)0.5 * delta * delta * ad + delta * res;
-      bool keep = change > (T)1e-10;
-      fn = keep ? fr : fn;
-      delta = keep ? (T)0 : delta;
-      change = keep ? (T)0 : change;
-      efc[8 * r + 1] = fn;  // every lane stores the same uniform value
-      v += delta * bv;
-      improvement -= change;
+    for (int r0 = 0; r0 < ne4; r0 += 4) {
+      T bv0 = Bm[(r0 + 0) * Bs + lc], bv1 = Bm[(r0 + 1) * Bs + lc];
+      T bv2 = Bm[(r0 + 2) * Bs + lc], bv3 = Bm[(r0 + 3) * Bs + lc];
+      bv0 = dl ? bv0 : (T)0; bv1 = dl ? bv1 : (T)0; bv2 = dl ? bv2 : (T)0; bv3 = dl ? bv3 : (T)0;
+      T d0 = bv0 * v, d1 = bv1 * v, d2 = bv2 * v, d3 = bv3 * v;
+      wave_sum4(d0, d1, d2, d3);
+      const T* a = blk + 2 * r0;
+      T a10 = a[0], a20 = a[1], a21 = a[2], a30 = a[3], a31 = a[4], a32 = a[5];
+      T dl0, dl1, dl2, dl3;
+#define MGX_ROW(i, DOT, DL)                                                        \
+      {                                                                            \
+        T* q = efc + 8 * (r0 + i);                                                 \
+        T br = q[0], fr = q[1], Rr = q[2], ai = q[3], ad = q[4];                   \
+        T res = br + (DOT) + Rr * fr;                                              \
+        T fn = fr - res * ai;                                                      \
+        fn = fn < 0 ? (T)0 : fn;                                                   \
+        T delta = fn - fr;                                                         \
+        T change = (T)0.5 * delta * delta * ad + delta * res;                      \
+        bool keep = change > (T)1e-10;                                             \
+        fn = keep ? fr : fn;                                                       \
+        DL = keep ? (T)0 : delta;                                                  \
+        improvement -= keep ? (T)0 : change;                                       \
+        q[1] = fn;                                                                 \
+      }
+      MGX_ROW(0, d0, dl0)
+      MGX_ROW(1, d1 + a10 * dl0, dl1)
+      MGX_ROW(2, d2 + a20 * dl0 + a21 * dl1, dl2)
+      MGX_ROW(3, d3 + a30 * dl0 + a31 * dl1 + a32 * dl2, dl3)
+#undef MGX_ROW
+      v += dl0 * bv0 + dl1 * bv1 + dl2 * bv2 + dl3 * bv3;
     }
     iter++;
     if (improvement * scale < tol) break;
@@ -892,6 +927,14 @@ __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
   MGX_STAMP(7);
   pgs(m, e);
   MGX_STAMP(8);
+#ifdef MGX_PROFILE
+  if (g_mgx_prof && lane_id() == 0) {
+    g_mgx_prof[blockIdx.x * 32 + 20] += e.nefc;
+    g_mgx_prof[blockIdx.x * 32 + 21] += e.niter;
+    g_mgx_prof[blockIdx.x * 32 + 22] += e.ncon;
+    g_mgx_prof[blockIdx.x * 32 + 23] += 1;
+  }
+#endif
 }
 
 // returns the number of bad-state resets performed (0..3)

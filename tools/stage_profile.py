@@ -53,6 +53,13 @@ def main():
     for i, s in enumerate(STAGES):
         print(f"  {s:16s} {v[:, i].mean():12.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {sorted(v[:, i])[int(0.99 * n)]:.0f}")
     print(f"  lds bytes per env {env.native.info.lds_bytes_per_env}")
+    raw = buf.view(n, 32).double().cpu().numpy()
+    calls = raw[:, 23].sum()
+    print(f"  per forward: nefc mean {raw[:, 20].sum() / calls:.1f}  PGS iterations mean {raw[:, 21].sum() / calls:.1f}"
+          f"  ncon mean {raw[:, 22].sum() / calls:.1f}  forwards per env-step {calls / (n * steps):.2f}")
+    import numpy as np
+    nefc_env = raw[:, 20] / np.maximum(raw[:, 23], 1)
+    print(f"  per-env mean nefc p50 {np.percentile(nefc_env, 50):.0f} p90 {np.percentile(nefc_env, 90):.0f} max {nefc_env.max():.0f}")
 
 
 if __name__ == "__main__":
