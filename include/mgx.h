@@ -146,6 +146,8 @@ typedef struct mgx_soccer_env {
                                     when every reset passes host draws */
   uint8_t *flags;        /* [N][2]  ball_contact, robot_upright of the last step (info dict,
                                     soccer_env.py:438-439); nullable */
+  void *rollout;         /* [N][4]  running sums: reward, terminated, truncated, env steps
+                                    (the end-of-rollout metrics; nullable) */
 } mgx_soccer_env;
 
 typedef struct mgx_soccer_ids {

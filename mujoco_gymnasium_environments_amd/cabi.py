@@ -72,7 +72,7 @@ class MgxFrames(C.Structure):
 class MgxSoccerEnv(C.Structure):
     _fields_ = [("prev_ball_pos", C.c_void_p), ("prev_robot_pos", C.c_void_p), ("wind", C.c_void_p),
                 ("step", C.c_void_p), ("goal_scored", C.c_void_p), ("stats", C.c_void_p),
-                ("episode", C.c_void_p), ("flags", C.c_void_p)]
+                ("episode", C.c_void_p), ("flags", C.c_void_p), ("rollout", C.c_void_p)]
 
 
 class MgxSoccerLogicIO(C.Structure):

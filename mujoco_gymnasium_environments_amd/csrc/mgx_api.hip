@@ -226,6 +226,13 @@ __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, 
     bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball, prev_robot, stats, o,
                             reward + env, terminated + env, truncated + env,
                             ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
+    if (ev.rollout && l == 0) {
+      T* ro = (T*)ev.rollout + 4 * (size_t)env;
+      ro[0] += (T)reward[env];
+      ro[1] += (T)terminated[env];
+      ro[2] += (T)truncated[env];
+      ro[3] += (T)1;
+    }
     if (done && autoreset) {
       if (final_obs)
         for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];

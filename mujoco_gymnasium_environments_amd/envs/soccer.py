@@ -136,6 +136,7 @@ class SoccerVectorEnv:
         self.stats = torch.zeros(N, 5, dtype=dt, device=dev)
         self.episode = torch.zeros(N, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(N, 2, dtype=torch.uint8, device=dev)
+        self.rollout = torch.zeros(N, 4, dtype=dt, device=dev)  # reward, terminated, truncated, steps
         self.obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
         self.final_obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
         self.reward = torch.zeros(N, dtype=torch.float64, device=dev)
@@ -143,7 +144,7 @@ class SoccerVectorEnv:
         self.truncated = torch.zeros(N, dtype=torch.uint8, device=dev)
         self._env = cabi.MgxSoccerEnv(*[t.data_ptr() for t in (self.prev_ball_pos, self.prev_robot_pos, self.wind,
                                                                self.step_count, self.goal_scored, self.stats,
-                                                               self.episode, self.flags)])
+                                                               self.episode, self.flags, self.rollout)])
         ids = self.tables.ids_struct()
         check(lib().mgx_soccer_configure(self.native.handle, C.byref(ids)), "mgx_soccer_configure")
         nq = np.array([int(self.model.jnt_qposadr[j]) for j in self.tables.noise_joints], dtype=np.int32)
