@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
+    ap.add_argument("--banks", type=int, default=4)
     args = ap.parse_args()
 
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
@@ -124,7 +126,8 @@ def main():
 
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     N = args.envs
-    env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
+    env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
+                          staged=not args.mono, banks=args.banks)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]

@@ -85,6 +85,8 @@ typedef struct mgx_model_info {
   int32_t max_nv, max_nbody, max_ncon, max_nefc, max_njnt;
   int32_t precision;
   int32_t lds_bytes_per_env; /* dynamic LDS used by the step kernel for one env */
+  int32_t lds_bytes_rows;    /* staged soccer step: row-builder LDS per env */
+  int32_t lds_bytes_finish;  /* staged soccer step: finisher LDS per env */
 } mgx_model_info;
 
 typedef struct mgx_model mgx_model; /* opaque: device-resident model constants */
@@ -148,6 +150,11 @@ typedef struct mgx_soccer_env {
                                     soccer_env.py:438-439); nullable */
   void *rollout;         /* [N][4]  running sums: reward, terminated, truncated, env steps
                                     (the end-of-rollout metrics; nullable) */
+  void *workspace;       /* nullable: staged-step workspace (mgx_soccer_workspace_bytes), bound
+                            to (model, N, banks); holds the reset banks between calls */
+  uint64_t workspace_bytes;
+  int32_t banks;         /* reset banks per env (0 = none; autoreset then resets in-launch) */
+  int32_t pad0;
 } mgx_soccer_env;
 
 typedef struct mgx_soccer_ids {
@@ -181,6 +188,14 @@ int mgx_soccer_step(const mgx_model *m, const mgx_state *s, const mgx_soccer_env
 int mgx_soccer_reset(const mgx_model *m, const mgx_state *s, const mgx_soccer_env *e,
                      const void *draws, float *obs, uint64_t seed, int env_offset, int n_env,
                      const uint8_t *env_mask, void *stream);
+
+/* Staged soccer step (row builder -> lane-group PGS -> finisher): size and
+ * initialise the workspace for N envs and `banks` precomputed resets per env. With a
+ * workspace, mgx_soccer_step runs the staged kernels; mgx_soccer_reset with device draws
+ * also settles the env's banks. */
+int64_t mgx_soccer_workspace_bytes(const mgx_model *m, int n_env, int banks);
+int mgx_soccer_workspace_init(const mgx_model *m, void *workspace, uint64_t bytes, int n_env, int banks,
+                              void *stream);
 
 /* Test hook: env logic only, on caller-supplied frames and contact lists (no physics). */
 typedef struct mgx_soccer_logic_io {

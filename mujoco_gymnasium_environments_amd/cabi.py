@@ -55,7 +55,8 @@ class MgxModelDesc(C.Structure):
 class MgxModelInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "npair", "max_nv", "max_nbody",
-                 "max_ncon", "max_nefc", "max_njnt", "precision", "lds_bytes_per_env"]]
+                 "max_ncon", "max_nefc", "max_njnt", "precision", "lds_bytes_per_env", "lds_bytes_rows",
+                 "lds_bytes_finish"]]
 
 
 class MgxState(C.Structure):
@@ -72,7 +73,9 @@ class MgxFrames(C.Structure):
 class MgxSoccerEnv(C.Structure):
     _fields_ = [("prev_ball_pos", C.c_void_p), ("prev_robot_pos", C.c_void_p), ("wind", C.c_void_p),
                 ("step", C.c_void_p), ("goal_scored", C.c_void_p), ("stats", C.c_void_p),
-                ("episode", C.c_void_p), ("flags", C.c_void_p), ("rollout", C.c_void_p)]
+                ("episode", C.c_void_p), ("flags", C.c_void_p), ("rollout", C.c_void_p),
+                ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32),
+                ("pad0", C.c_int32)]
 
 
 class MgxSoccerLogicIO(C.Structure):

@@ -11,7 +11,7 @@
 #include <vector>
 
 #include "../../include/mgx.h"
-#include "mgx_soccer.h"
+#include "mgx_staged.h"
 
 using namespace mgx;
 
@@ -43,9 +43,9 @@ struct mgx_model {
   int device;
   void* dbuf = nullptr;
   size_t dbytes = 0;
-  DevModel<float> mf;
-  DevModel<double> md;
-  Layout L;
+  DevModel<float> mf, mfs, mff;   // monolithic / staged row builder / staged finisher layouts
+  DevModel<double> md, mds, mdf;
+  Layout L, Ls, Lf;
   bool soccer_ok = false;
   SoccerIds<float> sf;
   SoccerIds<double> sd;
@@ -195,63 +195,257 @@ __device__ __forceinline__ int soccer_reset_body(const DevModel<T>& m, Env<T>& e
   return warn;
 }
 
-// soccer: MODE 0 = step (+ optional same-step autoreset), MODE 1 = reset
+// Philox-drawn reset of `env` for its current episode counter, then the counter advances;
+// with banks, the bank of the consumed episode restarts for episode + R. Writes the state.
+template <typename T>
+__device__ __forceinline__ void soccer_reset_philox(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, mgx_state s,
+                                                    mgx_soccer_env ev, float* obs, uint64_t seed, int env_offset, int env,
+                                                    const Pipe* P) {
+  int l = lane_id();
+  int E = ev.episode[env];
+  soccer_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)E, ids.n_noise, e.vec1);
+  wsync();
+  int warn = soccer_reset_body(m, e, ids, e.vec1, (T*)ev.wind + 3 * (size_t)env, (T*)ev.prev_ball_pos + 3 * (size_t)env,
+                               (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, ev.step + env,
+                               ev.goal_scored + env, obs + (size_t)env * 80);
+  store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
+              (T*)s.time, env);
+  if (l == 0) {
+    if (s.warning) s.warning[env] += warn;
+    ev.episode[env] = E + 1;
+  }
+  wsync();
+  if (P) bank_init(m, e, ids, *P, env, E % P->R, E + P->R, seed, env_offset);
+}
+
+// One full soccer step of `env` in one wave (pre, mj_step, post, same-step autoreset).
+template <typename T>
+__device__ __forceinline__ void soccer_step_mono(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, mgx_state s,
+                                                 mgx_soccer_env ev, const float* action, float* obs, double* reward,
+                                                 uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
+                                                 uint64_t seed, int env_offset, int env, const Pipe* P) {
+  T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
+  T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
+  load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  T* prev_ball = (T*)ev.prev_ball_pos + 3 * (size_t)env;
+  float* o = obs + (size_t)env * 80;
+  int l = lane_id();
+  const float* a = action + (size_t)env * m.nu;
+  soccer_pre(m, e, ids, a, prev_ball, (T*)ev.wind + 3 * (size_t)env);
+  int warn = mj_step_env(m, e);
+  bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball,
+                          (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, o, reward + env,
+                          terminated + env, truncated + env, ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
+  if (ev.rollout && l == 0) {
+    T* ro = (T*)ev.rollout + 4 * (size_t)env;
+    ro[0] += (T)reward[env];
+    ro[1] += (T)terminated[env];
+    ro[2] += (T)truncated[env];
+    ro[3] += (T)1;
+  }
+  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  if (l == 0 && s.warning) s.warning[env] += warn;
+  if (done && autoreset) {
+    if (final_obs)
+      for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];
+    __threadfence();
+    wsync();
+    if (!(P && bank_install(m, e, ids, *P, s, ev, obs, seed, env_offset, env)))
+      soccer_reset_philox(m, e, ids, s, ev, obs, seed, env_offset, env, P);
+  }
+}
+
+// soccer: MODE 0 = step (+ optional same-step autoreset), MODE 1 = reset. With a workspace
+// (P), MODE 1 also settles the env's R banks (episodes E+1 .. E+R) in the same wave.
 template <typename T, int MODE>
 __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
                                                const float* action, const T* draws, float* obs, double* reward,
                                                uint8_t* terminated, uint8_t* truncated, float* final_obs,
                                                int autoreset, uint64_t seed, int env_offset, int n_env,
-                                               const uint8_t* mask) {
+                                               const uint8_t* mask, Pipe pipe, int use_pipe) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int env = blockIdx.x;
   if (env >= n_env) return;
   if (mask && !mask[env]) return;
   Env<T> e;
   env_bind(m, e, smem);
+  const Pipe* P = use_pipe ? &pipe : nullptr;
+  if (MODE == 0) {
+    soccer_step_mono(m, e, ids, s, ev, action, obs, reward, terminated, truncated, final_obs, autoreset, seed,
+                     env_offset, env, P);
+    return;
+  }
+  if (!draws) {
+    soccer_reset_philox(m, e, ids, s, ev, obs, seed, env_offset, env, nullptr);
+    if (P) {
+      // prefill: bank for episode E' settles now, so the first R terminations never wait
+      int E1 = ev.episode[env];
+      for (int k = 0; k < P->R; k++) {
+        int Ep = E1 + k;
+        int bi = env * P->R + Ep % P->R;
+        bank_init(m, e, ids, *P, env, Ep % P->R, Ep, seed, env_offset);
+        int warn = 0;
+        for (int t = 0; t < 10; t++) warn += mj_step_env(m, e);
+        bank_store_state(m, e, *P, bi, warn);
+        bank_finalize(m, e, ids, *P, bi);
+        wsync();
+        if (lane_id() == 0) P->at<int>(P->o_bk)[bi] = 10;
+      }
+    }
+    return;
+  }
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  T* prev_ball = (T*)ev.prev_ball_pos + 3 * (size_t)env;
-  T* prev_robot = (T*)ev.prev_robot_pos + 3 * (size_t)env;
-  T* wind = (T*)ev.wind + 3 * (size_t)env;
-  T* stats = (T*)ev.stats + 5 * (size_t)env;
-  float* o = obs + (size_t)env * 80;
-  int l = lane_id();
-  int warn = 0;
-  bool do_reset = MODE == 1;
-  if (MODE == 0) {
-    const float* a = action + (size_t)env * m.nu;
-    soccer_pre(m, e, ids, a, prev_ball, wind);
-    warn += mj_step_env(m, e);
-    bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball, prev_robot, stats, o,
-                            reward + env, terminated + env, truncated + env,
-                            ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
-    if (ev.rollout && l == 0) {
-      T* ro = (T*)ev.rollout + 4 * (size_t)env;
-      ro[0] += (T)reward[env];
-      ro[1] += (T)terminated[env];
-      ro[2] += (T)truncated[env];
-      ro[3] += (T)1;
-    }
-    if (done && autoreset) {
-      if (final_obs)
-        for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];
-      do_reset = true;
-    }
-  }
-  if (do_reset) {
-    const T* d = draws ? draws + (size_t)env * 36 : nullptr;
-    if (!d) {  // counter-based draws for this env's next episode
-      soccer_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)ev.episode[env], ids.n_noise, e.vec1);
-      wsync();
-      d = e.vec1;
-    }
-    warn += soccer_reset_body(m, e, ids, d, wind, prev_ball, prev_robot, stats, ev.step + env,
-                              ev.goal_scored + env, o);
-    if (l == 0) ev.episode[env] += 1;
-  }
+  int warn = soccer_reset_body(m, e, ids, draws + (size_t)env * 36, (T*)ev.wind + 3 * (size_t)env,
+                               (T*)ev.prev_ball_pos + 3 * (size_t)env, (T*)ev.prev_robot_pos + 3 * (size_t)env,
+                               (T*)ev.stats + 5 * (size_t)env, ev.step + env, ev.goal_scored + env,
+                               obs + (size_t)env * 80);
+  if (ev.episode && lane_id() == 0) ev.episode[env] += 1;
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  if (lane_id() == 0 && s.warning) s.warning[env] += warn;
+}
+
+// ---- staged step kernels (mgx_staged.h)
+template <typename T>
+__global__ void __launch_bounds__(64) k_soccer_rows(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
+                                                    const float* action, int n_env, const uint8_t* mask, Pipe P,
+                                                    int banks) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int b = blockIdx.x;
+  int slot;
+  Env<T> e;
+  if (b < n_env) {
+    if (mask && !mask[b]) return;
+    env_bind(m, e, smem);
+    load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
+               (T*)s.time, b);
+    soccer_pre(m, e, ids, action + (size_t)b * m.nu, (T*)ev.prev_ball_pos + 3 * (size_t)b, (T*)ev.wind + 3 * (size_t)b);
+    slot = b;
+  } else {
+    int bi = b - n_env;
+    if (!banks || bi >= n_env * P.R) return;
+    int k = P.at<int>(P.o_bk)[bi];
+    if (k < 0 || k >= 10) return;
+    env_bind(m, e, smem);
+    bank_load_state(m, e, P, bi);
+    slot = b;
+  }
+  int warn = 0;  // mj_checkPos / mj_checkVel
+  if (any_bad(e.qpos, m.nq)) { reset_env(m, e); warn++; }
+  if (any_bad(e.qvel, m.nv)) { reset_env(m, e); warn++; }
+  stage_rows(m, e, P, slot, warn);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
+                                                      const float* action, float* obs, double* reward,
+                                                      uint8_t* terminated, uint8_t* truncated, float* final_obs,
+                                                      int autoreset, uint64_t seed, int env_offset, int n_env,
+                                                      const uint8_t* mask, Pipe P, int banks) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int env = blockIdx.x;
+  if (env >= n_env) return;
+  int l = lane_id();
+  if (env == 0 && l == 0) P.ctr()[1] = 0;  // the solver list is consumed
+  Env<T> e;
+  env_bind(m, e, smem);
+  if (banks) {
+    for (int b = 0; b < P.R; b++) {
+      int bi = env * P.R + b;
+      int k = P.at<int>(P.o_bk)[bi];
+      if (k < 0 || k >= 10) continue;
+      int slot = n_env + bi;
+      int warn = load_carry(m, e, P, slot);
+      if (!finish_physics(m, e, P, slot)) {
+        load_template(m, e, P);
+        warn++;
+      }
+      bank_store_state(m, e, P, bi, warn);
+      k++;
+      if (k == 10) bank_finalize(m, e, ids, P, bi);
+      if (l == 0) P.at<int>(P.o_bk)[bi] = k;
+      wsync();
+    }
+    __threadfence();
+    wsync();
+  }
+  if (mask && !mask[env]) return;
+  int warn = load_carry(m, e, P, env);
+  if (!finish_physics(m, e, P, env)) {
+    load_template(m, e, P);
+    warn++;
+  }
+  store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
+              (T*)s.time, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+  const float* a = action + (size_t)env * m.nu;
+  float* o = obs + (size_t)env * 80;
+  bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, (T*)ev.prev_ball_pos + 3 * (size_t)env,
+                          (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, o, reward + env,
+                          terminated + env, truncated + env, ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
+  if (ev.rollout && l == 0) {
+    T* ro = (T*)ev.rollout + 4 * (size_t)env;
+    ro[0] += (T)reward[env];
+    ro[1] += (T)terminated[env];
+    ro[2] += (T)truncated[env];
+    ro[3] += (T)1;
+  }
+  if (done && autoreset) {
+    if (final_obs)
+      for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];
+    __threadfence();
+    wsync();
+    bool ok = banks && bank_install(m, e, ids, P, s, ev, obs, seed, env_offset, env);
+    if (!ok && l == 0) {
+      int i = atomicAdd(P.ctr(), 1);
+      P.at<int>(P.o_fix)[i] = env * 4 + FIX_RESET;
+    }
+  }
+}
+
+// mj_step from mj_resetData'd state (the checkAcc template, see load_template)
+template <typename T>
+__global__ void __launch_bounds__(64) k_soccer_template(DevModel<T> m, Pipe P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Env<T> e;
+  env_bind(m, e, smem);
+  int l = lane_id();
+  reset_env(m, e);
+  forward(m, e);
+  e.qacc_ws = e.qacc;
+  euler(m, e);
+  for (int k = l; k < m.nq; k += 64) P.at<T>(P.o_tq)[k] = e.qpos[k];
+  for (int k = l; k < m.nv; k += 64) { P.at<T>(P.o_tv)[k] = e.qvel[k]; }
+  if (l < m.nv) P.at<T>(P.o_ta)[l] = e.qacc_ws;
+  for (int k = l; k < 3 * m.nbody; k += 64) { P.at<T>(P.o_tx)[k] = e.xpos[k]; P.at<T>(P.o_tsc)[k] = e.subtree_com[k]; }
+  for (int k = l; k < 4 * m.nbody; k += 64) P.at<T>(P.o_txq)[k] = e.xquat[k];
+  int nc = e.ncon < P.maxC ? e.ncon : P.maxC;
+  for (int k = l; k < nc; k += 64) {
+    P.at<int>(P.o_tcg)[2 * k] = e.con_geom[2 * k];
+    P.at<int>(P.o_tcg)[2 * k + 1] = e.con_geom[2 * k + 1];
+    P.at<T>(P.o_tcd)[k] = e.con_dist[k];
+    P.at<T>(P.o_tcm)[k] = e.con_mu[k];
+  }
+  if (l == 0) { P.at<int>(P.o_tn)[0] = nc; P.at<T>(P.o_tt)[0] = e.time; }
+}
+
+// S4: resets whose bank was not ready (listed by the finisher), monolithic: one wave per
+// env with the full LDS layout, grid-stride over the list
+template <typename T>
+__global__ void __launch_bounds__(64) k_soccer_fixup(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
+                                                     float* obs, uint64_t seed, int env_offset, Pipe P, int banks) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int cnt = P.ctr()[0];
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    int env = P.at<int>(P.o_fix)[i] >> 2;
+    Env<T> e;
+    env_bind(m, e, smem);
+    load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied,
+               (T*)s.xfrc_applied, (T*)s.time, env);
+    soccer_reset_philox(m, e, ids, s, ev, obs, seed, env_offset, env, banks ? &P : nullptr);
+    wsync();
+  }
 }
 
 // Env-logic-only test hook: frames/contacts come from the caller (golden vectors generated
@@ -301,21 +495,26 @@ namespace {
 
 int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
-Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active) {
+Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active, bool staged) {
   Layout L{};
   int p = 0;
   int al = 16 / real_bytes;  // 16-byte alignment in elements
   auto take = [&](int n) { int r = p; p = align_up(p + (n > 0 ? n : 1), al); return r; };
   int nb = d->nbody, nv = d->nv, nj = d->njnt, ng = d->ngeom;
   L.max_ncon = max_ncon; L.max_nefc = max_nefc; L.max_active = max_active;
-  // persistent for the whole step (state, frames read by env logic, factors, contacts, rows)
+  L.staged = staged ? 1 : 0;
+  // carry: state + frames read by env logic + factors + contacts (the finisher's inputs)
   L.qpos = take(d->nq); L.qvel = take(nv); L.ctrl = take(d->nu); L.xfrc = take(6 * nb);
-  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb); L.cdof = take(6 * nv);
-  L.qLD = take(d->nM); L.qMH = take(d->nM); L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64);
-  L.con_dist = take(max_ncon); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
-  L.con_mu = take(max_ncon);
-  L.efc = take(8 * max_nefc); L.efc_margin = take(max_nefc); L.efc_blk = take(2 * max_nefc);
-  // union: phase A (kinematics .. collision) arrays, then the B matrix of phase B on top
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb);
+  L.qLD = take(d->nM); L.qMH = take(d->nM); L.con_dist = take(max_ncon); L.con_mu = take(max_ncon);
+  L.carry_reals = p;
+  L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64); L.vec3 = take(64);
+  int vec_end = p;
+  // persistent for the rest of the forward pass
+  L.cdof = take(6 * nv); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
+  L.efc = take(8 * max_nefc); L.efc_margin = take(max_nefc); L.efc_blk = take(staged ? 1 : 2 * max_nefc);
+  // union: phase A (kinematics .. collision) arrays, then B rows on top (all rows for the
+  // monolithic kernel, one chunk of rows for the staged row builder)
   int u0 = p;
   L.xmat = take(9 * nb); L.xipos = take(3 * nb); L.ximat = take(9 * nb); L.cinert = take(10 * nb);
   L.crb = take(10 * nb); L.cvel = take(6 * nb); L.cfrc = take(6 * nb); L.cdof_dot = take(6 * nv);
@@ -324,13 +523,26 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   int endA = p;
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
   L.Bmat = u0;
-  int endB = align_up(u0 + max_nefc * L.Bstride, al);
+  L.chunk_rows = staged ? 64 : max_nefc;
+  int endB = align_up(u0 + L.chunk_rows * L.Bstride, al);
   L.reals = endA > endB ? endA : endB;
   int q = 0;
   auto takei = [&](int n) { int r = q; q = align_up(q + (n > 0 ? n : 1), 4); return r; };
-  L.con_geom = takei(2 * max_ncon); L.con_pair = takei(max_ncon); L.act_list = takei(max_active);
-  L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
+  L.con_geom = takei(2 * max_ncon);
+  L.carry_ints = q;
+  L.con_pair = takei(max_ncon); L.act_list = takei(max_active);
+  L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc); L.con_efcadr = takei(max_ncon);
   L.ints = q;
+  L.bytes = L.reals * real_bytes + L.ints * 4;
+  (void)vec_end;
+  return L;
+}
+
+// The finisher binds the staged layout but only owns the carry + scratch vectors.
+Layout finisher_layout(const Layout& S, int real_bytes) {
+  Layout L = S;
+  L.reals = S.vec3 + 64;
+  L.ints = S.carry_ints;
   L.bytes = L.reals * real_bytes + L.ints * 4;
   return L;
 }
@@ -447,6 +659,79 @@ int check_state(const mgx_state* s) {
 
 }  // namespace
 
+// Staged-step workspace layout for (model, n_env, banks); offsets in bytes, 256-aligned.
+static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P) {
+  int rb = m->precision == MGX_F32 ? 4 : 8;
+  int nq = m->precision == MGX_F32 ? m->mf.nq : m->md.nq;
+  int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
+  Pipe p{};
+  p.base = (char*)ws;
+  p.N = n_env; p.R = banks; p.S = n_env * (1 + banks);
+  p.maxE = m->Ls.max_nefc; p.nv = nv; p.dpl = (nv + 15) / 16;
+  p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
+  p.carryi_stride = m->Ls.carry_ints + 8;
+  p.brow = 16 * p.dpl;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t r = off; off = (off + bytes + 255) / 256 * 256; return r; };
+  size_t S = (size_t)p.S, NB = (size_t)n_env * (banks > 0 ? banks : 1);
+  p.o_ctr = take(64);
+  p.o_carry = take(S * p.carry_stride * rb);
+  p.o_carryi = take(S * p.carryi_stride * 4);
+  p.o_ne = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_fix = take((size_t)n_env * 4);
+  p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
+  p.o_B = take(S * (p.maxE + MGX_BPAD) * p.brow * rb);
+  p.o_vout = take(S * 64 * rb);
+  p.o_bq = take(NB * nq * rb); p.o_bv = take(NB * nv * rb); p.o_ba = take(NB * nv * rb); p.o_btime = take(NB * rb);
+  p.o_bobs = take(NB * 80 * 4); p.o_bprev = take(NB * 6 * rb); p.o_bwind = take(NB * 3 * rb);
+  p.o_bk = take(NB * 4); p.o_bep = take(NB * 4); p.o_bwarn = take(NB * 4); p.o_bseed = take(NB * 8);
+  int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
+  p.maxC = m->Ls.max_ncon;
+  p.o_tq = take(nq * rb); p.o_tv = take(nv * rb); p.o_ta = take(64 * rb); p.o_tt = take(rb);
+  p.o_tx = take(3 * nb * rb); p.o_txq = take(4 * nb * rb); p.o_tsc = take(3 * nb * rb); p.o_tn = take(4);
+  p.o_tcg = take(2 * p.maxC * 4); p.o_tcd = take(p.maxC * rb); p.o_tcm = take(p.maxC * rb);
+  if (P) *P = p;
+  return off;
+}
+
+static int pgs_lds_bytes(const mgx_model* m) {
+  int rb = m->precision == MGX_F32 ? 4 : 8;
+  return 4 * (MGX_SCAL * m->Ls.max_nefc + 4) * rb + 64;
+}
+
+template <typename T>
+static void launch_pgs(const Pipe& P, int grid, int lds, hipStream_t st, int maxit, T tol, T scale) {
+  switch (P.dpl) {
+    case 1: hipLaunchKernelGGL((k_pgs_groups<T, 1>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
+    case 2: hipLaunchKernelGGL((k_pgs_groups<T, 2>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
+    case 3: hipLaunchKernelGGL((k_pgs_groups<T, 3>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
+    default: hipLaunchKernelGGL((k_pgs_groups<T, 4>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
+  }
+}
+
+template <typename T>
+static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms, const DevModel<T>& Mf,
+                              const SoccerIds<T>& ids, const mgx_state* s, const mgx_soccer_env* e, const float* action,
+                              float* obs, double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs,
+                              int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t* mask,
+                              hipStream_t st) {
+  Pipe P;
+  int banks = autoreset ? e->banks : 0;
+  size_t need = make_pipe(m, e->workspace, n_env, e->banks, &P);
+  if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
+  int slots = n_env * (1 + banks);
+  hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, *e, action, n_env, mask, P,
+                     banks);
+  T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
+  launch_pgs<T>(P, (slots + 3) / 4, pgs_lds_bytes(m), st, M.iterations, M.tolerance, scale);
+  hipLaunchKernelGGL(k_soccer_finish<T>, dim3(n_env), dim3(64), m->Lf.bytes, st, Mf, ids, *s, *e, action, obs, reward,
+                     terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks);
+  int fgrid = n_env < 256 ? n_env : 256;
+  hipLaunchKernelGGL(k_soccer_fixup<T>, dim3(fgrid), dim3(64), m->L.bytes, st, M, ids, *s, *e, obs, seed, env_offset, P,
+                     banks);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
 template <typename T>
 static void fill_ids(SoccerIds<T>& o, const mgx_soccer_ids* ids, const DevModel<T>& M, const mgx_model_desc* unused) {
   (void)unused;
@@ -485,20 +770,31 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   int max_nefc = env_nefc ? atoi(env_nefc) : 192;
   int max_ncon = env_ncon ? atoi(env_ncon) : 64;
   if (max_nefc > 64 * MGX_EFC_SLOTS) max_nefc = 64 * MGX_EFC_SLOTS;
+  max_nefc = (max_nefc + 3) & ~3;  // the staged solver sweeps rows in blocks of 4
+  if (max_nefc < 4 || max_ncon < 1) { delete m; return fail(MGX_E_ARG, "MGX_MAX_NEFC / MGX_MAX_NCON too small"); }
   int rb = precision == MGX_F32 ? 4 : 8;
-  m->L = make_layout(d, rb, max_ncon, max_nefc, 128);
+  m->L = make_layout(d, rb, max_ncon, max_nefc, 128, false);
+  m->Ls = make_layout(d, rb, max_ncon, max_nefc, 128, true);
+  m->Lf = finisher_layout(m->Ls, rb);
   int rc;
-  if (precision == MGX_F32) { rc = build_model<float>(d, device, m, m->mf); m->mf.L = m->L; }
-  else { rc = build_model<double>(d, device, m, m->md); m->md.L = m->L; }
+  if (precision == MGX_F32) {
+    rc = build_model<float>(d, device, m, m->mf);
+    m->mf.L = m->L; m->mfs = m->mf; m->mfs.L = m->Ls; m->mff = m->mf; m->mff.L = m->Lf;
+  } else {
+    rc = build_model<double>(d, device, m, m->md);
+    m->md.L = m->L; m->mds = m->md; m->mds.L = m->Ls; m->mdf = m->md; m->mdf.L = m->Lf;
+  }
   if (rc != MGX_OK) { delete m; return rc; }
   if (m->L.bytes > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "per-env LDS exceeds 160 KiB"); }
   int r2 = precision == MGX_F32
                ? (set_lds(k_step<float>, m->L.bytes) | set_lds(k_debug_forward<float>, m->L.bytes) |
                   set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes) |
-                  set_lds(k_soccer_logic<float>, m->L.bytes))
+                  set_lds(k_soccer_logic<float>, m->L.bytes) | set_lds(k_soccer_fixup<float>, m->L.bytes) | set_lds(k_soccer_template<float>, m->L.bytes) |
+                  set_lds(k_soccer_rows<float>, m->Ls.bytes) | set_lds(k_soccer_finish<float>, m->Lf.bytes))
                : (set_lds(k_step<double>, m->L.bytes) | set_lds(k_debug_forward<double>, m->L.bytes) |
                   set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes) |
-                  set_lds(k_soccer_logic<double>, m->L.bytes));
+                  set_lds(k_soccer_logic<double>, m->L.bytes) | set_lds(k_soccer_fixup<double>, m->L.bytes) | set_lds(k_soccer_template<double>, m->L.bytes) |
+                  set_lds(k_soccer_rows<double>, m->Ls.bytes) | set_lds(k_soccer_finish<double>, m->Lf.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
   *out = m;
   return MGX_OK;
@@ -519,6 +815,7 @@ int mgx_model_get_info(const mgx_model* m, mgx_model_info* o) {
   o->nq = nq; o->nv = nv; o->nu = nu; o->nbody = nb; o->njnt = nj; o->ngeom = ng; o->npair = m->npair;
   o->max_nv = MGX_MAX_NV; o->max_nbody = 4096; o->max_ncon = m->L.max_ncon; o->max_nefc = m->L.max_nefc;
   o->max_njnt = 1 << 20; o->precision = m->precision; o->lds_bytes_per_env = m->L.bytes;
+  o->lds_bytes_rows = m->Ls.bytes; o->lds_bytes_finish = m->Lf.bytes;
   return MGX_OK;
 }
 
@@ -618,14 +915,23 @@ int mgx_soccer_step(const mgx_model* m, const mgx_state* s, const mgx_soccer_env
   if (rc) return rc;
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (e->workspace) {
+    if (e->banks < 0 || e->banks > 16) return fail(MGX_E_ARG, "banks must be in [0, 16]");
+    if (m->precision == MGX_F32)
+      return soccer_step_staged<float>(m, m->mf, m->mfs, m->mff, m->sf, s, e, action, obs, reward, terminated,
+                                       truncated, final_obs, autoreset, seed, env_offset, n_env, mask, st);
+    return soccer_step_staged<double>(m, m->md, m->mds, m->mdf, m->sd, s, e, action, obs, reward, terminated, truncated,
+                                      final_obs, autoreset, seed, env_offset, n_env, mask, st);
+  }
+  Pipe none{};
   if (m->precision == MGX_F32)
     hipLaunchKernelGGL((k_soccer<float, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e, action,
                        (const float*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
-                       env_offset, n_env, mask);
+                       env_offset, n_env, mask, none, 0);
   else
     hipLaunchKernelGGL((k_soccer<double, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e, action,
                        (const double*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
-                       env_offset, n_env, mask);
+                       env_offset, n_env, mask, none, 0);
   HIPCHK(hipGetLastError());
   return MGX_OK;
 }
@@ -639,14 +945,44 @@ int mgx_soccer_reset(const mgx_model* m, const mgx_state* s, const mgx_soccer_en
   if (rc) return rc;
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
+  Pipe P{};
+  int use_pipe = 0;
+  if (e->workspace && !draws && e->banks > 0) {
+    if (e->banks > 16) return fail(MGX_E_ARG, "banks must be in [0, 16]");
+    size_t need = make_pipe(m, e->workspace, n_env, e->banks, &P);
+    if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
+    use_pipe = 1;
+  }
   if (m->precision == MGX_F32)
     hipLaunchKernelGGL((k_soccer<float, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e,
                        (const float*)nullptr, (const float*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
-                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
+                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask, P, use_pipe);
   else
     hipLaunchKernelGGL((k_soccer<double, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e,
                        (const float*)nullptr, (const double*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
-                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
+                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask, P, use_pipe);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+int64_t mgx_soccer_workspace_bytes(const mgx_model* m, int n_env, int banks) {
+  if (!m || n_env <= 0 || banks < 0 || banks > 16) return fail(MGX_E_ARG, "bad argument");
+  return (int64_t)make_pipe(m, nullptr, n_env, banks, nullptr);
+}
+
+int mgx_soccer_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, void* stream) {
+  if (!m || !workspace || n_env <= 0 || banks < 0 || banks > 16) return fail(MGX_E_ARG, "bad argument");
+  Pipe P;
+  size_t need = make_pipe(m, workspace, n_env, banks, &P);
+  if (bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(workspace, 0, need, st));
+  size_t nb = (size_t)n_env * (banks > 0 ? banks : 1);
+  HIPCHK(hipMemsetAsync(P.base + P.o_bk, 0xFF, nb * 4, st));  // bank settle counters = -1 (empty)
+  if (m->precision == MGX_F32)
+    hipLaunchKernelGGL(k_soccer_template<float>, dim3(1), dim3(64), m->L.bytes, st, m->mf, P);
+  else
+    hipLaunchKernelGGL(k_soccer_template<double>, dim3(1), dim3(64), m->L.bytes, st, m->md, P);
   HIPCHK(hipGetLastError());
   return MGX_OK;
 }

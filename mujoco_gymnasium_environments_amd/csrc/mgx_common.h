@@ -25,16 +25,19 @@ enum { C_LIMIT_JOINT = 3, C_CONTACT_FRICTIONLESS = 5, C_CONTACT_PYRAMIDAL = 6 };
 // LDS layout, in elements of T (reals) or int32 (ints), offsets computed on the host.
 struct Layout {
   int qpos, qvel, ctrl, xfrc, xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cfrc;
-  int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, geom_xpos, geom_xmat, act_force;
+  int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, vec3, geom_xpos, geom_xmat, act_force;
   int con_dist, con_pos, con_frame, con_mu;
   int efc, efc_margin, efc_blk;
   int Bmat, Bstride;
   int reals;  // total reals
   // int region (after reals)
-  int con_geom, con_pair, act_list, efc_type, efc_id;
+  int con_geom, con_pair, act_list, efc_type, efc_id, con_efcadr;
   int ints;
   int bytes;
   int max_ncon, max_nefc, max_active;
+  // staged pipeline: reals [0, carry_reals) and ints [0, carry_ints) are handed from the row
+  // builder to the finisher through HBM; B rows are built chunk_rows at a time
+  int staged, carry_reals, carry_ints, chunk_rows;
 };
 
 // Device-resident model: pointers into one device allocation.

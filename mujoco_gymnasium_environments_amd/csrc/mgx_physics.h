@@ -19,7 +19,7 @@ namespace mgx {
 template <typename T>
 struct Env {
   T *qpos, *qvel, *ctrl, *xfrc, *xpos, *xquat, *xmat, *xipos, *ximat, *subtree_com, *cinert, *crb, *cvel, *cfrc;
-  T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *geom_xpos, *geom_xmat, *act_force;
+  T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *vec3, *geom_xpos, *geom_xmat, *act_force;
   T *con_dist, *con_pos, *con_frame, *con_mu;  // con_mu = |friction[0:2]| (soccer obs)
   // per-row constraint data, AoS with stride 8 so the solver fetches a row's scalars with one
   // 16-byte LDS read: [0] b, [1] f, [2] R (diagApprox until impedance), [3] 1/AR_rr,
@@ -27,7 +27,7 @@ struct Env {
   T *efc, *efc_margin, *efc_blk;
   T *Bm;
   int Bs;
-  int *con_geom, *con_pair, *act_list, *efc_type, *efc_id;
+  int *con_geom, *con_pair, *act_list, *efc_type, *efc_id, *con_efcadr;
   int ncon, nefc, niter, overflow;
   // dof-lane registers
   T qacc_ws, qfrc_applied, qfrc_smooth, qacc_smooth, qacc, qfrc_constraint, diaginv, time;
@@ -44,13 +44,13 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.ximat = R + L.ximat; e.subtree_com = R + L.subtree_com; e.cinert = R + L.cinert; e.crb = R + L.crb;
   e.cvel = R + L.cvel; e.cfrc = R + L.cfrc; e.xaxis = R + L.xaxis; e.xanchor = R + L.xanchor;
   e.cdof = R + L.cdof; e.cdof_dot = R + L.cdof_dot; e.qLD = R + L.qLD; e.qMH = R + L.qMH;
-  e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.geom_xpos = R + L.geom_xpos;
+  e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.vec3 = R + L.vec3; e.geom_xpos = R + L.geom_xpos;
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.con_dist = R + L.con_dist;
   e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
   e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
   int* I = reinterpret_cast<int*>(R + L.reals);
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
-  e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id;
+  e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id; e.con_efcadr = I + L.con_efcadr;
   int l = lane_id();
   e.chainlen = l < m.nv ? m.dof_chainlen[l] : 0;
   e.ancmask = l < m.nv ? m.dof_ancmask[l] : 0ull;

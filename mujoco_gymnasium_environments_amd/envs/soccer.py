@@ -21,7 +21,7 @@ import torch
 
 from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
-from ..native import check, lib
+from ..native import NativeError, check, lib
 from ..seeding import np_random
 from ..spaces import Box, EnvBase
 
@@ -117,7 +117,11 @@ class SoccerVectorEnv:
     metadata = {'render_modes': [], 'render_fps': 50}
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
-                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
+                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
+                 staged: bool = True, banks: int = 4):
+        """``staged`` selects the row-builder / lane-group PGS / finisher kernels
+        with ``banks`` precomputed resets per env; ``staged=False`` runs one monolithic wave per
+        env. Both compute the same step (parity-tested against each other and the oracle)."""
         self.num_envs = num_envs
         self.device = torch.device(device)
         self.model = soccer_model()
@@ -145,6 +149,18 @@ class SoccerVectorEnv:
         self._env = cabi.MgxSoccerEnv(*[t.data_ptr() for t in (self.prev_ball_pos, self.prev_robot_pos, self.wind,
                                                                self.step_count, self.goal_scored, self.stats,
                                                                self.episode, self.flags, self.rollout)])
+        self.staged = staged
+        self.workspace = None
+        if staged:
+            nb = int(lib().mgx_soccer_workspace_bytes(self.native.handle, N, banks))
+            if nb <= 0:
+                raise NativeError(f"mgx_soccer_workspace_bytes: {lib().mgx_last_error().decode()}")
+            self.workspace = torch.empty(nb, dtype=torch.uint8, device=dev)
+            check(lib().mgx_soccer_workspace_init(self.native.handle, _ptr(self.workspace), nb, N, banks, None),
+                  "mgx_soccer_workspace_init")
+            self._env.workspace = self.workspace.data_ptr()
+            self._env.workspace_bytes = nb
+            self._env.banks = banks
         ids = self.tables.ids_struct()
         check(lib().mgx_soccer_configure(self.native.handle, C.byref(ids)), "mgx_soccer_configure")
         nq = np.array([int(self.model.jnt_qposadr[j]) for j in self.tables.noise_joints], dtype=np.int32)
@@ -220,8 +236,9 @@ class HumanoidSoccerEnv(EnvBase):
         self.dt = 0.02
         self.max_episode_steps = MAX_EPISODE_STEPS
         self.render_mode = render_mode
+        # one env: the single-launch monolithic kernel has the lowest step latency
         self._vec = SoccerVectorEnv(1, device=device, precision=precision, autoreset=False,
-                                    max_episode_steps=self.max_episode_steps)
+                                    max_episode_steps=self.max_episode_steps, staged=False)
         self.model = self._vec.model
         self.num_joints = self.model.nu
         self.action_space = Box(low=-150.0, high=150.0, shape=(self.num_joints,), dtype=np.float32)

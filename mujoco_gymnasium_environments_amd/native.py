@@ -16,7 +16,7 @@ ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
 SOURCES = ["mgx_api.hip"]
-HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h"]
+HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h"]
 
 MGX_OK = 0
 MGX_F32 = 0
@@ -65,6 +65,8 @@ _SIGS = {
     "mgx_soccer_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, C.c_uint64,
                           C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_soccer_logic_test": ([_VP, C.POINTER(cabi.MgxSoccerLogicIO), C.c_int, _VP], C.c_int),
+    "mgx_soccer_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
+    "mgx_soccer_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
 }
 EXPORTS = tuple(_SIGS)
 

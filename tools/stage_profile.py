@@ -16,6 +16,9 @@ from mujoco_gymnasium_environments_amd import native  # noqa: E402
 PROF_LIB = os.path.join(native.PKG, "libmgx_prof.so")
 STAGES = ["kinematics", "com_crb", "factorM", "velocity", "qacc_smooth", "collision", "make_constraint",
           "transform_rows", "pgs", "euler"]
+# staged row builder (k_soccer_rows): blocks 0..N-1 live envs, N.. bank slots
+STAGES_ROWS = ["kinematics", "com_crb", "factorM", "velocity", "qacc_smooth", "collision", "rows_meta",
+               "rows (J, transform, scalars, A_ij, out)"]
 
 
 def build():
@@ -25,6 +28,7 @@ def build():
 
 
 def main():
+    import numpy as np
     if "--build" in sys.argv:
         build()
         return
@@ -35,9 +39,11 @@ def main():
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     n = int(os.environ.get("N", "4096"))
     steps = int(os.environ.get("K", "20"))
-    env = SoccerVectorEnv(n, seed=3)
+    staged = os.environ.get("MODE", "staged") == "staged"
+    env = SoccerVectorEnv(n, seed=3, staged=staged)
     env.reset()
-    buf = torch.zeros(n * 32, dtype=torch.int64, device="cuda:0")
+    nslot = n * 5 if staged else n
+    buf = torch.zeros(nslot * 32, dtype=torch.int64, device="cuda:0")
     g = torch.Generator(device="cuda:0"); g.manual_seed(0)
     acts = [(torch.rand(n, env.model.nu, device="cuda:0", generator=g) * 300 - 150) for _ in range(4)]
     for k in range(5):
@@ -47,17 +53,32 @@ def main():
     for k in range(steps):
         env.step(acts[k % 4])
     torch.cuda.synchronize()
-    v = buf.view(n, 32).double().cpu().numpy() / steps
-    tot = v[:, :10].sum(1).mean()
-    print(f"envs={n} steps={steps} mean cycles/env-step (s_memtime units) total={tot:.0f}")
-    for i, s in enumerate(STAGES):
-        print(f"  {s:16s} {v[:, i].mean():12.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {sorted(v[:, i])[int(0.99 * n)]:.0f}")
-    print(f"  lds bytes per env {env.native.info.lds_bytes_per_env}")
-    raw = buf.view(n, 32).double().cpu().numpy()
+    raw = buf.view(nslot, 32).double().cpu().numpy()
+    if staged:
+        calls = np.maximum(raw[:, 23], 1)
+        act = raw[:, 23] > 0
+        v = raw[act] / calls[act, None]
+        names = STAGES_ROWS
+        print(f"staged row builder: envs={n} steps={steps} slots with work {act.sum()} "
+              f"(live {act[:n].sum()}, bank {act[n:].sum()}); mean cycles per slot-step (s_memtime units)")
+    else:
+        v = raw / steps
+        names = STAGES
+        print(f"monolithic: envs={n} steps={steps} mean cycles/env-step (s_memtime units)")
+    tot = v[:, :len(names)].sum(1).mean()
+    print(f"  total {tot:.0f}")
+    for i, s in enumerate(names):
+        print(f"  {s:40s} {v[:, i].mean():12.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {np.percentile(v[:, i], 99):.0f}")
+    print(f"  lds bytes per env: monolithic {env.native.info.lds_bytes_per_env} rows {env.native.info.lds_bytes_rows} "
+          f"finish {env.native.info.lds_bytes_finish}")
+    if staged:
+        print(f"  per slot-step: nefc mean {(raw[:, 20].sum() / raw[:, 23].sum()):.1f}  ncon mean "
+              f"{(raw[:, 22].sum() / raw[:, 23].sum()):.1f}  nefc max {raw[:, 24].max():.0f}  "
+              f"slot-steps with capacity overflow {raw[:, 25].sum():.0f} of {raw[:, 23].sum():.0f}")
+        return
     calls = raw[:, 23].sum()
     print(f"  per forward: nefc mean {raw[:, 20].sum() / calls:.1f}  PGS iterations mean {raw[:, 21].sum() / calls:.1f}"
           f"  ncon mean {raw[:, 22].sum() / calls:.1f}  forwards per env-step {calls / (n * steps):.2f}")
-    import numpy as np
     nefc_env = raw[:, 20] / np.maximum(raw[:, 23], 1)
     print(f"  per-env mean nefc p50 {np.percentile(nefc_env, 50):.0f} p90 {np.percentile(nefc_env, 90):.0f} max {nefc_env.max():.0f}")
 
