@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   com_crb(m, e);
   for (int k = l; k < m.nM; k += 64) D[o.qM + k] = e.qLD[k];
   wsync();
-  e.diaginv = factor_ld(m, e.qLD);
+  e.diaginv = factor_ld(m, e, e.qLD);
   for (int k = l; k < m.nM; k += 64) D[o.qLD + k] = e.qLD[k];
   velocity(m, e);
   e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
@@ -512,7 +512,8 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   int vec_end = p;
   // persistent for the rest of the forward pass
   L.cdof = take(6 * nv); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
-  L.efc = take(8 * max_nefc); L.efc_margin = take(max_nefc); L.efc_blk = take(staged ? 1 : 2 * max_nefc);
+  L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged ? 1 : max_nefc);
+  L.efc_blk = take(staged ? 1 : 2 * max_nefc);
   // union: phase A (kinematics .. collision) arrays, then B rows on top (all rows for the
   // monolithic kernel, one chunk of rows for the staged row builder)
   int u0 = p;
@@ -520,10 +521,17 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.crb = take(10 * nb); L.cvel = take(6 * nb); L.cfrc = take(6 * nb); L.cdof_dot = take(6 * nv);
   L.xaxis = take(3 * nj); L.xanchor = take(3 * nj); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
   L.act_force = take(d->nu);
+  // staged: per-body sums of cdof * (qacc_smooth | qacc_warmstart), built after the velocity
+  // stage, over xmat .. crb (dead by then; cvel, read with it, lies beyond them)
+  L.cacc = L.xmat;
   int endA = p;
+  // staged: per-row impedance constants (4 per row) over cfrc .. (dead after velocity and
+  // collision), or their own space when that tail is too short
+  L.rowc = staged ? (endA - L.cfrc >= 4 * max_nefc ? L.cfrc : take(4 * max_nefc)) : 0;
+  if (staged && L.rowc != L.cfrc) endA = p;
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
   L.Bmat = u0;
-  L.chunk_rows = staged ? 64 : max_nefc;
+  L.chunk_rows = staged ? 0 : max_nefc;  // the staged row builder keeps rows in registers
   int endB = align_up(u0 + L.chunk_rows * L.Bstride, al);
   L.reals = endA > endB ? endA : endB;
   int q = 0;
@@ -531,7 +539,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.con_geom = takei(2 * max_ncon);
   L.carry_ints = q;
   L.con_pair = takei(max_ncon); L.act_list = takei(max_active);
-  L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc); L.con_efcadr = takei(max_ncon);
+  L.efc_type = takei(staged ? 1 : max_nefc); L.efc_id = takei(max_nefc); L.con_efcadr = takei(1);
   L.ints = q;
   L.bytes = L.reals * real_bytes + L.ints * 4;
   (void)vec_end;
@@ -590,13 +598,14 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
     depth[b] = (int)path.size();
     for (int c = 0; c < depth[b]; c++) chain[b * MGX_MAX_DEPTH + c] = path[depth[b] - 1 - c];
   }
-  std::vector<int> chainlen(nv), anc(nv * MGX_MAX_DEPTH, -1);
+  std::vector<int> chainlen(nv), anc(nv * MGX_MAX_DEPTH, -1), ancadr(nv * MGX_MAX_DEPTH, 0);
   std::vector<uint64_t> ancmask(nv, 0);
   for (int k = 0; k < nv; k++) {
     int t = 0;
     for (int j = k; j >= 0; j = d->dof_parentid[j], t++) {
       if (t >= MGX_MAX_DEPTH) return fail(MGX_E_CAPACITY, "dof chain longer than MGX_MAX_DEPTH");
       anc[k * MGX_MAX_DEPTH + t] = j;
+      ancadr[k * MGX_MAX_DEPTH + t] = d->dof_Madr[j];
       if (j != k) ancmask[k] |= 1ull << j;
     }
     chainlen[k] = t;
@@ -622,6 +631,7 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
   B.ints(d->dof_parentid, nv, &M.dof_parentid); B.ints(d->dof_Madr, nv, &M.dof_Madr);
   B.ints(chainlen.data(), nv, &M.dof_chainlen); B.ints(anc.data(), anc.size(), &M.dof_anc);
   B.add(ancmask.data(), 8 * ancmask.size(), (const void**)&M.dof_ancmask);
+  B.ints(ancadr.data(), ancadr.size(), &M.dof_ancadr);
   B.reals(d->dof_armature, nv, &M.dof_armature); B.reals(d->dof_damping, nv, &M.dof_damping);
   B.reals(d->dof_invweight0, nv, &M.dof_invweight0);
   B.ints(d->geom_type, ng, &M.geom_type); B.ints(d->geom_bodyid, ng, &M.geom_bodyid);

@@ -25,7 +25,7 @@ enum { C_LIMIT_JOINT = 3, C_CONTACT_FRICTIONLESS = 5, C_CONTACT_PYRAMIDAL = 6 };
 // LDS layout, in elements of T (reals) or int32 (ints), offsets computed on the host.
 struct Layout {
   int qpos, qvel, ctrl, xfrc, xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cfrc;
-  int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, vec3, geom_xpos, geom_xmat, act_force;
+  int xaxis, xanchor, cdof, cdof_dot, qLD, qMH, vec0, vec1, vec2, vec3, geom_xpos, geom_xmat, act_force, cacc, rowc;
   int con_dist, con_pos, con_frame, con_mu;
   int efc, efc_margin, efc_blk;
   int Bmat, Bstride;
@@ -57,6 +57,7 @@ struct DevModel {
   // dofs
   const int *dof_bodyid, *dof_jntid, *dof_parentid, *dof_Madr, *dof_chainlen, *dof_anc;  // anc: [nv][MAX_DEPTH]
   const uint64_t *dof_ancmask;  // bit i set if dof i is a strict ancestor of the dof
+  const int *dof_ancadr;        // [nv][MAX_DEPTH]: dof_Madr of ancestor t (0 past the chain)
   const T *dof_armature, *dof_damping, *dof_invweight0;
   // geoms
   const int *geom_type, *geom_bodyid;
@@ -104,6 +105,10 @@ __device__ __forceinline__ double readlane(double x, int l) {
   return __builtin_bit_cast(double, v);
 }
 __device__ __forceinline__ int readlane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
+  uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, l), hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // full-wave sum, result in every lane (butterfly over 6 xor steps)
 template <typename T>

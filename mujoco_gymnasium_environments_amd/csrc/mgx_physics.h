@@ -19,7 +19,7 @@ namespace mgx {
 template <typename T>
 struct Env {
   T *qpos, *qvel, *ctrl, *xfrc, *xpos, *xquat, *xmat, *xipos, *ximat, *subtree_com, *cinert, *crb, *cvel, *cfrc;
-  T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *vec3, *geom_xpos, *geom_xmat, *act_force;
+  T *xaxis, *xanchor, *cdof, *cdof_dot, *qLD, *qMH, *vec0, *vec1, *vec2, *vec3, *geom_xpos, *geom_xmat, *act_force, *cacc, *rowc;
   T *con_dist, *con_pos, *con_frame, *con_mu;  // con_mu = |friction[0:2]| (soccer obs)
   // per-row constraint data, AoS with stride 8 so the solver fetches a row's scalars with one
   // 16-byte LDS read: [0] b, [1] f, [2] R (diagApprox until impedance), [3] 1/AR_rr,
@@ -31,7 +31,7 @@ struct Env {
   int ncon, nefc, niter, overflow;
   // dof-lane registers
   T qacc_ws, qfrc_applied, qfrc_smooth, qacc_smooth, qacc, qfrc_constraint, diaginv, time;
-  int chainlen;
+  int chainlen, madr;  // this lane's dof: chain length, dof_Madr
   uint64_t ancmask;
 };
 
@@ -45,7 +45,7 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.cvel = R + L.cvel; e.cfrc = R + L.cfrc; e.xaxis = R + L.xaxis; e.xanchor = R + L.xanchor;
   e.cdof = R + L.cdof; e.cdof_dot = R + L.cdof_dot; e.qLD = R + L.qLD; e.qMH = R + L.qMH;
   e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.vec3 = R + L.vec3; e.geom_xpos = R + L.geom_xpos;
-  e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.con_dist = R + L.con_dist;
+  e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.cacc = R + L.cacc; e.rowc = R + L.rowc; e.con_dist = R + L.con_dist;
   e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
   e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
   int* I = reinterpret_cast<int*>(R + L.reals);
@@ -53,6 +53,7 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id; e.con_efcadr = I + L.con_efcadr;
   int l = lane_id();
   e.chainlen = l < m.nv ? m.dof_chainlen[l] : 0;
+  e.madr = l < m.nv ? m.dof_Madr[l] : 0;
   e.ancmask = l < m.nv ? m.dof_ancmask[l] : 0ull;
   e.overflow = 0;
 }
@@ -282,33 +283,55 @@ __device__ __forceinline__ void com_crb(const DevModel<T>& m, Env<T>& e) {
   wsync();
 }
 
-// mj_factorI on an LDS tree-sparse matrix: M = L' D L in place; returns diaginv in a register
+// mj_factorI on an LDS tree-sparse matrix: M = L' D L in place; returns diaginv in a register.
+// Step k updates the (t, s) pairs of its ancestor block in parallel: lane -> t = (l & 15) + 1,
+// s = s0 + (l >> 4), 4 values of s per pass; the ancestors' Madr come from the host table
+// dof_ancadr, prefetched one step ahead.
 template <typename T>
-__device__ __forceinline__ T factor_ld(const DevModel<T>& m, T* LD) {
+__device__ __forceinline__ T factor_ld(const DevModel<T>& m, const Env<T>& e, T* LD) {
   int l = lane_id();
+  const int t = (l & 15) + 1, sl = l >> 4;
+  int ai_next = m.nv > 0 ? m.dof_ancadr[(m.nv - 1) * MGX_MAX_DEPTH + (t & 15)] : 0;
   for (int k = m.nv - 1; k >= 0; k--) {
-    int akk = m.dof_Madr[k];
-    int mk = m.dof_chainlen[k] - 1;  // number of ancestors
+    int akk = readlane(e.madr, k);
+    int mk = readlane(e.chainlen, k) - 1;  // number of ancestors
+    int ai = ai_next;
+    if (k > 0) ai_next = m.dof_ancadr[(k - 1) * MGX_MAX_DEPTH + (t & 15)];
     T dkk = LD[akk];
     if (dkk < minval<T>()) dkk = minval<T>();
-    // pairs (t, s): t = 1..mk (ancestor index), s = 0..mk-t
-    int npair = mk * (mk + 1) / 2;
-    T tmp_own = 0;
-    for (int p = l; p < npair; p += 64) {
-      int t = 1, rem = p;
-      while (rem >= mk - t + 1) { rem -= mk - t + 1; t++; }
-      int s = rem;
-      T tmp = LD[akk + t] / dkk;
-      int ai = m.dof_Madr[m.dof_anc[k * MGX_MAX_DEPTH + t]];
-      LD[ai + s] -= LD[akk + t + s] * tmp;
+    T tmp = t <= mk ? LD[akk + t] / dkk : (T)0;
+    for (int s0 = 0; s0 < mk; s0 += 4) {
+      int s = s0 + sl;
+      if (t <= mk && s <= mk - t) LD[ai + s] -= LD[akk + t + s] * tmp;
     }
-    if (l >= 1 && l <= mk) tmp_own = LD[akk + l] / dkk;
+    T tmp_own = (l >= 1 && l <= mk) ? LD[akk + l] / dkk : (T)0;
     wsync();
     if (l >= 1 && l <= mk) LD[akk + l] = tmp_own;
     if (l == 0) LD[akk] = dkk;
     wsync();
   }
-  return l < m.nv ? (T)1 / LD[m.dof_Madr[l]] : (T)0;
+  return l < m.nv ? (T)1 / LD[e.madr] : (T)0;
+}
+
+// B_r = D^-1/2 L'^-1 J_r' for one row x (LDS, lane-private): for k = nv-1 .. 0 the ancestors
+// of k get x[anc] -= L[k][anc] x[k]. The ancestors of one k are distinct, so all their loads
+// are issued before any store (one LDS latency per k instead of one per ancestor).
+template <typename T>
+__device__ __forceinline__ void transform_row(const DevModel<T>& m, const Env<T>& e, T* x, const T* dinv_sqrt) {
+  for (int k = m.nv - 1; k >= 0; k--) {
+    const int* ak = m.dof_anc + k * MGX_MAX_DEPTH;
+    int mk = readlane(e.chainlen, k) - 1;
+    int a = readlane(e.madr, k) + 1;
+    T xk = x[k];
+    T xa[MGX_MAX_DEPTH], la[MGX_MAX_DEPTH];
+#pragma unroll
+    for (int t = 1; t < MGX_MAX_DEPTH; t++)
+      if (t <= mk) { xa[t] = x[ak[t]]; la[t] = e.qLD[a + t - 1]; }
+#pragma unroll
+    for (int t = 1; t < MGX_MAX_DEPTH; t++)
+      if (t <= mk) x[ak[t]] = xa[t] - la[t] * xk;
+    x[k] = xk * dinv_sqrt[k];
+  }
 }
 
 // x <- L'^-1 x (lane-distributed vector)
@@ -317,8 +340,9 @@ __device__ __forceinline__ T solve_LT(const DevModel<T>& m, const Env<T>& e, con
   int l = lane_id();
   for (int k = m.nv - 1; k >= 0; k--) {
     T xk = readlane(x, k);
-    uint64_t am = m.dof_ancmask[k];
-    if (l < m.nv && ((am >> l) & 1ull)) x -= LD[m.dof_Madr[k] + m.dof_chainlen[k] - e.chainlen] * xk;
+    uint64_t am = readlane_u64(e.ancmask, k);
+    int base = readlane(e.madr, k) + readlane(e.chainlen, k);
+    if (l < m.nv && ((am >> l) & 1ull)) x -= LD[base - e.chainlen] * xk;
   }
   return x;
 }
@@ -326,10 +350,11 @@ __device__ __forceinline__ T solve_LT(const DevModel<T>& m, const Env<T>& e, con
 template <typename T>
 __device__ __forceinline__ T solve_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
   int l = lane_id();
-  int madr = l < m.nv ? m.dof_Madr[l] : 0;
+  const int base = e.madr + e.chainlen;
   for (int i = 0; i < m.nv; i++) {
     T xi = readlane(x, i);
-    if (l < m.nv && ((e.ancmask >> i) & 1ull)) x -= LD[madr + e.chainlen - m.dof_chainlen[i]] * xi;
+    int ci = readlane(e.chainlen, i);
+    if (l < m.nv && ((e.ancmask >> i) & 1ull)) x -= LD[base - ci] * xi;
   }
   return x;
 }
@@ -337,11 +362,12 @@ __device__ __forceinline__ T solve_L(const DevModel<T>& m, const Env<T>& e, cons
 template <typename T>
 __device__ __forceinline__ T mul_L(const DevModel<T>& m, const Env<T>& e, const T* LD, T x) {
   int l = lane_id();
-  int madr = l < m.nv ? m.dof_Madr[l] : 0;
+  const int base = e.madr + e.chainlen;
   T y = x;
   for (int i = 0; i < m.nv; i++) {
     T xi = readlane(x, i);
-    if (l < m.nv && ((e.ancmask >> i) & 1ull)) y += LD[madr + e.chainlen - m.dof_chainlen[i]] * xi;
+    int ci = readlane(e.chainlen, i);
+    if (l < m.nv && ((e.ancmask >> i) & 1ull)) y += LD[base - ci] * xi;
   }
   return y;
 }
@@ -352,8 +378,9 @@ __device__ __forceinline__ T mul_LT(const DevModel<T>& m, const Env<T>& e, const
   T y = u;
   for (int k = 0; k < m.nv; k++) {
     T uk = readlane(u, k);
-    uint64_t am = m.dof_ancmask[k];
-    if (l < m.nv && ((am >> l) & 1ull)) y += LD[m.dof_Madr[k] + m.dof_chainlen[k] - e.chainlen] * uk;
+    uint64_t am = readlane_u64(e.ancmask, k);
+    int base = readlane(e.madr, k) + readlane(e.chainlen, k);
+    if (l < m.nv && ((am >> l) & 1ull)) y += LD[base - e.chainlen] * uk;
   }
   return y;
 }
@@ -434,6 +461,14 @@ __device__ __forceinline__ void collision(const DevModel<T>& m, Env<T>& e) {
 template <typename T>
 __device__ __forceinline__ bool body_has_dof(const DevModel<T>& m, int b, int d) {
   return (m.body_dofmask[b * m.nmaskword + (d >> 5)] >> (d & 31)) & 1u;
+}
+
+// dofs moving body b (its chain), nv <= 64
+template <typename T>
+__device__ __forceinline__ uint64_t body_mask64(const DevModel<T>& m, int b) {
+  uint64_t lo = m.body_dofmask[b * m.nmaskword];
+  uint64_t hi = m.nmaskword > 1 ? m.body_dofmask[b * m.nmaskword + 1] : 0u;
+  return lo | (hi << 32);
 }
 
 template <typename T>
@@ -584,16 +619,7 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
 template <typename T>
 __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
-  for (int r = l; r < e.nefc; r += 64) {
-    T* x = e.Bm + r * e.Bs;
-    for (int k = m.nv - 1; k >= 0; k--) {
-      T xk = x[k];
-      int a = m.dof_Madr[k] + 1;
-      int mk = m.dof_chainlen[k] - 1;
-      for (int t = 1; t <= mk; t++) x[m.dof_anc[k * MGX_MAX_DEPTH + t]] -= e.qLD[a + t - 1] * xk;
-      x[k] = xk * e.vec0[k];
-    }
-  }
+  for (int r = l; r < e.nefc; r += 64) transform_row(m, e, e.Bm + r * e.Bs, e.vec0);
   wsync();
 }
 
@@ -879,7 +905,7 @@ __device__ __forceinline__ void euler(const DevModel<T>& m, Env<T>& e) {
   T qa;
   if (!damp) qa = e.qacc;
   else {
-    T di = factor_ld(m, e.qMH);
+    T di = factor_ld(m, e, e.qMH);
     qa = solve_M(m, e, e.qMH, di, e.qfrc_smooth + e.qfrc_constraint);
   }
   if (l < m.nv) e.qvel[l] += m.timestep * qa;
@@ -910,7 +936,7 @@ __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
   MGX_STAMP(0);
   com_crb(m, e);
   MGX_STAMP(1);
-  e.diaginv = factor_ld(m, e.qLD);
+  e.diaginv = factor_ld(m, e, e.qLD);
   MGX_STAMP(2);
   velocity(m, e);
   MGX_STAMP(3);

@@ -46,95 +46,79 @@ struct Pipe {
 };
 
 // ------------------------------------------------------------------ S1 helpers
-// Row metadata (limits, then contacts in contact order) + impedance: the metadata half of
-// make_constraint (mgx_physics.h), J rows are produced per chunk by build_chunk.
+// Row plan (mj_makeConstraint order [ext]): joint limits (joint order, lower then upper),
+// padded with dummy rows to a multiple of 4, then one 4-row block per contact (the 4 pyramid
+// rows; a condim-1 contact uses row 0 and 3 dummies). Dummy rows have B = 0, b = f = 0 and
+// never change in the sweeps, so the Gauss-Seidel sequence over the real rows is MuJoCo's.
+// The limit list goes to efc_id (code 2*joint + side). Returns nefc (padded).
 template <typename T>
-__device__ __forceinline__ void rows_meta(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ int rows_plan(const DevModel<T>& m, Env<T>& e, int* nlim_out, int* ncon_out) {
   int l = lane_id();
-  const Layout& L = m.L;
-  int nefc = 0;
+  const int maxE = m.L.max_nefc;
+  int nlim = 0;
   for (int base = 0; base < m.njnt; base += 64) {
     int j = base + l;
-    int cnt = 0;
-    T dl = 0, du = 0;
     bool lo = false, hi = false;
     if (j < m.njnt && m.jnt_limited[j] && (m.jnt_type[j] == JHINGE || m.jnt_type[j] == JSLIDE)) {
       T val = e.qpos[m.jnt_qposadr[j]], margin = m.jnt_margin[j];
-      dl = val - m.jnt_range[2 * j];
-      du = m.jnt_range[2 * j + 1] - val;
-      lo = dl < margin;
-      hi = du < margin;
-      cnt = (int)lo + (int)hi;
+      lo = val - m.jnt_range[2 * j] < margin;
+      hi = m.jnt_range[2 * j + 1] - val < margin;
     }
     int total;
-    int off = wave_excl_scan(cnt, &total);
-    int r = nefc + off;
-    for (int side = 0; side < 2; side++) {
-      bool on = side == 0 ? lo : hi;
-      if (!on) continue;
-      if (r < L.max_nefc) {
-        e.efc_type[r] = C_LIMIT_JOINT; e.efc_id[r] = j;
-        e.efc[8 * r + 7] = side == 0 ? dl : du;
-        e.efc_margin[r] = m.jnt_margin[j];
-        e.efc[8 * r + 2] = m.dof_invweight0[m.jnt_dofadr[j]];
-        e.efc[8 * r + 1] = side == 0 ? (T)1 : (T)-1;
-      }
-      r++;
-    }
-    nefc += total;
+    int off = wave_excl_scan((int)lo + (int)hi, &total);
+    int r = nlim + off;
+    if (lo) { if (r < maxE) e.efc_id[r] = 2 * j; r++; }
+    if (hi) { if (r < maxE) e.efc_id[r] = 2 * j + 1; }
+    nlim += total;
   }
-  if (nefc > L.max_nefc) { nefc = L.max_nefc; e.overflow |= 4; }
-  // contacts: row offsets by a scan over contacts, lane per contact
-  for (int base = 0; base < e.ncon; base += 64) {
-    int c = base + l;
-    int nrow = 0;
-    if (c < e.ncon) nrow = m.pair_condim[e.con_pair[c]] == 1 ? 1 : 4;
-    int total;
-    int off = wave_excl_scan(nrow, &total);
-    int adr = nefc + off;
-    bool fits = adr + nrow <= L.max_nefc;
-    if (c < e.ncon) {
-      e.con_efcadr[c] = fits ? adr : -1;
-      if (fits) {
-        int p = e.con_pair[c];
-        int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
-        int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-        T tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-        for (int i = 0; i < nrow; i++) {
-          int r = adr + i;
-          T f = nrow == 1 ? (T)0 : m.pair_friction[5 * p + (i >> 1)];
-          e.efc_type[r] = nrow == 1 ? C_CONTACT_FRICTIONLESS : C_CONTACT_PYRAMIDAL;
-          e.efc_id[r] = c;
-          e.efc[8 * r + 7] = e.con_dist[c];
-          e.efc_margin[r] = m.pair_margin[p] - m.pair_gap[p];
-          e.efc[8 * r + 2] = tran + f * f * tran;
-        }
-      }
-    }
-    // MuJoCo stops adding rows at the first contact that does not fit; row offsets grow with
-    // the contact index, so every later contact is dropped too
-    unsigned long long bad = ballot(c < e.ncon && !fits);
-    if (bad) {
-      nefc = readlane(adr, __builtin_ctzll(bad));
-      e.overflow |= 4;
-      break;
-    }
-    nefc += total;
-  }
-  e.nefc = __builtin_amdgcn_readfirstlane(nefc);
+  if (nlim > maxE) { nlim = maxE; e.overflow |= 4; }
+  int nlim4 = (nlim + 3) & ~3;
+  int ncf = e.ncon;
+  if (nlim4 + 4 * ncf > maxE) { ncf = (maxE - nlim4) / 4; e.overflow |= 4; }
+  *nlim_out = nlim;
+  *ncon_out = ncf;
   wsync();
-  for (int r = l; r < e.nefc; r += 64) {
-    const T *solref, *solimp;
-    if (e.efc_type[r] == C_LIMIT_JOINT) {
-      solref = m.jnt_solref + 2 * e.efc_id[r];
-      solimp = m.jnt_solimp + 5 * e.efc_id[r];
-    } else {
-      int p = e.con_pair[e.efc_id[r]];
-      solref = m.pair_solref + 2 * p;
-      solimp = m.pair_solimp + 5 * p;
+  return nlim4 + 4 * ncf;
+}
+
+// Per-row constants of mj_makeImpedance [ext], lane per row, into e.rowc (4 per row):
+// R, B (damping of aref), K*imp*(pos - margin), 1 for a real row / 0 for padding.
+template <typename T>
+__device__ __forceinline__ void rows_impedance(const DevModel<T>& m, Env<T>& e, int ne, int nlim, int nlim4) {
+  const int l = lane_id();
+  for (int r = l; r < ne; r += 64) {
+    const T *solref = nullptr, *solimp = nullptr;
+    T pos = 0, margin = 0, diag = 0;
+    if (r < nlim) {
+      int code = e.efc_id[r];
+      int jn = code >> 1, side = code & 1;
+      T val = e.qpos[m.jnt_qposadr[jn]];
+      pos = side ? m.jnt_range[2 * jn + 1] - val : val - m.jnt_range[2 * jn];
+      margin = m.jnt_margin[jn];
+      diag = m.dof_invweight0[m.jnt_dofadr[jn]];
+      solref = m.jnt_solref + 2 * jn;
+      solimp = m.jnt_solimp + 5 * jn;
+    } else if (r >= nlim4) {
+      int c = (r - nlim4) >> 2, i = (r - nlim4) & 3;
+      int p = e.con_pair[c];
+      int dim = m.pair_condim[p];
+      if (dim != 1 || i == 0) {
+        int b1 = m.geom_bodyid[e.con_geom[2 * c]], b2 = m.geom_bodyid[e.con_geom[2 * c + 1]];
+        T tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+        T f = dim == 1 ? (T)0 : m.pair_friction[5 * p + (i >> 1)];
+        pos = e.con_dist[c];
+        margin = m.pair_margin[p] - m.pair_gap[p];
+        diag = tran + f * f * tran;
+        solref = m.pair_solref + 2 * p;
+        solimp = m.pair_solimp + 5 * p;
+      }
     }
-    T pos = e.efc[8 * r + 7];
-    T imp = impedance(solimp, pos, e.efc_margin[r]);
+    T* o = e.rowc + 4 * r;
+    if (!solref) {
+      o[0] = 1; o[1] = 0; o[2] = 0; o[3] = 0;
+      continue;
+    }
+    T imp = impedance(solimp, pos, margin);
     T dmax = clampv(solimp[1], (T)0.0001, (T)0.9999), K, B;
     if (solref[0] > 0) {
       T tc = solref[0], dr = solref[1];
@@ -145,72 +129,201 @@ __device__ __forceinline__ void rows_meta(const DevModel<T>& m, Env<T>& e) {
       K = -solref[0] / (dmax * dmax);
       B = -solref[1] / dmax;
     }
-    T R = ((T)1 - imp) * e.efc[8 * r + 2] / imp;
-    e.efc[8 * r + 6] = B;
-    e.efc[8 * r + 5] = K * imp * (pos - e.efc_margin[r]);
-    e.efc[8 * r + 2] = R > minval<T>() ? R : minval<T>();
+    T R = ((T)1 - imp) * diag / imp;
+    o[0] = R > minval<T>() ? R : minval<T>();
+    o[1] = B;
+    o[2] = K * imp * (pos - margin);
+    o[3] = 1;
   }
-  wsync();
 }
 
-// J rows [c0, c1) into the chunk buffer (row r at Bm + (r - c0) * Bs)
+// Contact constants of the J build, lane per contact (c < 64), read back with readlane
 template <typename T>
-__device__ __forceinline__ void build_chunk(const DevModel<T>& m, Env<T>& e, int c0, int c1) {
-  int l = lane_id();
-  int r = c0 + l;
-  if (r < c1) {
-    T* row = e.Bm + (r - c0) * e.Bs;
-    for (int k = 0; k < m.nv; k++) row[k] = 0;
-    if (e.efc_type[r] == C_LIMIT_JOINT) row[m.jnt_dofadr[e.efc_id[r]]] = e.efc[8 * r + 1];
-  }
-  wsync();
-  // contacts whose rows intersect the chunk, lane = dof
-  int cfirst = e.efc_type[c0] == C_LIMIT_JOINT ? 0 : e.efc_id[c0];
-  cfirst = __builtin_amdgcn_readfirstlane(cfirst);
-  for (int c = cfirst; c < e.ncon; c++) {
-    int adr = e.con_efcadr[c];
-    if (adr < 0 || adr >= c1) break;
+struct ContactMeta {
+  int dim, b1, b2, rt1, rt2;
+  uint64_t m1, m2;
+  T mu0, mu1;
+};
+template <typename T>
+__device__ __forceinline__ void contact_meta(const DevModel<T>& m, const Env<T>& e, int ncf, ContactMeta<T>& cm) {
+  const int c = lane_id();
+  cm.dim = 3; cm.b1 = 0; cm.b2 = 0; cm.rt1 = 0; cm.rt2 = 0; cm.m1 = 0; cm.m2 = 0; cm.mu0 = 0; cm.mu1 = 0;
+  if (c < ncf) {
     int p = e.con_pair[c];
-    int dim = m.pair_condim[p];
-    int nrow = dim == 1 ? 1 : 4;
-    if (adr + nrow <= c0) continue;
-    int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
-    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+    cm.dim = m.pair_condim[p];
+    cm.b1 = m.geom_bodyid[e.con_geom[2 * c]];
+    cm.b2 = m.geom_bodyid[e.con_geom[2 * c + 1]];
+    cm.rt1 = m.body_rootid[cm.b1];
+    cm.rt2 = m.body_rootid[cm.b2];
+    cm.m1 = cm.b1 > 0 ? body_mask64(m, cm.b1) : 0ull;
+    cm.m2 = cm.b2 > 0 ? body_mask64(m, cm.b2) : 0ull;
+    cm.mu0 = m.pair_friction[5 * p];
+    cm.mu1 = m.pair_friction[5 * p + 1];
+  }
+}
+
+#ifdef MGX_PROFILE
+#define MGX_BSTAMP(slot)                                                                \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                               \
+    if (g_mgx_prof && threadIdx.x == 0) g_mgx_prof[blockIdx.x * 32 + (slot)] += _t - _bt; \
+    _bt = _t;                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+  } while (0)
+#else
+#define MGX_BSTAMP(slot) do {} while (0)
+#endif
+
+__device__ __forceinline__ float readlane_t(float x, int l) { return readlane(x, l); }
+__device__ __forceinline__ double readlane_t(double x, int l) { return readlane(x, l); }
+
+// One 4-row block, lane = dof: J rows in registers; J.qvel, J.qacc_smooth, J.qacc_warmstart
+// (= B.(D^1/2 L x) of the monolithic path) per row in lane i without a reduction (limit
+// rows: the dof's entry; contacts: the bodies' chain sums cvel / cacc at the contact point);
+// B = D^-1/2 L'^-1 J' by a readlane sweep over the block's dof support only (the two bodies'
+// chains, closed under ancestors, highest dof first); then B.B and the block couplings A_ij,
+// the row scalars and B -> pipe.
+template <typename T>
+__device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, const Pipe& P, int r0, int nlim, int nlim4,
+                                            const ContactMeta<T>& cm, T dinvs, T* scal, T* Bo) {
+  const int l = lane_id();
+  const int nv = m.nv;
+  const bool dl = l < nv;
+#ifdef MGX_PROFILE
+  unsigned long long _bt = __builtin_amdgcn_s_memtime();
+#endif
+  T j0 = 0, j1 = 0, j2 = 0, j3 = 0;
+  uint64_t sup = 0;
+  T dv = 0, ds = 0, dw = 0;
+  if (r0 < nlim4) {
+    T* jj[4] = {&j0, &j1, &j2, &j3};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      int r = r0 + i;
+      if (r < nlim) {
+        int code = e.efc_id[r];
+        int d = m.jnt_dofadr[code >> 1];
+        T sg = (code & 1) ? (T)-1 : (T)1;
+        *jj[i] = l == d ? sg : (T)0;
+        sup |= readlane_u64(e.ancmask, d) | (1ull << d);
+        if (l == i) { dv = sg * e.qvel[d]; ds = sg * e.vec1[d]; dw = sg * e.vec2[d]; }
+      }
+    }
+  } else {
+    const int c = (r0 - nlim4) >> 2;
+    const int dim = readlane(cm.dim, c), b1 = readlane(cm.b1, c), b2 = readlane(cm.b2, c);
+    const int rt1 = readlane(cm.rt1, c), rt2 = readlane(cm.rt2, c);
+    const uint64_t m1 = readlane_u64(cm.m1, c), m2 = readlane_u64(cm.m2, c);
+    const T mu0 = readlane_t(cm.mu0, c), mu1 = readlane_t(cm.mu1, c);
     const T* fr = e.con_frame + 9 * c;
-    const T* pos = e.con_pos + 3 * c;
-    if (l < m.nv) {
-      T j1[3] = {0, 0, 0}, j2[3] = {0, 0, 0};
+    const T* cp = e.con_pos + 3 * c;
+    sup = m1 | m2;
+    T o1[3] = {cp[0] - e.subtree_com[3 * rt1], cp[1] - e.subtree_com[3 * rt1 + 1], cp[2] - e.subtree_com[3 * rt1 + 2]};
+    T o2[3] = {cp[0] - e.subtree_com[3 * rt2], cp[1] - e.subtree_com[3 * rt2 + 1], cp[2] - e.subtree_com[3 * rt2 + 2]};
+    if (dl) {
+      T jd[3] = {0, 0, 0};
       const T* cd = e.cdof + 6 * l;
-      if (b2 > 0 && body_has_dof(m, b2, l)) {
-        int r2 = m.body_rootid[b2];
-        T off[3] = {pos[0] - e.subtree_com[3 * r2], pos[1] - e.subtree_com[3 * r2 + 1], pos[2] - e.subtree_com[3 * r2 + 2]}, t[3];
-        cross3(t, cd, off);
-        j2[0] = cd[3] + t[0]; j2[1] = cd[4] + t[1]; j2[2] = cd[5] + t[2];
+      if ((m2 >> l) & 1ull) {
+        T t[3];
+        cross3(t, cd, o2);
+        jd[0] += cd[3] + t[0]; jd[1] += cd[4] + t[1]; jd[2] += cd[5] + t[2];
       }
-      if (b1 > 0 && body_has_dof(m, b1, l)) {
-        int r1 = m.body_rootid[b1];
-        T off[3] = {pos[0] - e.subtree_com[3 * r1], pos[1] - e.subtree_com[3 * r1 + 1], pos[2] - e.subtree_com[3 * r1 + 2]}, t[3];
-        cross3(t, cd, off);
-        j1[0] = cd[3] + t[0]; j1[1] = cd[4] + t[1]; j1[2] = cd[5] + t[2];
+      if ((m1 >> l) & 1ull) {
+        T t[3];
+        cross3(t, cd, o1);
+        jd[0] -= cd[3] + t[0]; jd[1] -= cd[4] + t[1]; jd[2] -= cd[5] + t[2];
       }
-      T jd[3] = {j2[0] - j1[0], j2[1] - j1[1], j2[2] - j1[2]};
       T cj0 = fr[0] * jd[0] + fr[1] * jd[1] + fr[2] * jd[2];
-      T val[4];
       if (dim == 1) {
-        val[0] = cj0;
+        j0 = cj0;
       } else {
         T cj1 = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
         T cj2 = fr[6] * jd[0] + fr[7] * jd[1] + fr[8] * jd[2];
-        T mu0 = m.pair_friction[5 * p], mu1 = m.pair_friction[5 * p + 1];
-        val[0] = cj0 + mu0 * cj1; val[1] = cj0 - mu0 * cj1; val[2] = cj0 + mu1 * cj2; val[3] = cj0 - mu1 * cj2;
-      }
-      for (int i = 0; i < nrow; i++) {
-        int rr = adr + i;
-        if (rr >= c0 && rr < c1) e.Bm[(rr - c0) * e.Bs + l] = val[i];
+        j0 = cj0 + mu0 * cj1; j1 = cj0 - mu0 * cj1; j2 = cj0 + mu1 * cj2; j3 = cj0 - mu1 * cj2;
       }
     }
+    if (l < 4) {
+      // relative point motion of body 2 vs body 1 in the contact frame, for x = qvel,
+      // qacc_smooth, qacc_warmstart (vel = cvel, the others = cacc[0:6] / cacc[6:12])
+      T out[3];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const T* s2 = q == 0 ? e.cvel + 6 * b2 : e.cacc + 12 * b2 + 6 * (q - 1);
+        const T* s1 = q == 0 ? e.cvel + 6 * b1 : e.cacc + 12 * b1 + 6 * (q - 1);
+        T t2[3], t1[3];
+        cross3(t2, s2, o2);
+        cross3(t1, s1, o1);
+        T dd[3] = {s2[3] + t2[0] - s1[3] - t1[0], s2[4] + t2[1] - s1[4] - t1[1], s2[5] + t2[2] - s1[5] - t1[2]};
+        T cn = fr[0] * dd[0] + fr[1] * dd[1] + fr[2] * dd[2];
+        T ct = (l >> 1) == 0 ? fr[3] * dd[0] + fr[4] * dd[1] + fr[5] * dd[2] : fr[6] * dd[0] + fr[7] * dd[1] + fr[8] * dd[2];
+        T mu = (l >> 1) == 0 ? mu0 : mu1;
+        out[q] = dim == 1 ? cn : ((l & 1) ? cn - mu * ct : cn + mu * ct);
+      }
+      dv = out[0]; ds = out[1]; dw = out[2];
+    }
   }
-  wsync();
+  MGX_BSTAMP(8);
+  // L'^-1 over the support, highest dof first (the rows of a dof's descendants are final);
+  // the next step's L column is loaded before this step's updates
+  uint64_t sp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sup) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sup >> 32)) << 32);
+  if (sp) {
+    int k = 63 - __clzll(sp);
+    int base = readlane(e.madr, k) + readlane(e.chainlen, k) - e.chainlen;
+    T ld = e.qLD[base > 0 ? base : 0];
+    while (true) {
+      sp &= ~(1ull << k);
+      uint64_t am = readlane_u64(e.ancmask, k);
+      T x0 = readlane(j0, k), x1 = readlane(j1, k), x2 = readlane(j2, k), x3 = readlane(j3, k);
+      int kn = sp ? 63 - __clzll(sp) : k;
+      int basen = readlane(e.madr, kn) + readlane(e.chainlen, kn) - e.chainlen;
+      T ldn = e.qLD[basen > 0 ? basen : 0];
+      T coef = (dl && ((am >> l) & 1ull)) ? ld : (T)0;
+      j0 -= coef * x0; j1 -= coef * x1; j2 -= coef * x2; j3 -= coef * x3;
+      if (!sp) break;
+      k = kn;
+      ld = ldn;
+    }
+  }
+  j0 *= dinvs; j1 *= dinvs; j2 *= dinvs; j3 *= dinvs;
+  MGX_BSTAMP(9);
+  // B.B and the couplings (10 sums; the last two slots of the third call are unused)
+  T n0 = j0 * j0, n1 = j1 * j1, n2 = j2 * j2, n3 = j3 * j3;
+  T a10 = j1 * j0, a20 = j2 * j0, a21 = j2 * j1, a30 = j3 * j0, a31 = j3 * j1, a32 = j3 * j2;
+  wave_sum4(n0, n1, n2, n3);
+  wave_sum4(a10, a20, a21, a30);
+  T z0 = 0, z1 = 0;
+  wave_sum4(a31, a32, z0, z1);
+  MGX_BSTAMP(10);
+  if (l < 4) {
+    T* o = scal + (size_t)(r0 + l) * MGX_SCAL;
+    const T* rc = e.rowc + 4 * (r0 + l);
+    T nn = l == 0 ? n0 : l == 1 ? n1 : l == 2 ? n2 : n3;
+    if (rc[3] != 0) {
+      T R = rc[0];
+      T aref = -rc[1] * dv - rc[2];   // mj_referenceConstraint
+      T jar = dw - aref;
+      T ad = nn + R;
+      o[0] = ds - aref;                 // b = J qacc_smooth - aref
+      o[1] = jar < 0 ? -jar / R : (T)0; // warmstart force (mj_constraintUpdate, pyramidal)
+      o[2] = R;
+      o[3] = (T)1 / ad;
+      o[4] = (T)0.5 * ad;               // the solver's cost change is delta * (delta * AR / 2 + res)
+    } else {
+      o[0] = 0; o[1] = 0; o[2] = 1; o[3] = 1; o[4] = (T)0.5;
+    }
+    o[5] = l == 0 ? a10 : l == 1 ? a30 : (T)0;
+    o[6] = l == 0 ? a20 : l == 1 ? a31 : (T)0;
+    o[7] = l == 0 ? a21 : l == 1 ? a32 : (T)0;
+  }
+  if (l < P.brow) {
+    Bo[(size_t)(r0 + 0) * P.brow + l] = dl ? j0 : (T)0;
+    Bo[(size_t)(r0 + 1) * P.brow + l] = dl ? j1 : (T)0;
+    Bo[(size_t)(r0 + 2) * P.brow + l] = dl ? j2 : (T)0;
+    Bo[(size_t)(r0 + 3) * P.brow + l] = dl ? j3 : (T)0;
+  }
+  MGX_BSTAMP(11);
 }
 
 // S1 body: forward up to the constraint rows, rows -> pipe, carry -> pipe
@@ -223,7 +336,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   MGX_STAMP(0);
   com_crb(m, e);
   MGX_STAMP(1);
-  e.diaginv = factor_ld(m, e.qLD);
+  e.diaginv = factor_ld(m, e, e.qLD);
   MGX_STAMP(2);
   velocity(m, e);
   MGX_STAMP(3);
@@ -231,77 +344,41 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   MGX_STAMP(4);
   collision(m, e);
   MGX_STAMP(5);
-  rows_meta(m, e);
+  int nlim, ncf;
+  const int ne = rows_plan(m, e, &nlim, &ncf);
+  e.nefc = ne;
   MGX_STAMP(6);
-  const int ne = e.nefc;
   const bool dl = l < nv;
   if (ne > 0) {
-    T sqrtD = dl ? sqrt(e.qLD[m.dof_Madr[l]]) : (T)0;
-    T qv = dl ? e.qvel[l] : (T)0;
-    T wv = sqrtD * mul_L(m, e, e.qLD, qv);
-    T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
-    T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
-    wsync();
-    if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww; e.vec3[l] = sqrt(e.diaginv); }
-    wsync();
+    const T dinvs = dl ? sqrt(e.diaginv) : (T)0;
     T* scal = P.at<T>(P.o_scal) + (size_t)slot * P.maxE * MGX_SCAL;
     T* Bo = P.at<T>(P.o_B) + (size_t)slot * (P.maxE + MGX_BPAD) * P.brow;
-    const int CH = m.L.chunk_rows;
-    for (int c0 = 0; c0 < ne; c0 += CH) {
-      int c1 = c0 + CH < ne ? c0 + CH : ne;
-      build_chunk(m, e, c0, c1);
-      int r = c0 + l;
-      if (r < c1) {
-        // B_r = D^-1/2 L'^-1 J_r' in place (transform_rows), then the row scalars of pgs()
-        T* x = e.Bm + (r - c0) * e.Bs;
-        for (int k = nv - 1; k >= 0; k--) {
-          T xk = x[k];
-          int a = m.dof_Madr[k] + 1;
-          int mk = m.dof_chainlen[k] - 1;
-          for (int t = 1; t <= mk; t++) x[m.dof_anc[k * MGX_MAX_DEPTH + t]] -= e.qLD[a + t - 1] * xk;
-          x[k] = xk * e.vec3[k];
+    const int nlim4 = (nlim + 3) & ~3;
+    // qacc_smooth / qacc_warmstart into LDS (limit rows) and their per-body chain sums
+    if (dl) { e.vec1[l] = e.qacc_smooth; e.vec2[l] = e.qacc_ws; }
+    wsync();
+    if (ncf > 0) {
+      for (int b = l; b < m.nbody; b += 64) {
+        T a[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        int depth = m.body_depth[b];
+        for (int c = 0; c < depth; c++) {
+          int i = m.body_chain[b * MGX_MAX_DEPTH + c];
+          int bda = m.body_dofadr[i], nd = m.body_dofnum[i];
+          for (int jd = bda; jd < bda + nd; jd++) {
+            T xs = e.vec1[jd], xw = e.vec2[jd];
+            const T* cd = e.cdof + 6 * jd;
+            for (int q = 0; q < 6; q++) { a[q] += cd[q] * xs; a[6 + q] += cd[q] * xw; }
+          }
         }
-        T dv = 0, ds = 0, dw = 0, nn = 0;
-        for (int k = 0; k < nv; k++) {
-          T xx = x[k];
-          dv += xx * e.vec0[k]; ds += xx * e.vec1[k]; dw += xx * e.vec2[k]; nn += xx * xx;
-        }
-        const T* q = e.efc + 8 * r;
-        T aref = -q[6] * dv - q[5];
-        T Rr = q[2];
-        T jar = dw - aref;
-        T ad = nn + Rr;
-        T* o = scal + r * MGX_SCAL;
-        o[0] = ds - aref;
-        o[1] = jar < 0 ? -jar / Rr : (T)0;
-        o[2] = Rr;
-        o[3] = (T)1 / ad;
-        o[4] = (T)0.5 * ad;  // the solver's cost change is delta * (delta * AR / 2 + res)
+        for (int q = 0; q < 12; q++) e.cacc[12 * b + q] = a[q];
       }
-      wsync();
-      // block Gauss-Seidel couplings A_ij = B_i.B_j (j < i) of each 4-row block in the chunk:
-      // row 4b holds A10 A20 A21 in slots 5..7, row 4b+1 holds A30 A31 A32
-      if (4 * l < c1 - c0) {
-        int rb0 = 4 * l;
-        const T* x0 = e.Bm + rb0 * e.Bs;
-        bool h1 = c0 + rb0 + 1 < c1, h2 = c0 + rb0 + 2 < c1, h3 = c0 + rb0 + 3 < c1;
-        T a10 = 0, a20 = 0, a21 = 0, a30 = 0, a31 = 0, a32 = 0;
-        for (int k = 0; k < nv; k++) {
-          T y0 = x0[k];
-          T y1 = h1 ? x0[e.Bs + k] : (T)0, y2 = h2 ? x0[2 * e.Bs + k] : (T)0, y3 = h3 ? x0[3 * e.Bs + k] : (T)0;
-          a10 += y1 * y0; a20 += y2 * y0; a21 += y2 * y1; a30 += y3 * y0; a31 += y3 * y1; a32 += y3 * y2;
-        }
-        T* o = scal + (c0 + rb0) * MGX_SCAL;
-        o[5] = a10; o[6] = a20; o[7] = a21;
-        if (h1) { o[MGX_SCAL + 5] = a30; o[MGX_SCAL + 6] = a31; o[MGX_SCAL + 7] = a32; }
-        else { o[MGX_SCAL + 5] = 0; o[MGX_SCAL + 6] = 0; o[MGX_SCAL + 7] = 0; }
-      }
-      wsync();
-      // B rows out, lane = dof, zero padded to brow
-      if (l < P.brow)
-        for (int rr = c0; rr < c1; rr++) Bo[(size_t)rr * P.brow + l] = dl ? e.Bm[(rr - c0) * e.Bs + l] : (T)0;
       wsync();
     }
+    rows_impedance(m, e, ne, nlim, nlim4);
+    ContactMeta<T> cm;
+    contact_meta(m, e, ncf, cm);
+    wsync();
+    for (int r0 = 0; r0 < ne; r0 += 4) build_block(m, e, P, r0, nlim, nlim4, cm, dinvs, scal, Bo);
   }
   MGX_STAMP(7);
   // carry + registers + ints
