@@ -6,8 +6,10 @@
 
 One "step" = one SoccerVectorEnv.step over all envs of a rank: action clip, goalkeeper, wind,
 mj_step (kinematics .. PGS .. Euler) and observation/reward/termination for every env, with
-same-step autoreset — one fused HIP kernel launch (mgx_soccer_step). Actions are synthetic
-U(-150, 150)^33 float32 drawn before the timed region and resident in HBM.
+same-step autoreset — mgx_soccer_step, the staged kernels k_soccer_rows -> k_pgs_groups ->
+k_soccer_finish -> k_soccer_fixup on one stream (--mono: one fused kernel).
+Reset settle steps of the precomputed reset banks run inside the same launches. Actions are
+synthetic U(-150, 150)^33 float32 drawn before the timed region and resident in HBM.
 Ranks shard envs (global index = rank * envs + i); the only collective is the end-of-rollout
 metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
 """
@@ -165,13 +167,14 @@ def main():
         bytes_per_launch = ALG_BYTES_PER_ENV_STEP * N
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
+        mode = "mono" if args.mono else "staged"
         pmc = os.path.join(ROOT, "profiles", "r01_pmc.json")
         if os.path.exists(pmc):
             try:
                 with open(pmc) as f:
                     p = json.load(f)
-                if p.get("envs") == N and p.get("precision") == args.precision:
-                    traffic = p.get("hbm_bytes_per_launch")
+                if p.get("envs") == N and p.get("precision") == args.precision and p.get("mode") == mode:
+                    traffic = p.get("hbm_bytes_per_step")
             except Exception:  # noqa: BLE001
                 traffic = None
         out = {
@@ -181,13 +184,17 @@ def main():
             "data": "synthetic (U(-150,150) actions, Philox reset draws)",
             "config": {"workload": "humanoid_soccer_env, 4096 envs/GPU (BASELINE configs[2])",
                        "envs_per_gpu": N, "global_batch": N * world, "parallelism": f"dp{world} (env shards)",
-                       "autoreset": "same-step", "episodes_started": int(acc[1].item()),
+                       "autoreset": "same-step", "step_kernels": mode, "reset_banks": 0 if args.mono else args.banks,
+                       "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "mean_reward": round(acc[2].item() / total_steps, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_soccer<float,0> (mgx_soccer_step)",
-                         "alg_bytes_per_launch": bytes_per_launch, "launch_ms": round(launch_ms, 4)},
+                         "kernel": ("mgx_soccer_step = k_soccer_rows + k_pgs_groups + k_soccer_finish + k_soccer_fixup"
+                                    if mode == "staged" else "mgx_soccer_step = k_soccer<T,0>"),
+                         "alg_bytes_per_step": bytes_per_launch, "launch_ms": round(launch_ms, 4),
+                         "note": "achieved = algorithmic bytes of one env step x envs / HIP-event time of the "
+                                 "step's launches; traffic = PMC HBM bytes of those launches per step"},
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_steps)

@@ -677,10 +677,11 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   Pipe p{};
   p.base = (char*)ws;
   p.N = n_env; p.R = banks; p.S = n_env * (1 + banks);
-  p.maxE = m->Ls.max_nefc; p.nv = nv; p.dpl = (nv + 15) / 16;
+  p.maxE = m->Ls.max_nefc; p.nv = nv; p.dpl = (nv + 7) / 8;  // solver: support entries per lane
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.brow = 16 * p.dpl;
+  p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t r = off; off = (off + bytes + 255) / 256 * 256; return r; };
   size_t S = (size_t)p.S, NB = (size_t)n_env * (banks > 0 ? banks : 1);
@@ -689,7 +690,8 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.o_carryi = take(S * p.carryi_stride * 4);
   p.o_ne = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_fix = take((size_t)n_env * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
-  p.o_B = take(S * (p.maxE + MGX_BPAD) * p.brow * rb);
+  p.o_blk = take(S * p.maxE * 4);  // 8 uint16 per 4-row block
+  p.o_B = take(S * (size_t)p.bcap * rb);
   p.o_vout = take(S * 64 * rb);
   p.o_bq = take(NB * nq * rb); p.o_bv = take(NB * nv * rb); p.o_ba = take(NB * nv * rb); p.o_btime = take(NB * rb);
   p.o_bobs = take(NB * 80 * 4); p.o_bprev = take(NB * 6 * rb); p.o_bwind = take(NB * 3 * rb);
@@ -705,16 +707,20 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 
 static int pgs_lds_bytes(const mgx_model* m) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
-  return 4 * (MGX_SCAL * m->Ls.max_nefc + 4) * rb + 64;
+  int nb3 = (m->Ls.max_nefc / 4 + 2) / 3 * 3;  // whole ring turns of 3 blocks
+  return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 1) * rb + MGX_PGS_SPW * nb3 * 16 + 64;
 }
 
 template <typename T>
-static void launch_pgs(const Pipe& P, int grid, int lds, hipStream_t st, int maxit, T tol, T scale) {
+static void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale) {
+  static const int spw = getenv("MGX_PGS_SPW") ? atoi(getenv("MGX_PGS_SPW")) : MGX_PGS_SPW;  // debug: slots per wave
+  int grid = (slots + (spw < 0 ? -spw : spw) - 1) / (spw < 0 ? -spw : spw);
   switch (P.dpl) {
-    case 1: hipLaunchKernelGGL((k_pgs_groups<T, 1>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
-    case 2: hipLaunchKernelGGL((k_pgs_groups<T, 2>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
-    case 3: hipLaunchKernelGGL((k_pgs_groups<T, 3>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
-    default: hipLaunchKernelGGL((k_pgs_groups<T, 4>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale); break;
+#define MGX_PGS_CASE(E) \
+    case E: hipLaunchKernelGGL((k_pgs_groups<T, E>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw); break;
+    MGX_PGS_CASE(1) MGX_PGS_CASE(2) MGX_PGS_CASE(3) MGX_PGS_CASE(4) MGX_PGS_CASE(5) MGX_PGS_CASE(6) MGX_PGS_CASE(7)
+    default: hipLaunchKernelGGL((k_pgs_groups<T, 8>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw); break;
+#undef MGX_PGS_CASE
   }
 }
 
@@ -732,7 +738,7 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, *e, action, n_env, mask, P,
                      banks);
   T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
-  launch_pgs<T>(P, (slots + 3) / 4, pgs_lds_bytes(m), st, M.iterations, M.tolerance, scale);
+  launch_pgs<T>(P, slots, pgs_lds_bytes(m), st, M.iterations, M.tolerance, scale);
   hipLaunchKernelGGL(k_soccer_finish<T>, dim3(n_env), dim3(64), m->Lf.bytes, st, Mf, ids, *s, *e, action, obs, reward,
                      terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks);
   int fgrid = n_env < 256 ? n_env : 256;
@@ -806,6 +812,20 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
                   set_lds(k_soccer_logic<double>, m->L.bytes) | set_lds(k_soccer_fixup<double>, m->L.bytes) | set_lds(k_soccer_template<double>, m->L.bytes) |
                   set_lds(k_soccer_rows<double>, m->Ls.bytes) | set_lds(k_soccer_finish<double>, m->Lf.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
+  {
+    int pl = pgs_lds_bytes(m);
+    if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
+    int r3 = precision == MGX_F32
+                 ? (set_lds(k_pgs_groups<float, 1>, pl) | set_lds(k_pgs_groups<float, 2>, pl) |
+                    set_lds(k_pgs_groups<float, 3>, pl) | set_lds(k_pgs_groups<float, 4>, pl) |
+                    set_lds(k_pgs_groups<float, 5>, pl) | set_lds(k_pgs_groups<float, 6>, pl) |
+                    set_lds(k_pgs_groups<float, 7>, pl) | set_lds(k_pgs_groups<float, 8>, pl))
+                 : (set_lds(k_pgs_groups<double, 1>, pl) | set_lds(k_pgs_groups<double, 2>, pl) |
+                    set_lds(k_pgs_groups<double, 3>, pl) | set_lds(k_pgs_groups<double, 4>, pl) |
+                    set_lds(k_pgs_groups<double, 5>, pl) | set_lds(k_pgs_groups<double, 6>, pl) |
+                    set_lds(k_pgs_groups<double, 7>, pl) | set_lds(k_pgs_groups<double, 8>, pl));
+    if (r3 != MGX_OK) { delete m; return r3; }
+  }
   *out = m;
   return MGX_OK;
 }

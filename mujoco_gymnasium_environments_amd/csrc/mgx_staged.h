@@ -25,8 +25,8 @@
 namespace mgx {
 
 #define MGX_PGS_LPE 16         // lanes per slot in the solver kernel
-#define MGX_SCAL 8             // row scalars: b, f, R, 1/AR, AR/2, then 3 slots of the block's A_ij
-#define MGX_BPAD 24            // B rows past max_nefc: the solver prefetches up to 3 blocks ahead
+#define MGX_SCAL 5             // row scalars: b, f, R, 1/AR, AR/2
+#define MGX_PGS_SPW 8          // solver: slots per wave (8 lanes each)
 enum { FIX_RESET = 2 };
 
 // Workspace layout (byte offsets from base), computed on the host (mgx_soccer_workspace_bytes)
@@ -35,8 +35,9 @@ struct Pipe {
   int N, R, S, maxE, dpl, nv;
   int carry_stride;    // reals per slot: carry_reals (64-aligned) + 5 * 64 registers
   int carryi_stride;   // ints per slot: carry_ints + 8
-  int brow;            // reals per B row (16 * dpl)
-  size_t o_carry, o_carryi, o_ne, o_niter, o_k2list, o_ctr, o_fix, o_scal, o_B, o_vout;
+  int brow;            // unused (dense-row width of earlier layouts)
+  int bcap;            // reals per slot of group-compressed B: 32 + (max_nefc / 4) * (8 + 32 * ceil(nv / 8))
+  size_t o_carry, o_carryi, o_ne, o_niter, o_k2list, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
   size_t o_bq, o_bv, o_ba, o_btime, o_bobs, o_bprev, o_bwind, o_bk, o_bep, o_bwarn, o_bseed;
   // the checkAcc template: mj_step's outcome after mj_resetData (state + forward frames)
   size_t o_tq, o_tv, o_ta, o_tt, o_tx, o_txq, o_tsc, o_tn, o_tcg, o_tcd, o_tcm;
@@ -186,7 +187,7 @@ __device__ __forceinline__ double readlane_t(double x, int l) { return readlane(
 // the row scalars and B -> pipe.
 template <typename T>
 __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, const Pipe& P, int r0, int nlim, int nlim4,
-                                            const ContactMeta<T>& cm, T dinvs, T* scal, T* Bo) {
+                                            const ContactMeta<T>& cm, T dinvs, T* scal, int* blk, T* Bo, int& boff) {
   const int l = lane_id();
   const int nv = m.nv;
   const bool dl = l < nv;
@@ -313,15 +314,29 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
     } else {
       o[0] = 0; o[1] = 0; o[2] = 1; o[3] = 1; o[4] = (T)0.5;
     }
-    o[5] = l == 0 ? a10 : l == 1 ? a30 : (T)0;
-    o[6] = l == 0 ? a20 : l == 1 ? a31 : (T)0;
-    o[7] = l == 0 ? a21 : l == 1 ? a32 : (T)0;
   }
-  if (l < P.brow) {
-    Bo[(size_t)(r0 + 0) * P.brow + l] = dl ? j0 : (T)0;
-    Bo[(size_t)(r0 + 1) * P.brow + l] = dl ? j1 : (T)0;
-    Bo[(size_t)(r0 + 2) * P.brow + l] = dl ? j2 : (T)0;
-    Bo[(size_t)(r0 + 3) * P.brow + l] = dl ? j3 : (T)0;
+  // the block for the solver: [A10 A20 A21 A30 A31 A32 0 0] then, for each 8-dof group the
+  // block's support touches (ascending), [8 dofs][4 rows] (a lane's 4 rows are one 16-byte
+  // load). The block table entry holds 8 uint16 offsets: the A offset, then per group g < 7
+  // its data offset, or the slot's zero group (offset 0, 32 zeros never written) when the
+  // block does not touch it: no index math or selects in the sweeps.
+  {
+    uint32_t gm = 0;
+#pragma unroll
+    for (int g = 0; g < 8; g++) gm |= ((sup >> (8 * g)) & 0xffull) ? (1u << g) : 0u;
+    T* o = Bo + boff;
+    if (l < 8) o[l] = l == 0 ? a10 : l == 1 ? a20 : l == 2 ? a21 : l == 3 ? a30 : l == 4 ? a31 : l == 5 ? a32 : (T)0;
+    const int g = l >> 3, jj = l & 7;
+    if (dl && ((gm >> g) & 1u)) {
+      T* og = o + 8 + 32 * __popc(gm & ((1u << g) - 1u)) + 4 * jj;
+      og[0] = j0; og[1] = j1; og[2] = j2; og[3] = j3;
+    }
+    if (l < 8) {
+      uint16_t* bt = reinterpret_cast<uint16_t*>(blk) + 8 * (r0 >> 2);
+      int v = l == 0 ? boff : (((gm >> (l - 1)) & 1u) ? boff + 8 + 32 * __popc(gm & ((1u << (l - 1)) - 1u)) : 0);
+      bt[l] = (uint16_t)v;
+    }
+    boff += 8 + 32 * __popc(gm);
   }
   MGX_BSTAMP(11);
 }
@@ -352,7 +367,9 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   if (ne > 0) {
     const T dinvs = dl ? sqrt(e.diaginv) : (T)0;
     T* scal = P.at<T>(P.o_scal) + (size_t)slot * P.maxE * MGX_SCAL;
-    T* Bo = P.at<T>(P.o_B) + (size_t)slot * (P.maxE + MGX_BPAD) * P.brow;
+    T* Bo = P.at<T>(P.o_B) + (size_t)slot * P.bcap;
+    int* blk = P.at<int>(P.o_blk) + (size_t)slot * P.maxE;  // 8 uint16 per 4-row block
+    int boff = 32;                                          // [0, 32): the zero group
     const int nlim4 = (nlim + 3) & ~3;
     // qacc_smooth / qacc_warmstart into LDS (limit rows) and their per-body chain sums
     if (dl) { e.vec1[l] = e.qacc_smooth; e.vec2[l] = e.qacc_ws; }
@@ -378,7 +395,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
     ContactMeta<T> cm;
     contact_meta(m, e, ncf, cm);
     wsync();
-    for (int r0 = 0; r0 < ne; r0 += 4) build_block(m, e, P, r0, nlim, nlim4, cm, dinvs, scal, Bo);
+    for (int r0 = 0; r0 < ne; r0 += 4) build_block(m, e, P, r0, nlim, nlim4, cm, dinvs, scal, blk, Bo, boff);
   }
   MGX_STAMP(7);
   // carry + registers + ints
@@ -410,185 +427,257 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
 }
 
 // ------------------------------------------------------------------ S2: lane-group PGS
+// Gauss-Seidel sweeps of mj_solPGS [ext], 8 slots per wave, 8 lanes per slot. Row scalars
+// (b, f, R, 1/AR, AR/2), the block table (offset, support size S) and v = B'f (one real per
+// dof, plus a sink entry) live in LDS. Each 4-row block's B comes compressed to its dof support
+// (S ~ 6..25 of nv, index list + 4 value rows) with its couplings A_ij; lane j of a slot holds
+// support entries j, j+8, ..; a 4-block register ring keeps 3 blocks in flight ahead of use,
+// and support entries past the wave's largest S are skipped uniformly. Per block the four
+// B_r.v use the pre-block v (interleaved 8-lane reductions) and row i adds
+// sum_{j<i} A_ij delta_j: the sequential Gauss-Seidel update. Per-slot results do not depend
+// on which slots share the wave (other slots only add masked no-op blocks / sweeps).
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
 }
-// sum over the 16 lanes of a DPP row; every lane of the row gets the identical total
-__device__ __forceinline__ float row16_sum(float x) {
-  x += dpp_row<0xB1>(x);   // quad_perm 1,0,3,2
-  x += dpp_row<0x4E>(x);   // quad_perm 2,3,0,1
-  x += dpp_row<0x141>(x);  // row_half_mirror
-  x += dpp_row<0x140>(x);  // row_mirror
-  return x;
-}
-// four independent 16-lane sums, DPP steps interleaved to fill each other's hazard slots
-__device__ __forceinline__ void row16_sum4(float& a, float& b, float& c, float& d) {
+// four independent 8-lane sums (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror); every lane of
+// the 8-lane group ends with the identical total
+__device__ __forceinline__ void oct_sum4(float& a, float& b, float& c, float& d) {
 #define MGX_R4(CTRL) a += dpp_row<CTRL>(a); b += dpp_row<CTRL>(b); c += dpp_row<CTRL>(c); d += dpp_row<CTRL>(d);
   MGX_R4(0xB1)
   MGX_R4(0x4E)
   MGX_R4(0x141)
-  MGX_R4(0x140)
 #undef MGX_R4
 }
-__device__ __forceinline__ void row16_sum4(double& a, double& b, double& c, double& d);
-__device__ __forceinline__ double row16_sum(double x) {
+__device__ __forceinline__ double oct_sum(double x) {
   x += __shfl_xor(x, 1);
   x += __shfl_xor(x, 2);
   x += __shfl_xor(x, 4);
-  x += __shfl_xor(x, 8);
   return x;
 }
-__device__ __forceinline__ void row16_sum4(double& a, double& b, double& c, double& d) {
-  a = row16_sum(a); b = row16_sum(b); c = row16_sum(c); d = row16_sum(d);
+__device__ __forceinline__ void oct_sum4(double& a, double& b, double& c, double& d) {
+  a = oct_sum(a); b = oct_sum(b); c = oct_sum(c); d = oct_sum(d);
 }
 
-// Gauss-Seidel sweeps of mj_solPGS [ext] for 4 slots per wave, 16 lanes per slot. Row
-// scalars live in LDS (8 per row); B rows stream from the pipe (row-major, 16*DPL reals, lane j
-// reads dofs j + 16d) through a 4-block register ring, 3 blocks (12 rows) ahead of use. Rows
-// go in blocks of 4: the four B_r.v use the pre-block v (interleaved reductions) and row i adds
-// sum_{j<i} A_ij delta_j with A_ij = B_i.B_j from the row builder -> the sequential
-// Gauss-Seidel update in a quarter of the reduction latency. Results per slot do not depend
-// on which slots share the wave (other slots only add masked no-op rows / sweeps).
-template <typename T, int DPL>
-__device__ __forceinline__ void pgs_load_block(T (&dst)[4][DPL], const T* Bs, int r0, int brow) {
+template <typename T>
+struct Vec4T;
+template <>
+struct Vec4T<float> { typedef float type __attribute__((ext_vector_type(4))); };
+template <>
+struct Vec4T<double> { typedef double type __attribute__((ext_vector_type(4))); };
+
+template <typename T, int EPL>
+struct PgsBlk {
+  typename Vec4T<T>::type b[EPL];  // B of the block's 4 rows at this lane's dof j + 8d
+  typename Vec4T<T>::type a0, a1;  // A10 A20 A21 A30 | A31 A32 - -
+  T q[4][4];                       // the rows' b, R, 1/AR, AR/2
+};
+
+// f32: two values per v_pk_fma_f32
+typedef float mgx_f2 __attribute__((ext_vector_type(2)));
+
+template <typename T, int EPL>
+__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint16_t* bt, int blk,
+                                               int j) {
+  // the table entry of a block past the slot's end points at the zero group (A included);
+  // every load is one 16-byte vector load at a table offset
+  typedef typename Vec4T<T>::type V4;
+  const uint16_t* t = bt + 8 * blk;
+  const V4* pa = reinterpret_cast<const V4*>(Bsl + t[0]);
+  k.a0 = pa[0];
+  k.a1 = pa[1];
 #pragma unroll
-  for (int i = 0; i < 4; i++)
+  for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t[1 + d] + 4 * j);
+  const T* q = sc + 4 * blk * MGX_SCAL;
 #pragma unroll
-    for (int d = 0; d < DPL; d++) dst[i][d] = Bs[(size_t)(r0 + i) * brow + 16 * d];
+  for (int i = 0; i < 4; i++) {
+    k.q[i][0] = q[i * MGX_SCAL + 0];
+    k.q[i][1] = q[i * MGX_SCAL + 2];
+    k.q[i][2] = q[i * MGX_SCAL + 3];
+    k.q[i][3] = q[i * MGX_SCAL + 4];
+  }
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
 }
 
-template <typename T, int DPL>
-__device__ __forceinline__ void pgs_block(T (&bb)[4][DPL], T (&v)[DPL], T* sc, int r0, int ne, bool act, T& impr) {
-  const bool ok0 = act && r0 < ne, ok1 = act && r0 + 1 < ne, ok2 = act && r0 + 2 < ne, ok3 = act && r0 + 3 < ne;
-  T d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+template <typename T, int EPL>
+__device__ __forceinline__ void pgs_dots(const PgsBlk<T, EPL>& k, const T (&v)[EPL], T& d0, T& d1, T& d2, T& d3) {
+  d0 = d1 = d2 = d3 = 0;
 #pragma unroll
-  for (int d = 0; d < DPL; d++) {
-    bb[0][d] = ok0 ? bb[0][d] : (T)0;
-    bb[1][d] = ok1 ? bb[1][d] : (T)0;
-    bb[2][d] = ok2 ? bb[2][d] : (T)0;
-    bb[3][d] = ok3 ? bb[3][d] : (T)0;
-    d0 += bb[0][d] * v[d]; d1 += bb[1][d] * v[d]; d2 += bb[2][d] * v[d]; d3 += bb[3][d] * v[d];
+  for (int d = 0; d < EPL; d++) {
+    d0 += k.b[d].x * v[d]; d1 += k.b[d].y * v[d]; d2 += k.b[d].z * v[d]; d3 += k.b[d].w * v[d];
   }
-  row16_sum4(d0, d1, d2, d3);
-  T* q0 = sc + r0 * MGX_SCAL;
-  const T a10 = q0[5], a20 = q0[6], a21 = q0[7], a30 = q0[MGX_SCAL + 5], a31 = q0[MGX_SCAL + 6], a32 = q0[MGX_SCAL + 7];
-  T dl0, dl1, dl2, dl3;
-#define MGX_PGS_ROW(I, OK, DOT, DL)                                      \
-  {                                                                      \
-    T* q = q0 + (I) * MGX_SCAL;                                          \
-    T br = q[0], fr = q[1], Rr = q[2], ai = q[3], hd = q[4];             \
-    T res = br + (DOT) + Rr * fr;                                        \
-    T fn = fr - res * ai;                                                \
-    fn = fn < 0 ? (T)0 : fn;                                             \
-    T delta = fn - fr;                                                   \
-    T change = delta * (delta * hd + res);                               \
-    bool keep = !(OK) || change > (T)1e-10;                              \
-    DL = keep ? (T)0 : delta;                                            \
-    impr -= keep ? (T)0 : change;                                        \
-    q[1] = keep ? fr : fn;                                               \
-  }
-  MGX_PGS_ROW(0, ok0, d0, dl0)
-  MGX_PGS_ROW(1, ok1, d1 + a10 * dl0, dl1)
-  MGX_PGS_ROW(2, ok2, d2 + a20 * dl0 + a21 * dl1, dl2)
-  MGX_PGS_ROW(3, ok3, d3 + a30 * dl0 + a31 * dl1 + a32 * dl2, dl3)
-#undef MGX_PGS_ROW
+}
+template <int EPL>
+__device__ __forceinline__ void pgs_dots(const PgsBlk<float, EPL>& k, const float (&v)[EPL], float& d0, float& d1,
+                                         float& d2, float& d3) {
+  mgx_f2 p01 = {0.f, 0.f}, p23 = {0.f, 0.f};
 #pragma unroll
-  for (int d = 0; d < DPL; d++) v[d] += dl0 * bb[0][d] + dl1 * bb[1][d] + dl2 * bb[2][d] + dl3 * bb[3][d];
+  for (int d = 0; d < EPL; d++) {
+    mgx_f2 vv = {v[d], v[d]};
+    p01 = __builtin_elementwise_fma(k.b[d].xy, vv, p01);
+    p23 = __builtin_elementwise_fma(k.b[d].zw, vv, p23);
+  }
+  d0 = p01.x; d1 = p01.y; d2 = p23.x; d3 = p23.y;
 }
 
-template <typename T, int DPL>
-__global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale) {
+template <typename T, int EPL>
+__device__ __forceinline__ void pgs_update(const PgsBlk<T, EPL>& k, T (&v)[EPL], T dl0, T dl1, T dl2, T dl3) {
+#pragma unroll
+  for (int d = 0; d < EPL; d++) v[d] += dl0 * k.b[d].x + dl1 * k.b[d].y + dl2 * k.b[d].z + dl3 * k.b[d].w;
+}
+
+template <typename T, int EPL>
+__device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], T* sc, int r0, bool ok0, T& impr) {
+  T* q0 = sc + r0 * MGX_SCAL;
+  // forces read here, not with the prefetch: a row's f must be its latest value
+  const T f0 = q0[1], f1 = q0[MGX_SCAL + 1], f2 = q0[2 * MGX_SCAL + 1], f3 = q0[3 * MGX_SCAL + 1];
+  T d0, d1, d2, d3;
+  pgs_dots(k, v, d0, d1, d2, d3);
+  // b + R f off the dependent chain
+  const T t0 = k.q[0][0] + k.q[0][1] * f0, t1 = k.q[1][0] + k.q[1][1] * f1;
+  const T t2 = k.q[2][0] + k.q[2][1] * f2, t3 = k.q[3][0] + k.q[3][1] * f3;
+  oct_sum4(d0, d1, d2, d3);
+  T dl0, dl1, dl2, dl3;
+#define MGX_PGS_ROW(I, DOT, DL)                                   \
+  {                                                               \
+    const T fr = f##I, ai = k.q[I][2], hd = k.q[I][3];            \
+    T res = (DOT) + t##I;                                         \
+    T fn = fmax(fr - res * ai, (T)0);                             \
+    T delta = fn - fr;                                            \
+    T change = delta * (delta * hd + res);                        \
+    bool keep = !ok0 || change > (T)1e-10;                        \
+    T nf = keep ? fr : fn;                                        \
+    DL = nf - fr;                                                 \
+    impr -= keep ? (T)0 : change;                                 \
+    q0[(I) * MGX_SCAL + 1] = nf;                                  \
+  }
+  MGX_PGS_ROW(0, d0, dl0)
+  MGX_PGS_ROW(1, d1 + k.a0.x * dl0, dl1)
+  MGX_PGS_ROW(2, d2 + k.a0.y * dl0 + k.a0.z * dl1, dl2)
+  MGX_PGS_ROW(3, d3 + k.a0.w * dl0 + k.a1.x * dl1 + k.a1.y * dl2, dl3)
+#undef MGX_PGS_ROW
+  pgs_update(k, v, dl0, dl1, dl2, dl3);
+}
+
+template <typename T, int EPL>
+__global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int l = threadIdx.x, s = l >> 4, j = l & 15;
+  const int l = threadIdx.x, s = l >> 3, j = l & 7;
   if (blockIdx.x == 0 && l == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
   const int cnt = P.ctr()[1];
-  const int base = blockIdx.x * 4;
+  const int spn = spw < 0 ? -spw : spw;
+  const int base = blockIdx.x * spn;
   if (base >= cnt) return;
   const int idx = base + s;
-  const int slot = idx < cnt ? P.at<int>(P.o_k2list)[idx] : -1;
-  const int ne = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;
-  const int sstride = MGX_SCAL * P.maxE + 4;
+  const int slot = (s < spn && idx < cnt) ? P.at<int>(P.o_k2list)[idx] : -1;
+  const int ne = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;  // a multiple of 4
+  const int nblk = ne >> 2;
+  // LDS capacity in whole ring turns: nbcap3 = max_nefc / 4 rounded up to a multiple of 3
+  const int nbcap = P.maxE / 4, nbcap3 = (nbcap + 2) / 3 * 3;
+  const int sstride = MGX_SCAL * 4 * nbcap3 + 1;
   T* sc = reinterpret_cast<T*>(smem) + s * sstride;
-  const T* gsc = P.at<T>(P.o_scal) + (size_t)(slot >= 0 ? slot : 0) * P.maxE * MGX_SCAL;
-  for (int q = j; q < ne * MGX_SCAL; q += 16) sc[q] = gsc[q];
-  int nm = ne;
+  uint16_t* bt = reinterpret_cast<uint16_t*>(reinterpret_cast<T*>(smem) + MGX_PGS_SPW * sstride) + s * 8 * nbcap3;
+  const size_t sl = (size_t)(slot >= 0 ? slot : 0);
+  const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
+  const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * P.maxE);
+  for (int q = j; q < MGX_SCAL * 4 * nbcap3; q += 8) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
+  // block table: the slot's blocks, then zero-group entries up to the capacity
+  for (int q = j; q < 8 * nbcap3; q += 8) bt[q] = q < 8 * nblk ? gbt[q] : (uint16_t)0;
+  int nm = nblk;
+  nm = max(nm, __shfl_xor(nm, 8));
   nm = max(nm, __shfl_xor(nm, 16));
   nm = max(nm, __shfl_xor(nm, 32));
-  const int neMax = __builtin_amdgcn_readfirstlane(nm);
-  const int ne4 = (neMax + 3) & ~3;
-  const int brow = 16 * DPL;
-  const T* Bs = P.at<T>(P.o_B) + (size_t)(slot >= 0 ? slot : 0) * (P.maxE + MGX_BPAD) * brow + j;
+  int nbMax = __builtin_amdgcn_readfirstlane(nm);
+  if (spw < 0) nbMax = nbcap;  // debug: sweep every block slot
+  // whole ring turns (3 blocks): the sweep has no remainder path; the padding blocks are
+  // zero-table blocks whose rows are masked (their LDS scalars zero-filled below)
+  const int nbRun = (nbMax + 2) / 3 * 3;
+  const T* Bsl = P.at<T>(P.o_B) + sl * P.bcap;
   __syncthreads();
   // warmstart: v = B' f, dual cost, reset to zero if the cost is positive
-  T v[DPL];
+  T v[EPL];
 #pragma unroll
-  for (int d = 0; d < DPL; d++) v[d] = 0;
-  for (int r = 0; r < neMax; r++) {
-    bool ok = r < ne;
-    T f = ok ? sc[r * MGX_SCAL + 1] : (T)0;
-#pragma unroll
-    for (int d = 0; d < DPL; d++) {
-      T b = Bs[(size_t)r * brow + 16 * d];
-      v[d] += f * (ok ? b : (T)0);
-    }
+  for (int d = 0; d < EPL; d++) v[d] = 0;
+  for (int b = 0; b < nbMax; b++) {
+    PgsBlk<T, EPL> k;
+    pgs_load_block<T, EPL>(k, Bsl, sc, bt, b, j);
+    const T* qf = sc + 4 * b * MGX_SCAL + 1;
+    bool ok = b < nblk;
+    T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[MGX_SCAL] : (T)0, f2 = ok ? qf[2 * MGX_SCAL] : (T)0,
+      f3 = ok ? qf[3 * MGX_SCAL] : (T)0;
+    pgs_update(k, v, f0, f1, f2, f3);
   }
   T cpart = 0;
-  for (int r = 0; r < neMax; r++) {
-    bool ok = r < ne;
-    T dot = 0;
+  for (int b = 0; b < nbMax; b++) {
+    PgsBlk<T, EPL> k;
+    pgs_load_block<T, EPL>(k, Bsl, sc, bt, b, j);
+    T d0, d1, d2, d3;
+    pgs_dots(k, v, d0, d1, d2, d3);
+    oct_sum4(d0, d1, d2, d3);
+    if (b < nblk) {
+      T dd[4] = {d0, d1, d2, d3};
+      const T* qq = sc + 4 * b * MGX_SCAL;
 #pragma unroll
-    for (int d = 0; d < DPL; d++) {
-      T b = Bs[(size_t)r * brow + 16 * d];
-      dot += (ok ? b : (T)0) * v[d];
+      for (int i = 0; i < 4; i++) {
+        const T* qi = qq + i * MGX_SCAL;
+        cpart += qi[1] * (qi[0] + (T)0.5 * (dd[i] + qi[2] * qi[1]));
+      }
     }
-    dot = row16_sum(dot);
-    const T* q = sc + r * MGX_SCAL;
-    if (ok) cpart += q[1] * (q[0] + (T)0.5 * (dot + q[2] * q[1]));
   }
   if (cpart > 0) {
-    for (int r = j; r < ne; r += 16) sc[r * MGX_SCAL + 1] = 0;
+    for (int r = j; r < ne; r += 8) sc[r * MGX_SCAL + 1] = 0;
 #pragma unroll
-    for (int d = 0; d < DPL; d++) v[d] = 0;
+    for (int d = 0; d < EPL; d++) v[d] = 0;
   }
   __syncthreads();
   bool act = ne > 0;
   int it = 0;
+#ifdef MGX_PROFILE
+  unsigned long long t_sweep0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r_sweep0 = __builtin_amdgcn_s_memrealtime();
+  int nsweep = 0;
+#endif
   for (int iter = 0; iter < maxit; iter++) {
     if (__ballot(act) == 0ull) break;
+#ifdef MGX_PROFILE
+    nsweep++;
+#endif
     T impr = 0;
-    T R0[4][DPL], R1[4][DPL], R2[4][DPL], R3[4][DPL];
-    pgs_load_block<T, DPL>(R0, Bs, 0, brow);
-    pgs_load_block<T, DPL>(R1, Bs, 4, brow);
-    pgs_load_block<T, DPL>(R2, Bs, 8, brow);
-    // full groups of 4 blocks: no early exit inside, so every prefetch is consumed on every
-    // path and the compiler cannot sink the loads next to their use
-    int r0 = 0;
-    for (; r0 + 16 <= ne4; r0 += 16) {
-      pgs_load_block<T, DPL>(R3, Bs, r0 + 12, brow);
-      pgs_block<T, DPL>(R0, v, sc, r0, ne, act, impr);
-      pgs_load_block<T, DPL>(R0, Bs, r0 + 16, brow);
-      pgs_block<T, DPL>(R1, v, sc, r0 + 4, ne, act, impr);
-      pgs_load_block<T, DPL>(R1, Bs, r0 + 20, brow);
-      pgs_block<T, DPL>(R2, v, sc, r0 + 8, ne, act, impr);
-      pgs_load_block<T, DPL>(R2, Bs, r0 + 24, brow);
-      pgs_block<T, DPL>(R3, v, sc, r0 + 12, ne, act, impr);
+    PgsBlk<T, EPL> R0, R1, R2;
+    pgs_load_block<T, EPL>(R0, Bsl, sc, bt, 0, j);
+    pgs_load_block<T, EPL>(R1, Bsl, sc, bt, 1, j);
+    // full groups of 3 blocks (ring of 3, 2 ahead): no early exit inside, so every prefetch is
+    // consumed on every path and the compiler cannot sink the loads next to their use. The
+    // table has zero entries up to its capacity, so the look-ahead past nbMax reads zeros.
+    for (int b0 = 0; b0 < nbRun; b0 += 3) {
+      pgs_load_block<T, EPL>(R2, Bsl, sc, bt, b0 + 2, j);
+      pgs_block<T, EPL>(R0, v, sc, 4 * b0, act && b0 < nblk, impr);
+      pgs_load_block<T, EPL>(R0, Bsl, sc, bt, min(b0 + 3, nbcap3 - 1), j);
+      pgs_block<T, EPL>(R1, v, sc, 4 * (b0 + 1), act && b0 + 1 < nblk, impr);
+      pgs_load_block<T, EPL>(R1, Bsl, sc, bt, min(b0 + 4, nbcap3 - 1), j);
+      pgs_block<T, EPL>(R2, v, sc, 4 * (b0 + 2), act && b0 + 2 < nblk, impr);
     }
-    // 0..3 remaining blocks, already in the ring
-    if (r0 < ne4) pgs_block<T, DPL>(R0, v, sc, r0, ne, act, impr);
-    if (r0 + 4 < ne4) pgs_block<T, DPL>(R1, v, sc, r0 + 4, ne, act, impr);
-    if (r0 + 8 < ne4) pgs_block<T, DPL>(R2, v, sc, r0 + 8, ne, act, impr);
     if (act) {
       it++;
       if (impr * scale < tol) act = false;
     }
   }
+#ifdef MGX_PROFILE
+  if (g_mgx_prof && l == 0) {
+    // solver diagnostics, one record per wave in slots 26..30 of the wave's profile row
+    unsigned long long* pr = g_mgx_prof + (size_t)blockIdx.x * 32;
+    pr[26] += __builtin_amdgcn_s_memtime() - t_sweep0;
+    pr[27] += (unsigned long long)nsweep * nbMax;
+    pr[28] += 1;
+    pr[29] += __builtin_amdgcn_s_memrealtime() - r_sweep0;
+    if ((unsigned long long)(nsweep * nbMax) > pr[30]) pr[30] = nsweep * nbMax;
+  }
+#endif
   if (slot >= 0) {
     T* vo = P.at<T>(P.o_vout) + (size_t)slot * 64;
 #pragma unroll
-    for (int d = 0; d < DPL; d++)
-      if (j + 16 * d < P.nv) vo[j + 16 * d] = v[d];
+    for (int d = 0; d < EPL; d++)
+      if (j + 8 * d < P.nv) vo[j + 8 * d] = v[d];
     if (j == 0) P.at<int>(P.o_niter)[slot] = it;
   }
 }

@@ -74,6 +74,15 @@ def main():
     print(f"  lds bytes per env: monolithic {env.native.info.lds_bytes_per_env} rows {env.native.info.lds_bytes_rows} "
           f"finish {env.native.info.lds_bytes_finish}")
     if staged:
+        k2 = raw[:, 28] > 0
+        if k2.any():
+            cyc, blks = raw[k2, 26].sum(), raw[k2, 27].sum()
+            print(f"  solver waves (block index = wave): {int(raw[k2, 28].sum())} wave-launches; sweep cycles per "
+                  f"block {cyc / max(blks, 1):.0f}; mean sweep cycles per wave-launch {cyc / raw[k2, 28].sum():.0f}")
+            rt = raw[k2, 29].sum()
+            print(f"  s_memtime ticks per s_memrealtime tick (100 MHz): {cyc / max(rt, 1):.2f} -> shader clock "
+                  f"{cyc / max(rt, 1) * 0.1:.2f} GHz; solver sweep time per wave-launch {rt / raw[k2, 28].sum() / 100:.1f} us "
+                  f"mean, blocks swept by the heaviest wave {raw[k2, 30].max():.0f} (mean {blks / raw[k2, 28].sum():.0f})")
         print(f"  per slot-step: nefc mean {(raw[:, 20].sum() / raw[:, 23].sum()):.1f}  ncon mean "
               f"{(raw[:, 22].sum() / raw[:, 23].sum()):.1f}  nefc max {raw[:, 24].max():.0f}  "
               f"slot-steps with capacity overflow {raw[:, 25].sum():.0f} of {raw[:, 23].sum():.0f}")

@@ -1,8 +1,11 @@
 """Summarise a tools/profile_round.sh run into small committed files under profiles/.
 
-HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB,
-collected in separate passes; on gfx950 FETCH_SIZE counts half the bytes of a wide coalesced
-read, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (the raw values are kept too).
+One env step is several launches (staged: k_soccer_rows, k_pgs_groups, k_soccer_finish,
+k_soccer_fixup; monolithic: k_soccer<.., 0>), each called once per step: the step's kernel
+time is the sum of their rocprof averages, and its HBM traffic the sum of their per-dispatch
+counter means. HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
+KiB, collected in separate passes; on gfx950 FETCH_SIZE counts half the bytes of a wide
+coalesced read, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (raw values kept too).
 """
 import csv
 import glob
@@ -11,7 +14,15 @@ import os
 import shutil
 import sys
 
-KERNEL = "k_soccer<float, 0>"
+STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_finish", "k_soccer_fixup", "k_soccer<float, 0>",
+                "k_soccer<double, 0>"]
+
+
+def step_kernel(name):
+    for k in STEP_KERNELS:
+        if k in name:
+            return k
+    return None
 
 
 def find(d, pat):
@@ -19,47 +30,55 @@ def find(d, pat):
     return g[0] if g else None
 
 
-def counter_mean(d, name):
+def counter_means(d, counter):
+    """mean counter value per dispatch, per step kernel"""
     f = find(d, "*counter_collection.csv")
     if not f:
-        return None, 0
-    vals = {}
+        return {}
+    per = {}
     for r in csv.DictReader(open(f)):
-        if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == name:
-            key = r.get("Dispatch_Id") or r.get("Correlation_Id")
-            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    if not vals:
-        return None, 0
-    return sum(vals.values()) / len(vals), len(vals)
+        k = step_kernel(r.get("Kernel_Name", ""))
+        if not k or r.get("Counter_Name") != counter:
+            continue
+        key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        per.setdefault(k, {})
+        per[k][key] = per[k].get(key, 0.0) + float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in per.items() if v}
 
 
 def main(out, tag):
     summ = os.path.join(out, "summary")
     os.makedirs(summ, exist_ok=True)
     stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
-    res = {"tag": tag}
+    res = {"tag": tag, "kernels": {}}
     if stats:
         shutil.copy(stats, os.path.join(summ, f"{tag}_kernel_stats.csv"))
         for r in csv.DictReader(open(stats)):
-            if KERNEL in r["Name"]:
-                res["rocprof_avg_ms"] = float(r["AverageNs"]) / 1e6
-                res["rocprof_calls"] = int(r["Calls"])
-                res["rocprof_pct"] = float(r["Percentage"])
+            k = step_kernel(r["Name"])
+            if k:
+                res["kernels"][k] = {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"]),
+                                     "pct": float(r["Percentage"])}
+        res["rocprof_step_ms"] = sum(v["avg_ms"] for v in res["kernels"].values())
     bj = os.path.join(out, "bench_under_rocprof.json")
     if os.path.exists(bj):
         line = [x for x in open(bj).read().splitlines() if x.startswith("{")]
         if line:
             b = json.loads(line[-1])
             shutil.copy(bj, os.path.join(summ, f"{tag}_bench_under_rocprof.json"))
-            res["bench_launch_ms_same_run"] = b["roofline"]["launch_ms"]
+            res["bench_step_ms_same_run"] = b["roofline"]["launch_ms"]
             res["envs"] = b["config"]["envs_per_gpu"]
             res["precision"] = b["dtype"]
-    fetch, nf = counter_mean(os.path.join(out, "pmc_fetch"), "FETCH_SIZE")
-    write, nw = counter_mean(os.path.join(out, "pmc_write"), "WRITE_SIZE")
-    if fetch is not None and write is not None:
-        res.update({"fetch_size_kib_raw": fetch, "write_size_kib_raw": write, "dispatches": [nf, nw],
-                    "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
-                    "correction": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md §HBM"})
+            res["mode"] = b["config"].get("step_kernels", "staged")
+    fetch = counter_means(os.path.join(out, "pmc_fetch"), "FETCH_SIZE")
+    write = counter_means(os.path.join(out, "pmc_write"), "WRITE_SIZE")
+    if fetch and write:
+        for k in set(fetch) | set(write):
+            kk = res["kernels"].setdefault(k, {})
+            kk["fetch_kib_raw"] = fetch.get(k, 0.0)
+            kk["write_kib_raw"] = write.get(k, 0.0)
+            kk["hbm_bytes"] = (2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024
+        res["hbm_bytes_per_step"] = sum(v.get("hbm_bytes", 0.0) for v in res["kernels"].values())
+        res["correction"] = "(2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md §HBM"
     with open(os.path.join(summ, f"{tag}_pmc.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
