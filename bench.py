@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+PMC_PROFILE = "r01_v4_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
@@ -109,7 +110,7 @@ def main():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-envs", type=int, default=16)
-    ap.add_argument("--cpu-steps", type=int, default=800)
+    ap.add_argument("--cpu-steps", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
@@ -168,7 +169,7 @@ def main():
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         mode = "mono" if args.mono else "staged"
-        pmc = os.path.join(ROOT, "profiles", "r01_pmc.json")
+        pmc = os.path.join(ROOT, "profiles", PMC_PROFILE)
         if os.path.exists(pmc):
             try:
                 with open(pmc) as f:
