@@ -215,6 +215,69 @@ typedef struct mgx_soccer_logic_io {
 } mgx_soccer_logic_io;
 int mgx_soccer_logic_test(const mgx_model *m, const mgx_soccer_logic_io *io, int n_env, void *stream);
 
+/* ---- quadruped_parkour env logic fused with physics -------------------------------- */
+/* Index tables (quadruped_parkour_env/parkour_env.py:180-222, :757-795). */
+typedef struct mgx_parkour_ids {
+  int32_t torso, feet[4];          /* body ids: torso, fl/fr/bl/br_foot (feet compared with contact
+                                      GEOM ids, parkour_env.py:481, quirk P2) */
+  int32_t platform_qpos, pendulum_qpos; /* joint ids of platform_slide / pendulum_swing, used as
+                                           qpos indices by _randomize_obstacles (quirk P1) */
+  int32_t platform_act, pendulum_act;   /* actuator ids of the obstacle motors (-1 = absent) */
+  int32_t n_leg;                        /* 16 leg actuators written from the action */
+  int32_t max_episode_steps;            /* 6000 (parkour_env.py:41) */
+  float act_lim[16];                    /* action_space bounds (parkour_env.py:236-249) */
+} mgx_parkour_ids;
+
+/* Persistent per-env task state (device, env-major). Real buffers follow the precision. */
+typedef struct mgx_parkour_env {
+  void *last_position;      /* [N][3]  parkour_env.py:59 */
+  void *max_progress;       /* [N]     max_forward_progress */
+  double *episode_reward;   /* [N]     episode_reward (numpy promotion kind in er_kind) */
+  uint8_t *er_kind;         /* [N]     0 Python float, 1 np.float64, 2 np.float32 */
+  int32_t *reached;         /* [N]     checkpoints_reached as a bitmask: bits 0-5 checkpoints
+                                       15..90, bits 6-17 the 12 obstacle keys (parkour_env.py:669-684) */
+  int32_t *fall_count;      /* [N] */
+  int32_t *stuck;           /* [N]     stuck_counter */
+  int32_t *step;            /* [N]     step_count */
+  int32_t *episode;         /* [N]     episodes started (keys the device reset draws); nullable
+                                       when every reset passes host draws */
+  void *rollout;            /* [N][4]  reward, terminated, truncated, env steps (nullable) */
+} mgx_parkour_env;
+
+int mgx_parkour_configure(mgx_model *m, const mgx_parkour_ids *ids);
+
+/* One env step for N envs (parkour_env.py:356-394): action clip, ctrl[:16], 10 mj_step's,
+ * obstacle motors, observation [N][95] float32, reward [N] float64, terminated/truncated.
+ * autoreset != 0: envs that end are reset in the same launch (Philox draws keyed by
+ * (seed, env_offset + env, episode)); obs then holds the reset observation and final_obs
+ * (nullable) the last one. */
+int mgx_parkour_step(const mgx_model *m, const mgx_state *s, const mgx_parkour_env *e, const float *action,
+                     float *obs, double *reward, uint8_t *terminated, uint8_t *truncated, float *final_obs,
+                     int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t *env_mask,
+                     void *stream);
+
+/* reset() for masked envs (parkour_env.py:314-354): mj_resetData, start pose, the 2 obstacle
+ * draws (`draws` [N][2] real in reference order, e.g. numpy PCG64; NULL = device Philox),
+ * tracking reset, 10 settle mj_step's, obs. */
+int mgx_parkour_reset(const mgx_model *m, const mgx_state *s, const mgx_parkour_env *e, const void *draws,
+                      float *obs, uint64_t seed, int env_offset, int n_env, const uint8_t *env_mask, void *stream);
+
+/* Test hook: parkour env logic only (clip/ctrl, obstacle motors, obs, reward, termination,
+ * counters) on caller-supplied frames and contact lists (no physics). */
+typedef struct mgx_parkour_logic_io {
+  const void *qpos, *qvel, *xpos;   /* [N][nq] [N][nv] [N][nbody][3] */
+  const int32_t *ncon, *con_geom;   /* [N], [N][max_contacts][2] */
+  int32_t max_contacts;
+  int32_t pad0;
+  void *ctrl;                       /* in/out [N][nu] */
+  const float *action;              /* [N][16] */
+  float *obs;                       /* [N][95] */
+  double *reward;
+  uint8_t *terminated, *truncated;
+} mgx_parkour_logic_io;
+int mgx_parkour_logic_test(const mgx_model *m, const mgx_parkour_logic_io *io, const mgx_parkour_env *e, int n_env,
+                           void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,13 +6,15 @@ Public surface:
   batch.PhysicsBatch         N env states on one GPU + mgx_step (mujoco.mj_step)
   envs.SoccerVectorEnv       batched humanoid_soccer (device tensors)
   envs.HumanoidSoccerEnv     drop-in gymnasium-style single env
+  envs.ParkourVectorEnv      batched quadruped_parkour (10 substeps per env step)
+  envs.QuadrupedParkourEnv   drop-in gymnasium-style single env
 The compute path is libmgx.so (HIP, gfx950); there is no CPU fallback.
 """
 __version__ = "0.1.0"
 
 
 def __getattr__(name):  # lazy: importing the package must not require a GPU
-    if name in ("HumanoidSoccerEnv", "SoccerVectorEnv", "register_envs"):
+    if name in ("HumanoidSoccerEnv", "SoccerVectorEnv", "register_envs", "ParkourVectorEnv", "QuadrupedParkourEnv"):
         from . import envs
         return getattr(envs, name)
     raise AttributeError(name)

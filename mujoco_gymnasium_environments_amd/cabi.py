@@ -89,6 +89,25 @@ class MgxSoccerLogicIO(C.Structure):
                 ("truncated", C.c_void_p), ("flags", C.c_void_p)]
 
 
+class MgxParkourIds(C.Structure):
+    _fields_ = [("torso", C.c_int32), ("feet", C.c_int32 * 4), ("platform_qpos", C.c_int32),
+                ("pendulum_qpos", C.c_int32), ("platform_act", C.c_int32), ("pendulum_act", C.c_int32),
+                ("n_leg", C.c_int32), ("max_episode_steps", C.c_int32), ("act_lim", C.c_float * 16)]
+
+
+class MgxParkourEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ["last_position", "max_progress", "episode_reward", "er_kind", "reached", "fall_count", "stuck",
+                 "step", "episode", "rollout"]]
+
+
+class MgxParkourLogicIO(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("xpos", C.c_void_p), ("ncon", C.c_void_p),
+                ("con_geom", C.c_void_p), ("max_contacts", C.c_int32), ("pad0", C.c_int32), ("ctrl", C.c_void_p),
+                ("action", C.c_void_p), ("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p),
+                ("truncated", C.c_void_p)]
+
+
 class MgxSoccerIds(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ["torso", "ball", "goalkeeper", "ball_geom", "right_foot", "left_foot", "field_geom",

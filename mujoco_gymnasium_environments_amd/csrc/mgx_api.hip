@@ -10,8 +10,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/mgx.h"
-#include "mgx_staged.h"
+#include "mgx_internal.h"
 
 using namespace mgx;
 
@@ -31,26 +30,12 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-#define HIPCHK(x)                                                                  \
-  do {                                                                             \
-    hipError_t _e = (x);                                                           \
-    if (_e != hipSuccess) return fail(MGX_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
-  } while (0)
+#define HIPCHK(x) MGX_HIPCHK(x)
 }  // namespace
 
-struct mgx_model {
-  int precision;
-  int device;
-  void* dbuf = nullptr;
-  size_t dbytes = 0;
-  DevModel<float> mf, mfs, mff;   // monolithic / staged row builder / staged finisher layouts
-  DevModel<double> md, mds, mdf;
-  Layout L, Ls, Lf;
-  bool soccer_ok = false;
-  SoccerIds<float> sf;
-  SoccerIds<double> sd;
-  int npair;
-};
+namespace mgx {
+int host_fail(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace mgx
 
 // ------------------------------------------------------------------------- kernels
 template <typename T>
@@ -656,18 +641,19 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
 }
 
 template <typename KernelT>
-int set_lds(KernelT k, int bytes) {
-  if (bytes > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  return MGX_OK;
-}
+int set_lds(KernelT k, int bytes) { return mgx_set_lds(k, bytes); }
 
-int check_state(const mgx_state* s) {
+int check_state(const mgx_state* s) { return mgx::host_check_state(s); }
+
+}  // namespace
+
+namespace mgx {
+int host_check_state(const mgx_state* s) {
   if (!s || !s->qpos || !s->qvel || !s->qacc_warmstart || !s->ctrl || !s->qfrc_applied || !s->xfrc_applied || !s->time)
     return fail(MGX_E_ARG, "null state buffer");
   return MGX_OK;
 }
-
-}  // namespace
+}  // namespace mgx
 
 // Staged-step workspace layout for (model, n_env, banks); offsets in bytes, 256-aligned.
 static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P) {

@@ -1,0 +1,45 @@
+// mgx_internal.h — host-side definitions shared by the translation units of libmgx.so
+// (mgx_api.hip: model, physics and soccer; mgx_parkour.hip: quadruped_parkour).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/mgx.h"
+#include "mgx_parkour.h"
+#include "mgx_staged.h"
+
+struct mgx_model {
+  int precision;
+  int device;
+  void* dbuf = nullptr;
+  size_t dbytes = 0;
+  mgx::DevModel<float> mf, mfs, mff;   // monolithic / staged row builder / staged finisher layouts
+  mgx::DevModel<double> md, mds, mdf;
+  mgx::Layout L, Ls, Lf;
+  bool soccer_ok = false;
+  mgx::SoccerIds<float> sf;
+  mgx::SoccerIds<double> sd;
+  bool parkour_ok = false;
+  mgx::ParkourIds<float> pkf;
+  mgx::ParkourIds<double> pkd;
+  int npair;
+};
+
+namespace mgx {
+// records the message returned by mgx_last_error() and returns `code`
+int host_fail(int code, const std::string& msg);
+int host_check_state(const mgx_state* s);
+}  // namespace mgx
+
+#define MGX_HIPCHK(x)                                                                                   \
+  do {                                                                                                  \
+    hipError_t _e = (x);                                                                                \
+    if (_e != hipSuccess) return mgx::host_fail(MGX_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename KernelT>
+int mgx_set_lds(KernelT k, int bytes) {
+  if (bytes > 64 * 1024) MGX_HIPCHK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  return MGX_OK;
+}

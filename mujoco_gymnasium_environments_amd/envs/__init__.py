@@ -1,2 +1,4 @@
-"""Task environments. humanoid_soccer is the headline task (BASELINE.json)."""
+"""Task environments. humanoid_soccer is the headline task (BASELINE.json); quadruped_parkour is
+the low-DoF bring-up task (BASELINE configs 1-2)."""
+from .parkour import ParkourVectorEnv, QuadrupedParkourEnv  # noqa: F401
 from .soccer import HumanoidSoccerEnv, SoccerVectorEnv, register_envs  # noqa: F401

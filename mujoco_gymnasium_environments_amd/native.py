@@ -15,8 +15,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = ["mgx_api.hip"]
-HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h"]
+SOURCES = ["mgx_api.hip", "mgx_parkour.hip"]
+HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
+           "mgx_internal.h"]
 
 MGX_OK = 0
 MGX_F32 = 0
@@ -35,11 +36,24 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if all(os.path.getmtime(s) <= lib_t for s in srcs):
             return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", LIB_PATH + ".tmp", os.path.join(CSRC, "mgx_api.hip")]
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
+    build_dir = os.path.join(PKG, "_build")
+    os.makedirs(build_dir, exist_ok=True)
+    # one translation unit per task family, compiled in parallel, then linked
+    procs = []
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(build_dir, src.replace(".hip", ".o"))
+        objs.append(obj)
+        procs.append((src, subprocess.Popen([hipcc, *flags, "-c", "-o", obj, os.path.join(CSRC, src)],
+                                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+    for src, p in procs:
+        _, err = p.communicate()
+        if p.returncode != 0:
+            raise NativeError(f"hipcc {src} failed ({p.returncode}):\n{err[-4000:]}")
+    r = subprocess.run([hipcc, *flags, "-shared", "-o", LIB_PATH + ".tmp", *objs], capture_output=True, text=True)
     if r.returncode != 0:
-        raise NativeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+        raise NativeError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-4000:]}")
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     if verbose:
         print(f"built {LIB_PATH}")
@@ -67,6 +81,13 @@ _SIGS = {
     "mgx_soccer_logic_test": ([_VP, C.POINTER(cabi.MgxSoccerLogicIO), C.c_int, _VP], C.c_int),
     "mgx_soccer_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
     "mgx_soccer_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
+    "mgx_parkour_configure": ([_VP, C.POINTER(cabi.MgxParkourIds)], C.c_int),
+    "mgx_parkour_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxParkourEnv), _VP, _VP, _VP, _VP, _VP,
+                          _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_parkour_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxParkourEnv), _VP, _VP, C.c_uint64,
+                           C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_parkour_logic_test": ([_VP, C.POINTER(cabi.MgxParkourLogicIO), C.POINTER(cabi.MgxParkourEnv), C.c_int, _VP],
+                               C.c_int),
 }
 EXPORTS = tuple(_SIGS)
 

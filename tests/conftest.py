@@ -28,3 +28,16 @@ def soccer_model(soccer_xml):
 def soccer_packed(soccer_model):
     from mujoco_gymnasium_environments_amd import cabi
     return cabi.pack_model(soccer_model)
+
+
+@pytest.fixture(scope="session")
+def parkour_model():
+    from mujoco_gymnasium_environments_amd import mjcf
+    with open(os.path.join(ROOT, "mujoco_gymnasium_environments_amd", "assets", "quadruped_parkour.xml")) as f:
+        return mjcf.compile_xml(f.read())
+
+
+@pytest.fixture(scope="session")
+def parkour_packed(parkour_model):
+    from mujoco_gymnasium_environments_amd import cabi
+    return cabi.pack_model(parkour_model)

@@ -148,6 +148,7 @@ class FakeData:
         self.xfrc_applied = np.zeros((c.nbody, 6))
         self.xpos = np.zeros((c.nbody, 3))
         self.xquat = np.tile([1.0, 0, 0, 0], (c.nbody, 1))
+        self.xmat = np.tile(np.eye(3).reshape(-1), (c.nbody, 1))
         self.subtree_com = np.zeros((c.nbody, 3))
         self.contact = []
         self.ncon = 0
@@ -343,12 +344,114 @@ def _pad(a, n, w=None, fill=0.0):
     return out
 
 
+# ------------------------------------------------------------------------------- parkour
+PARKOUR_OBSTACLES = [8.0, 16.0, 24.0, 30.0, 36.0, 44.0, 50.0, 58.0, 72.0, 78.0, 88.0, 92.0]
+PARKOUR_CHECKPOINTS = [15, 30, 45, 60, 75, 90]
+
+
+def parkour_env():
+    install_stubs()
+    mod = load_module(f"{REF}/quadruped_parkour_env/parkour_env.py", "ref_parkour_env2")
+    return mod.QuadrupedParkourEnv(render_mode=None)
+
+
+def _parkour_keys(env):
+    """bit k of the reached-mask <-> key k of checkpoints_reached: 6 checkpoints, 12 obstacles"""
+    return list(PARKOUR_CHECKPOINTS) + [f"{x}_{t}" for x, t in env.obstacle_positions]
+
+
+def parkour_reset_vectors(env, seeds):
+    """reset(seed) (parkour_env.py:314-354): the randomised qpos before the settle steps (the
+    stub mj_step does not move the state)."""
+    rows = []
+    for s in seeds:
+        env.reset(seed=int(s))
+        rows.append(env.data.qpos.copy())
+    return dict(seeds=np.asarray(seeds, np.int64), qpos=np.stack(rows))
+
+
+def parkour_envlogic_vectors(env, n, seed=4321, max_contacts=14):
+    """Random synthetic MjData-like states -> the reference's own step() (parkour_env.py:356-394)
+    with physics stubbed out: clip + ctrl write, dynamic obstacles, obs, reward, termination,
+    truncation, counters and info."""
+    c = env.model._c
+    rng = np.random.default_rng(seed)
+    keys = _parkour_keys(env)
+    torso = env.torso_id
+    feet = list(env.foot_ids.values())
+    nb = c.nbody
+    cols = {k: [] for k in ["qpos", "qvel", "xpos", "ncon", "con_geom", "action", "ctrl_in", "last_position_in",
+                            "max_progress_in", "reached_in", "fall_count_in", "stuck_in", "step_count_in",
+                            "episode_reward_in",
+                            "obs", "reward", "terminated", "truncated", "ctrl_out", "last_position_out",
+                            "max_progress_out", "reached_out", "fall_count_out", "stuck_out", "step_count_out",
+                            "episode_reward_out", "course_completion"]}
+    for i in range(n):
+        d = env.data
+        d.reset()
+        scen = i % 10
+        qpos = c.qpos0.copy()
+        qpos[:] = rng.normal(scale=0.8, size=c.nq)
+        q = rng.normal(size=4)
+        if scen in (1, 2):
+            q = np.array([rng.uniform(0.6, 1.0), *rng.normal(scale=0.3, size=3)])
+        qpos[3:7] = q / np.linalg.norm(q) if scen != 3 else q  # scen 3: unnormalised
+        d.qpos[:] = qpos
+        d.qvel[:] = rng.normal(scale=rng.choice([0.5, 5.0, 30.0]), size=c.nv)
+        xpos = rng.uniform(-1, 1, (nb, 3))
+        x = float(rng.choice([rng.uniform(-5, 105), rng.choice([15, 30, 45, 60, 75, 90, 98]) + rng.uniform(-0.02, 0.02),
+                              rng.choice(PARKOUR_OBSTACLES) + 2 + rng.uniform(-0.02, 0.02)]))
+        xpos[torso] = [x, rng.choice([rng.uniform(-11, 11), rng.uniform(-1, 1)]),
+                       rng.choice([rng.uniform(0.1, 0.25), rng.uniform(0.1, 0.8)])]
+        for f in feet:
+            xpos[f] = xpos[torso] + rng.normal(scale=0.3, size=3)
+        d.xpos[:] = xpos
+        ncon = int(rng.integers(0, max_contacts + 1))
+        geoms = rng.integers(0, c.ngeom, (ncon, 2))
+        if scen in (4, 5, 6) and ncon:  # geom ids that equal the feet's BODY ids (quirk P2)
+            for k in range(min(ncon, int(rng.integers(1, 5)))):
+                geoms[k, int(rng.integers(0, 2))] = feet[int(rng.integers(0, 4))]
+        d.contact = [FakeContact(g[0], g[1], 0.0, np.zeros(5)) for g in geoms]
+        d.ncon = ncon
+        d.ctrl[:] = rng.normal(size=c.nu)
+        ctrl_in = d.ctrl.copy()
+        prog = float(rng.choice([rng.uniform(-0.3, 0.3), rng.uniform(-0.012, 0.012), rng.uniform(-0.12, -0.08)]))
+        env.last_position = np.array([x - prog, rng.normal(), rng.normal()])
+        env.max_forward_progress = float(rng.uniform(0, 100))
+        mask = int(rng.integers(0, 1 << 18)) if scen in (7, 8) else 0
+        env.checkpoints_reached = {k for b, k in enumerate(keys) if (mask >> b) & 1}
+        env.fall_count = int(rng.integers(0, 5))
+        env.stuck_counter = int(rng.choice([0, 99, 100, 101, 999, 1000, 1001, int(rng.integers(0, 1200))]))
+        env.step_count = int(rng.choice([0, 1, 5999, 6000, 6001, int(rng.integers(0, 7000))]))
+        env.episode_reward = float(rng.normal(scale=1e4))
+        inp = dict(qpos=qpos, qvel=d.qvel.copy(), xpos=xpos, ncon=ncon, con_geom=_pad(geoms, max_contacts, 2, -1),
+                   ctrl_in=ctrl_in, last_position_in=env.last_position.copy(), max_progress_in=env.max_forward_progress,
+                   reached_in=mask, fall_count_in=env.fall_count, stuck_in=env.stuck_counter,
+                   step_count_in=env.step_count, episode_reward_in=env.episode_reward)
+        lim = env.action_space.high
+        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim).astype(np.float32)
+        obs, reward, term, trunc, info = env.step(action)
+        reached = sum(1 << b for b, k in enumerate(keys) if k in env.checkpoints_reached)
+        out = dict(action=action, obs=obs, reward=float(reward), terminated=bool(term), truncated=bool(trunc),
+                   ctrl_out=d.ctrl.copy(), last_position_out=np.asarray(env.last_position, np.float64),
+                   max_progress_out=env.max_forward_progress, reached_out=reached, fall_count_out=env.fall_count,
+                   stuck_out=env.stuck_counter, step_count_out=env.step_count,
+                   episode_reward_out=float(env.episode_reward), course_completion=info["course_completion"])
+        assert info["checkpoints_reached"] == len(env.checkpoints_reached)
+        for k, v in {**inp, **out}.items():
+            cols[k].append(v)
+    return {k: np.asarray(v) for k, v in cols.items()}
+
+
 def main():
     install_stubs()
     dump_xml()
     env = soccer_env()
     np.savez_compressed(f"{HERE}/soccer_reset.npz", **soccer_reset_vectors(env, list(range(0, 40)) + [12345, 2**31 - 1]))
     np.savez_compressed(f"{HERE}/soccer_envlogic.npz", **soccer_envlogic_vectors(env, 400))
+    penv = parkour_env()
+    np.savez_compressed(f"{HERE}/parkour_reset.npz", **parkour_reset_vectors(penv, list(range(0, 40)) + [12345]))
+    np.savez_compressed(f"{HERE}/parkour_envlogic.npz", **parkour_envlogic_vectors(penv, 500))
     print("fixtures written to", HERE)
 
 

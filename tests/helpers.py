@@ -4,14 +4,17 @@ import numpy as np
 STATE_FIELDS = ("qpos", "qvel", "qacc_warmstart", "ctrl", "qfrc_applied", "xfrc_applied")
 
 
-def oracle_states(packed, n, seed=0, max_steps=60, action_scale=150.0):
-    """n oracle states reached from qpos0 under random actions (snapshot before a step)."""
+def oracle_states(packed, n, seed=0, max_steps=60, action_scale=150.0, init=None):
+    """n oracle states reached from qpos0 (with qpos overrides ``init`` {index: value}) under
+    random actions (snapshot before a step)."""
     from oracle.mjref import RefSim
     rng = np.random.default_rng(seed)
     m = packed.model
     out = []
     for i in range(n):
         s = RefSim(packed)
+        for a, v in (init or {}).items():
+            s.qpos[a] = v
         k = int(rng.integers(0, max_steps))
         for _ in range(k):
             s.ctrl[:] = rng.uniform(-action_scale, action_scale, m.nu)

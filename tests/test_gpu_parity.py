@@ -18,9 +18,17 @@ pytestmark = pytest.mark.gpu
 N = 8
 
 
-@pytest.fixture(scope="module")
-def states(soccer_packed):
-    return oracle_states(soccer_packed, N, seed=7)
+@pytest.fixture(scope="module", params=["soccer", "parkour"])
+def case(request, soccer_model, soccer_packed, parkour_model, parkour_packed):
+    """(model, packed model, oracle states): humanoid_soccer (dt 0.02, 5 primitive pair types) and
+    quadruped_parkour (dt 0.001, plane pairs, ~30 contacts / ~128 rows when grounded)."""
+    if request.param == "soccer":
+        return soccer_model, soccer_packed, oracle_states(soccer_packed, N, seed=7)
+    return parkour_model, parkour_packed, oracle_states(parkour_packed, N, seed=7, max_steps=600,
+                                                       action_scale=20.0, init=PARKOUR_START)
+
+
+PARKOUR_START = {0: 2.0, 1: 0.0, 2: 0.6}  # parkour_env.py:328-331
 
 
 def _batch(model, prec, n=N):
@@ -33,15 +41,15 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("prec", ["f64", "f32"])
-def test_forward_stages(soccer_model, soccer_packed, states, prec):
-    m = soccer_model
+def test_forward_stages(case, prec):
+    m, packed, states = case
     b = _batch(m, prec)
     load_states(b, states)
     dbg = b.debug_forward()
     tol_k = 1e-10 if prec == "f64" else 2e-5
     tol_m = 1e-9 if prec == "f64" else 1e-4
     for i, st in enumerate(states):
-        o = oracle_at(soccer_packed, st)
+        o = oracle_at(packed, st)
         o.forward()
         nb = m.nbody
         np.testing.assert_allclose(dbg["xpos"][i], o.xpos, atol=tol_k, err_msg=f"xpos env {i}")
@@ -80,16 +88,17 @@ def test_forward_stages(soccer_model, soccer_packed, states, prec):
 
 
 @pytest.mark.parametrize("prec", ["f64", "f32"])
-def test_one_step(soccer_model, soccer_packed, states, prec):
+def test_one_step(case, prec):
     import torch
-    b = _batch(soccer_model, prec)
+    m, packed, states = case
+    b = _batch(m, prec)
     load_states(b, states)
     b.step(1)
     torch.cuda.synchronize()
     qpos = b.qpos.double().cpu().numpy()
     qvel = b.qvel.double().cpu().numpy()
     for i, st in enumerate(states):
-        o = oracle_at(soccer_packed, st)
+        o = oracle_at(packed, st)
         o.step()
         tol = 1e-6 if prec == "f64" else 2e-3
         assert np.max(np.abs(qpos[i] - o.qpos)) < tol * max(1, np.abs(o.qpos).max()), f"qpos env {i}"
@@ -97,16 +106,19 @@ def test_one_step(soccer_model, soccer_packed, states, prec):
         assert np.max(np.abs(qvel[i] - o.qvel)) < (1e-4 if prec == "f64" else 5e-2) * vscale, f"qvel env {i}"
 
 
-def test_rollout_f64_zero_action(soccer_model, soccer_packed):
-    """Non-chaotic settle from qpos0 (zero ctrl): trajectories agree over 200 steps."""
+@pytest.mark.parametrize("task,nsub,nstep", [("soccer", 1, 200), ("parkour", 10, 100)])
+def test_rollout_f64_zero_action(task, nsub, nstep, soccer_model, soccer_packed, parkour_model, parkour_packed):
+    """Non-chaotic settle from qpos0 (zero ctrl): trajectories agree over 200 soccer steps /
+    1000 parkour substeps (100 env steps of 10 mj_step's each, parkour_env.py:367-368)."""
     import torch
     from oracle.mjref import RefSim
-    b = _batch(soccer_model, "f64", n=2)
-    o = RefSim(soccer_packed)
+    model, packed = (soccer_model, soccer_packed) if task == "soccer" else (parkour_model, parkour_packed)
+    b = _batch(model, "f64", n=2)
+    o = RefSim(packed)
     worst = 0.0
-    for t in range(200):
-        b.step(1)
-        o.step()
+    for t in range(nstep):
+        b.step(nsub)
+        o.step(nsub)
         q = b.qpos[0].cpu().numpy()
         worst = max(worst, float(np.max(np.abs(q - o.qpos))))
     torch.cuda.synchronize()

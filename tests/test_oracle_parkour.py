@@ -1,0 +1,79 @@
+"""CPU: pin the quadruped_parkour env-logic oracle and reset draws to the reference's outputs.
+
+Golden vectors (tests/golden/parkour_*.npz) come from the reference's own step() and reset()
+(parkour_env.py:314-394) run on synthetic MjData-like state with physics stubbed out; see
+tests/golden/make_fixtures.py. Bars: observation, reward, flags, counters, reached-mask and
+the obstacle-motor ctrl are bit-exact (the oracle reproduces the reference's float32/float64
+promotion of the reward, oracle/parkour_logic.py).
+"""
+import numpy as np
+import pytest
+
+from mujoco_gymnasium_environments_amd.seeding import np_random
+from oracle.parkour_logic import ParkourLogic, ParkourTables
+
+G = "tests/golden/"
+
+
+@pytest.fixture(scope="module")
+def tables(parkour_model):
+    return ParkourTables(parkour_model)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return dict(np.load(G + "parkour_envlogic.npz"))
+
+
+def state_from_golden(g, i):
+    n = int(g["ncon"][i])
+    return dict(qpos=g["qpos"][i].copy(), qvel=g["qvel"][i].copy(), xpos=g["xpos"][i].copy(),
+                ncon=n, con_geom=g["con_geom"][i][:n].astype(int), ctrl=g["ctrl_in"][i].copy(),
+                last_position=g["last_position_in"][i].copy(), max_progress=float(g["max_progress_in"][i]),
+                reached=int(g["reached_in"][i]), fall_count=int(g["fall_count_in"][i]), stuck=int(g["stuck_in"][i]),
+                step_count=int(g["step_count_in"][i]), episode_reward=float(g["episode_reward_in"][i]), er_kind=0)
+
+
+def test_golden_fixture_coverage(golden):
+    n = golden["obs"].shape[0]
+    assert golden["obs"].shape == (n, 95) and golden["action"].shape == (n, 16)
+    for k in ("terminated", "truncated"):
+        assert golden[k].any() and (~golden[k]).any(), k
+    assert (golden["obs"][:, 45:49] != 0).any(), "foot-contact quirk (geom id == body id) exercised"
+    assert (golden["reached_out"] != golden["reached_in"]).any()
+    assert (golden["fall_count_out"] > golden["fall_count_in"]).any()
+
+
+def test_parkour_logic_matches_reference(tables, golden):
+    L = ParkourLogic(tables)
+    n = golden["obs"].shape[0]
+    for i in range(n):
+        s = state_from_golden(golden, i)
+        a = L.pre(s, golden["action"][i])
+        np.testing.assert_array_equal(s["ctrl"][:16], golden["ctrl_out"][i][:16])
+        o, r, term, trunc = L.post(s, a)
+        np.testing.assert_array_equal(o, golden["obs"][i], err_msg=f"obs case {i}")
+        assert r == golden["reward"][i], (i, r, golden["reward"][i])
+        assert term == bool(golden["terminated"][i]) and trunc == bool(golden["truncated"][i]), i
+        np.testing.assert_array_equal(s["ctrl"], golden["ctrl_out"][i])
+        assert s["reached"] == golden["reached_out"][i], i
+        assert s["fall_count"] == golden["fall_count_out"][i] and s["stuck"] == golden["stuck_out"][i], i
+        assert s["step_count"] == golden["step_count_out"][i], i
+        assert s["max_progress"] == golden["max_progress_out"][i], i
+        np.testing.assert_array_equal(s["last_position"], golden["last_position_out"][i])
+        assert s["episode_reward"] == golden["episode_reward_out"][i], (i, s["episode_reward"])
+        assert L.course_completion(s, golden["xpos"][i][tables.torso][0]) == golden["course_completion"][i]
+
+
+def test_parkour_reset_draws(tables, parkour_model):
+    g = np.load(G + "parkour_reset.npz")
+    L = ParkourLogic(tables)
+    for seed, q in zip(g["seeds"], g["qpos"]):
+        rng, _ = np_random(int(seed))
+        s = dict(qpos=np.zeros(parkour_model.nq), qvel=np.zeros(parkour_model.nv))
+        L.apply_reset(s, tables.reset_draws(rng))
+        np.testing.assert_array_equal(s["qpos"], q)
+    # quirk P1: the draws land on bl_knee / bl_ankle, not on the platform / pendulum joints
+    m = parkour_model
+    assert m.id2name("joint", 11) == "bl_knee" and m.jnt_qposadr[11] == tables.platform_qpos
+    assert m.id2name("joint", 12) == "bl_ankle" and m.jnt_qposadr[12] == tables.pendulum_qpos
