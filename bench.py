@@ -12,6 +12,10 @@ Reset settle steps of the precomputed reset banks run inside the same launches. 
 synthetic U(-150, 150)^33 float32 drawn before the timed region and resident in HBM.
 Ranks shard envs (global index = rank * envs + i); the only collective is the end-of-rollout
 metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
+
+--task parkour benchmarks BASELINE configs[1] instead (quadruped_parkour, 4096 envs/GPU): one
+step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obstacle motors,
+obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
 """
 from __future__ import annotations
 
@@ -35,6 +39,11 @@ PMC_PROFILE = "r01_v4_pmc.json"  # latest tools/profile_round.sh summary (HBM tr
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
 ALG_BYTES_PER_ENV_STEP = 4 * (2 * 121 + 33 + 2 * 3 + 2 * 11 + 80) + 8 + 2
+# parkour: r/w qpos 38 + qvel 37 + qacc_warmstart 37, r/w the 2 obstacle-motor
+# ctrl, read action 16, r/w last_position 3 + max_progress 1 (fp32), r/w episode_reward (fp64)
+# + er_kind (u8) + reached/fall/stuck/step (int32), write obs 95, reward (fp64), flags (u8)
+PARKOUR_ALG_BYTES = 4 * (2 * 112 + 2 * 2 + 16 + 2 * 4 + 95) + 2 * 8 + 2 + 2 * 16 + 8 + 2
+PARKOUR_METRIC = "env steps/sec (whole node), quadruped_parkour 4096 envs/GPU (BASELINE configs[1])"
 
 
 def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
@@ -102,6 +111,53 @@ def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
             "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
 
 
+def cpu_baseline_parkour(n_envs: int, n_steps: int, seed: int = 0) -> dict:
+    """Oracle port on one host core: mjref (C, fp64) physics x 10 substeps + numpy env logic."""
+    from mujoco_gymnasium_environments_amd import cabi
+    from mujoco_gymnasium_environments_amd.envs.parkour import action_limits, parkour_model
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.mjref import RefSim
+    from oracle.parkour_logic import ParkourLogic, ParkourTables
+    m = parkour_model()
+    pk = cabi.pack_model(m)
+    L = ParkourLogic(ParkourTables(m))
+    rng = np.random.default_rng(seed)
+    acts = (rng.uniform(-1, 1, (64, 16)) * action_limits()).astype(np.float32)
+    total = 0
+    t0 = time.perf_counter()
+    for e in range(n_envs):
+        sim = RefSim(pk)
+        er = np_random(seed + e)[0]
+        s = {}
+
+        def view():
+            c = sim.contacts()
+            s.update(qpos=sim.qpos, qvel=sim.qvel, ctrl=sim.ctrl, xpos=sim.xpos.reshape(-1, 3), con_geom=c["geom"],
+                     ncon=int(sim.ncon[0]))
+
+        def reset():
+            sim.reset()
+            view()
+            L.apply_reset(s, L.t.reset_draws(er))
+            sim.step(10)
+            view()
+        reset()
+        for k in range(n_steps):
+            a = L.pre(s, acts[k % 64])
+            sim.step(10)
+            view()
+            _, _, term, trunc = L.post(s, a)
+            total += 1
+            if term or trunc:
+                reset()
+    dt = time.perf_counter() - t0
+    return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_envs} envs x {n_steps} steps (10 substeps each, autoreset) of quadruped_parkour, "
+                      f"U(-lim, lim) actions, oracle/mjref.c fp64 physics + oracle/parkour_logic.py; CPU MuJoCo "
+                      f"unavailable (not installed)",
+            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,7 +170,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
+    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour"])
     args = ap.parse_args()
+    if args.task == "parkour":
+        args.mono = True  # one fused wave-per-env launch per step
 
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     world, rank, local = world_from_env()
@@ -127,13 +186,19 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
-    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     N = args.envs
-    env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
-                          staged=not args.mono, banks=args.banks)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
-    pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]
+    if args.task == "parkour":
+        from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv, action_limits
+        env = ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
+        lim = torch.as_tensor(action_limits(), dtype=torch.float32, device=dev)
+        pool = [((torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * lim).contiguous() for _ in range(16)]
+    else:
+        from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+        env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
+                              staged=not args.mono, banks=args.banks)
+        pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]
     env.reset()
     for k in range(args.warmup):
         env.step(pool[k % len(pool)])
@@ -164,7 +229,28 @@ def main():
     acc, elapsed = reduce_rollout(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
     value = total_steps / elapsed
-    if rank == 0:
+    if rank == 0 and args.task == "parkour":
+        bytes_per_launch = PARKOUR_ALG_BYTES * N
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        out = {
+            "metric": PARKOUR_METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (U(-lim,lim) actions per joint, Philox reset draws)",
+            "config": {"workload": "quadruped_parkour_env, 4096 envs/GPU (BASELINE configs[1])", "envs_per_gpu": N,
+                       "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
+                       "substeps_per_step": 10, "episodes_started": int(acc[1].item()),
+                       "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "mean_reward": round(acc[2].item() / total_steps, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "mgx_parkour_step = k_parkour<float,0>", "alg_bytes_per_step": bytes_per_launch,
+                         "launch_ms": round(launch_ms, 4)},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_parkour(max(1, args.cpu_envs // 4), args.cpu_steps // 4)
+        print(json.dumps(out))
+    elif rank == 0:
         bytes_per_launch = ALG_BYTES_PER_ENV_STEP * N
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None

@@ -48,6 +48,8 @@ typedef struct mgx_model_desc {
   int32_t integrator;  /* 0 Euler, 1 RK4 (mjtIntegrator) */
   int32_t cone;        /* 0 pyramidal, 1 elliptic */
   int32_t iterations;
+  int32_t efc_capacity; /* constraint-row capacity per env (0 = library default 192) */
+  int32_t con_capacity; /* contact capacity per env (0 = library default 64) */
   int32_t pad0;
   double timestep, tolerance, impratio, meaninertia;
   double gravity[3];
@@ -87,6 +89,9 @@ typedef struct mgx_model_info {
   int32_t lds_bytes_per_env; /* dynamic LDS used by the step kernel for one env */
   int32_t lds_bytes_rows;    /* staged soccer step: row-builder LDS per env */
   int32_t lds_bytes_finish;  /* staged soccer step: finisher LDS per env */
+  int32_t scratch_bytes_per_env; /* > 0: the constraint rows live in caller-owned device scratch
+                                    (mgx_state.scratch, [N][scratch_bytes_per_env]) because they
+                                    do not fit the per-env LDS budget (large models, e.g. bipedal) */
 } mgx_model_info;
 
 typedef struct mgx_model mgx_model; /* opaque: device-resident model constants */
@@ -101,6 +106,7 @@ typedef struct mgx_state {
   void *xfrc_applied;   /* [N][nbody][6] */
   void *time;           /* [N] */
   int32_t *warning;     /* [N] count of bad-state auto-resets (mj_checkPos/Vel/Acc) */
+  void *scratch;        /* [N][scratch_bytes_per_env] device bytes; NULL when the model needs none */
 } mgx_state;
 
 /* Per-step outputs of the forward pass that env logic reads (stale "pre-integration"

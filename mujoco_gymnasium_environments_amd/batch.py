@@ -81,9 +81,13 @@ class PhysicsBatch:
         self.ncon = torch.zeros(n_env, dtype=torch.int32, device=self.device)
         self.nefc = torch.zeros(n_env, dtype=torch.int32, device=self.device)
         self.niter = torch.zeros(n_env, dtype=torch.int32, device=self.device)
+        # constraint-row scratch for models whose rows do not fit the per-env LDS budget
+        sb = int(self.native.info.scratch_bytes_per_env)
+        self.scratch = torch.empty(n_env * sb, dtype=torch.uint8, device=self.device) if sb > 0 else None
         self._state = cabi.MgxState(*[t.data_ptr() for t in (self.qpos, self.qvel, self.qacc_warmstart, self.ctrl,
                                                              self.qfrc_applied, self.xfrc_applied, self.time,
-                                                             self.warning)])
+                                                             self.warning)],
+                                    self.scratch.data_ptr() if self.scratch is not None else None)
         self._frames = cabi.MgxFrames(*[t.data_ptr() for t in (self.xpos, self.xquat, self.subtree_com, self.ncon,
                                                               self.nefc, self.niter)])
 

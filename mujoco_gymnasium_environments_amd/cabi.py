@@ -17,7 +17,7 @@ P_F64 = C.POINTER(C.c_double)
 
 # (field, kind) in declaration order of mgx_model_desc
 _INT_SIZES = ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "npair", "nM", "nmaskword",
-              "solver", "integrator", "cone", "iterations", "pad0"]
+              "solver", "integrator", "cone", "iterations", "efc_capacity", "con_capacity", "pad0"]
 _REAL_SCALARS = ["timestep", "tolerance", "impratio", "meaninertia"]
 _ARRAYS = [
     ("body_parentid", "i"), ("body_rootid", "i"), ("body_weldid", "i"), ("body_jntnum", "i"),
@@ -56,13 +56,13 @@ class MgxModelInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "npair", "max_nv", "max_nbody",
                  "max_ncon", "max_nefc", "max_njnt", "precision", "lds_bytes_per_env", "lds_bytes_rows",
-                 "lds_bytes_finish"]]
+                 "lds_bytes_finish", "scratch_bytes_per_env"]]
 
 
 class MgxState(C.Structure):
     _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("qacc_warmstart", C.c_void_p),
                 ("ctrl", C.c_void_p), ("qfrc_applied", C.c_void_p), ("xfrc_applied", C.c_void_p),
-                ("time", C.c_void_p), ("warning", C.c_void_p)]
+                ("time", C.c_void_p), ("warning", C.c_void_p), ("scratch", C.c_void_p)]
 
 
 class MgxFrames(C.Structure):
@@ -122,6 +122,9 @@ class PackedModel:
 
     def __init__(self, model: Model):
         self.model = model
+        # per-env capacities: task modules may set these hints on the model (0 = library default)
+        efc_capacity = int(getattr(model, "efc_capacity", 0))
+        con_capacity = int(getattr(model, "con_capacity", 0))
         self.arrays = {}
         d = MgxModelDesc()
         A = model.arrays
@@ -129,7 +132,8 @@ class PackedModel:
         sizes = dict(nq=model.nq, nv=model.nv, nu=model.nu, nbody=model.nbody, njnt=model.njnt,
                      ngeom=model.ngeom, npair=int(A["pair_geom"].shape[0]), nM=model.nM,
                      nmaskword=nmask, solver=model.solver, integrator=model.integrator,
-                     cone=model.cone, iterations=model.iterations, pad0=0)
+                     cone=model.cone, iterations=model.iterations, efc_capacity=efc_capacity,
+                     con_capacity=con_capacity, pad0=0)
         for k, v in sizes.items():
             setattr(d, k, int(v))
         d.timestep, d.tolerance = model.timestep, model.tolerance

@@ -38,131 +38,6 @@ int host_fail(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace mgx
 
 // ------------------------------------------------------------------------- kernels
-template <typename T>
-__global__ void __launch_bounds__(64) k_step(DevModel<T> m, mgx_state s, mgx_frames fr, int n_env, int nsub,
-                                             const uint8_t* mask) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int env = blockIdx.x;
-  if (env >= n_env) return;
-  if (mask && !mask[env]) return;
-  Env<T> e;
-  env_bind(m, e, smem);
-  T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
-  T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
-  load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  int warn = 0;
-  for (int k = 0; k < nsub; k++) warn += mj_step_env(m, e);
-  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  int l = lane_id();
-  if (l == 0 && s.warning) s.warning[env] += warn;
-  if (fr.xpos) for (int k = l; k < 3 * m.nbody; k += 64) ((T*)fr.xpos)[(size_t)env * 3 * m.nbody + k] = e.xpos[k];
-  if (fr.xquat) for (int k = l; k < 4 * m.nbody; k += 64) ((T*)fr.xquat)[(size_t)env * 4 * m.nbody + k] = e.xquat[k];
-  if (fr.subtree_com)
-    for (int k = l; k < 3 * m.nbody; k += 64) ((T*)fr.subtree_com)[(size_t)env * 3 * m.nbody + k] = e.subtree_com[k];
-  if (l == 0) {
-    if (fr.ncon) fr.ncon[env] = e.ncon;
-    if (fr.nefc) fr.nefc[env] = e.nefc;
-    if (fr.niter) fr.niter[env] = e.niter;
-  }
-}
-
-template <typename T>
-__global__ void k_reset(DevModel<T> m, mgx_state s, int n_env, const uint8_t* mask) {
-  int env = blockIdx.x;
-  if (env >= n_env || (mask && !mask[env])) return;
-  int l = threadIdx.x;
-  for (int k = l; k < m.nq; k += 64) ((T*)s.qpos)[(size_t)env * m.nq + k] = m.qpos0[k];
-  for (int k = l; k < m.nv; k += 64) {
-    ((T*)s.qvel)[(size_t)env * m.nv + k] = 0;
-    ((T*)s.qacc_warmstart)[(size_t)env * m.nv + k] = 0;
-    ((T*)s.qfrc_applied)[(size_t)env * m.nv + k] = 0;
-  }
-  for (int k = l; k < m.nu; k += 64) ((T*)s.ctrl)[(size_t)env * m.nu + k] = 0;
-  for (int k = l; k < 6 * m.nbody; k += 64) ((T*)s.xfrc_applied)[(size_t)env * 6 * m.nbody + k] = 0;
-  if (l == 0) ((T*)s.time)[env] = 0;
-}
-
-// Debug dump of one forward pass (stage outputs), offsets from mgx_debug_layout.
-struct DbgOff {
-  int xpos, xquat, xipos, subtree_com, cinert, cdof, qM, qLD, geom_xpos, geom_xmat, ncon, con_dist, con_pos,
-      con_frame, con_geom, nefc, efc_type, efc_id, efc_pos, efc_margin, efc_R, efc_aref, Bmat, cvel, cdof_dot,
-      qfrc_smooth, qacc_smooth, efc_force, qacc, qfrc_constraint, niter, total;
-};
-
-static DbgOff dbg_offsets(int nb, int nv, int nM, int ng, int C, int E) {
-  DbgOff o;
-  int p = 0;
-  auto take = [&](int n) { int r = p; p += n; return r; };
-  o.xpos = take(3 * nb); o.xquat = take(4 * nb); o.xipos = take(3 * nb); o.subtree_com = take(3 * nb);
-  o.cinert = take(10 * nb); o.cdof = take(6 * nv); o.qM = take(nM); o.qLD = take(nM);
-  o.geom_xpos = take(3 * ng); o.geom_xmat = take(9 * ng); o.ncon = take(1); o.con_dist = take(C);
-  o.con_pos = take(3 * C); o.con_frame = take(9 * C); o.con_geom = take(2 * C); o.nefc = take(1);
-  o.efc_type = take(E); o.efc_id = take(E); o.efc_pos = take(E); o.efc_margin = take(E); o.efc_R = take(E);
-  o.efc_aref = take(E); o.Bmat = take(E * nv); o.cvel = take(6 * nb); o.cdof_dot = take(6 * nv);
-  o.qfrc_smooth = take(nv); o.qacc_smooth = take(nv); o.efc_force = take(E); o.qacc = take(nv);
-  o.qfrc_constraint = take(nv); o.niter = take(1); o.total = p;
-  return o;
-}
-
-template <typename T>
-__global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s, int n_env, T* dbg, DbgOff o) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int env = blockIdx.x;
-  if (env >= n_env) return;
-  Env<T> e;
-  env_bind(m, e, smem);
-  load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied,
-             (T*)s.xfrc_applied, (T*)s.time, env);
-  T* D = dbg + (size_t)env * o.total;
-  int l = lane_id();
-  kinematics(m, e);
-  com_crb(m, e);
-  for (int k = l; k < m.nM; k += 64) D[o.qM + k] = e.qLD[k];
-  wsync();
-  e.diaginv = factor_ld(m, e, e.qLD);
-  for (int k = l; k < m.nM; k += 64) D[o.qLD + k] = e.qLD[k];
-  velocity(m, e);
-  e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
-  collision(m, e);
-  wsync();
-  for (int k = l; k < 3 * m.nbody; k += 64) D[o.xipos + k] = e.xipos[k];
-  for (int k = l; k < 10 * m.nbody; k += 64) D[o.cinert + k] = e.cinert[k];
-  for (int k = l; k < 6 * m.nv; k += 64) D[o.cdof_dot + k] = e.cdof_dot[k];
-  for (int k = l; k < 6 * m.nbody; k += 64) D[o.cvel + k] = e.cvel[k];
-  for (int k = l; k < 3 * m.ngeom; k += 64) D[o.geom_xpos + k] = e.geom_xpos[k];
-  for (int k = l; k < 9 * m.ngeom; k += 64) D[o.geom_xmat + k] = e.geom_xmat[k];
-  wsync();
-  make_constraint(m, e);
-  if (l < m.nv) e.vec0[l] = sqrt(e.diaginv);
-  wsync();
-  transform_rows(m, e);
-  wsync();
-  for (int r = l; r < e.nefc; r += 64)
-    for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];
-  pgs(m, e);
-  wsync();
-  for (int k = l; k < 3 * m.nbody; k += 64) { D[o.xpos + k] = e.xpos[k]; D[o.subtree_com + k] = e.subtree_com[k]; }
-  for (int k = l; k < 4 * m.nbody; k += 64) D[o.xquat + k] = e.xquat[k];
-  for (int k = l; k < 6 * m.nv; k += 64) D[o.cdof + k] = e.cdof[k];
-  if (l == 0) { D[o.ncon] = (T)e.ncon; D[o.nefc] = (T)e.nefc; D[o.niter] = (T)e.niter; }
-  for (int c = l; c < e.ncon; c += 64) {
-    D[o.con_dist + c] = e.con_dist[c];
-    for (int k = 0; k < 3; k++) D[o.con_pos + 3 * c + k] = e.con_pos[3 * c + k];
-    for (int k = 0; k < 9; k++) D[o.con_frame + 9 * c + k] = e.con_frame[9 * c + k];
-    D[o.con_geom + 2 * c] = (T)e.con_geom[2 * c];
-    D[o.con_geom + 2 * c + 1] = (T)e.con_geom[2 * c + 1];
-  }
-  for (int r = l; r < e.nefc; r += 64) {
-    D[o.efc_type + r] = (T)e.efc_type[r]; D[o.efc_id + r] = (T)e.efc_id[r]; D[o.efc_pos + r] = e.efc[8 * r + 7];
-    D[o.efc_margin + r] = e.efc_margin[r]; D[o.efc_R + r] = e.efc[8 * r + 2]; D[o.efc_aref + r] = e.efc[8 * r + 5];
-    D[o.efc_force + r] = e.efc[8 * r + 1];
-  }
-  if (l < m.nv) {
-    D[o.qfrc_smooth + l] = e.qfrc_smooth; D[o.qacc_smooth + l] = e.qacc_smooth; D[o.qacc + l] = e.qacc;
-    D[o.qfrc_constraint + l] = e.qfrc_constraint;
-  }
-}
-
 // soccer reset body shared by the explicit-reset and autoreset paths: draws (36 values in
 // reference order, from the host or from Philox) -> randomised qpos, 10 settle mj_steps, obs.
 template <typename T>
@@ -480,7 +355,8 @@ namespace {
 
 int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
-Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active, bool staged) {
+Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active, bool staged,
+                   bool gB = false) {
   Layout L{};
   int p = 0;
   int al = 16 / real_bytes;  // 16-byte alignment in elements
@@ -495,6 +371,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.carry_reals = p;
   L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64); L.vec3 = take(64);
   int vec_end = p;
+  L.rk = (!staged && d->integrator == 1) ? take(((d->nq + 3) & ~3) + 64) : 0;
   // persistent for the rest of the forward pass
   L.cdof = take(6 * nv); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
   L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged ? 1 : max_nefc);
@@ -517,6 +394,11 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
   L.Bmat = u0;
   L.chunk_rows = staged ? 0 : max_nefc;  // the staged row builder keeps rows in registers
+  if (gB && !staged) {  // rows in per-env global scratch
+    L.gB = 1;
+    L.gB_stride = align_up(max_nefc * L.Bstride, al);
+    L.chunk_rows = 0;
+  }
   int endB = align_up(u0 + L.chunk_rows * L.Bstride, al);
   L.reals = endA > endB ? endA : endB;
   int q = 0;
@@ -759,8 +641,8 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   if (!d || !out) return fail(MGX_E_ARG, "null argument");
   if (precision != MGX_F32 && precision != MGX_F64) return fail(MGX_E_ARG, "precision must be MGX_F32 or MGX_F64");
   if (d->nv > MGX_MAX_NV) return fail(MGX_E_CAPACITY, "nv > 64 not supported by the wave-per-env kernel");
-  if (d->nbody > 4096 || d->solver != 0 || d->integrator != 0)
-    return fail(MGX_E_UNSUPPORTED, "this build implements PGS + Euler (solver=PGS, integrator=Euler)");
+  if (d->nbody > 4096 || d->solver != 0 || (d->integrator != 0 && d->integrator != 1))
+    return fail(MGX_E_UNSUPPORTED, "this build implements PGS with Euler or RK4 (solver=PGS)");
   for (int p = 0; p < d->npair; p++)
     if (d->pair_condim[p] != 1 && d->pair_condim[p] != 3) return fail(MGX_E_UNSUPPORTED, "condim must be 1 or 3");
   mgx_model* m = new mgx_model();
@@ -769,14 +651,23 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   m->npair = d->npair;
   const char* env_nefc = getenv("MGX_MAX_NEFC");
   const char* env_ncon = getenv("MGX_MAX_NCON");
-  int max_nefc = env_nefc ? atoi(env_nefc) : 192;
-  int max_ncon = env_ncon ? atoi(env_ncon) : 64;
-  if (max_nefc > 64 * MGX_EFC_SLOTS) max_nefc = 64 * MGX_EFC_SLOTS;
+  // capacities: the model's request (efc_capacity / con_capacity), else 192 rows / 64 contacts
+  int max_nefc = env_nefc ? atoi(env_nefc) : (d->efc_capacity > 0 ? d->efc_capacity : 192);
+  int max_ncon = env_ncon ? atoi(env_ncon) : (d->con_capacity > 0 ? d->con_capacity : 64);
+  if (max_nefc > 1024) max_nefc = 1024;
+  if (max_ncon > 512) max_ncon = 512;
   max_nefc = (max_nefc + 3) & ~3;  // the staged solver sweeps rows in blocks of 4
   if (max_nefc < 4 || max_ncon < 1) { delete m; return fail(MGX_E_ARG, "MGX_MAX_NEFC / MGX_MAX_NCON too small"); }
   int rb = precision == MGX_F32 ? 4 : 8;
-  m->L = make_layout(d, rb, max_ncon, max_nefc, 128, false);
-  m->Ls = make_layout(d, rb, max_ncon, max_nefc, 128, true);
+  // broadphase survivor list: 128 for the small candidate sets (soccer 251, parkour 48 pairs),
+  // up to 768 for large ones (bipedal 3185 pairs)
+  int max_active = d->npair <= 256 ? 128 : (d->npair < 768 ? d->npair : 768);
+  m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false);
+  // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
+  if (m->L.bytes > 160 * 1024) m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false, true);
+  // the staged soccer pipeline (register-ring solver) handles Euler models up to 192 rows
+  m->staged_ok = d->integrator == 0 && max_nefc <= 64 * MGX_EFC_SLOTS;
+  m->Ls = make_layout(d, rb, max_ncon, m->staged_ok ? max_nefc : 4, 128, true);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;
   if (precision == MGX_F32) {
@@ -788,17 +679,17 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   }
   if (rc != MGX_OK) { delete m; return rc; }
   if (m->L.bytes > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "per-env LDS exceeds 160 KiB"); }
-  int r2 = precision == MGX_F32
-               ? (set_lds(k_step<float>, m->L.bytes) | set_lds(k_debug_forward<float>, m->L.bytes) |
-                  set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes) |
+  int r2 = step_kernels_configure(m);
+  if (r2 != MGX_OK) { delete m; return r2; }
+  r2 = precision == MGX_F32
+               ? (set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes) |
                   set_lds(k_soccer_logic<float>, m->L.bytes) | set_lds(k_soccer_fixup<float>, m->L.bytes) | set_lds(k_soccer_template<float>, m->L.bytes) |
                   set_lds(k_soccer_rows<float>, m->Ls.bytes) | set_lds(k_soccer_finish<float>, m->Lf.bytes))
-               : (set_lds(k_step<double>, m->L.bytes) | set_lds(k_debug_forward<double>, m->L.bytes) |
-                  set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes) |
+               : (set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes) |
                   set_lds(k_soccer_logic<double>, m->L.bytes) | set_lds(k_soccer_fixup<double>, m->L.bytes) | set_lds(k_soccer_template<double>, m->L.bytes) |
                   set_lds(k_soccer_rows<double>, m->Ls.bytes) | set_lds(k_soccer_finish<double>, m->Lf.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
-  {
+  if (m->staged_ok) {
     int pl = pgs_lds_bytes(m);
     if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
     int r3 = precision == MGX_F32
@@ -832,70 +723,14 @@ int mgx_model_get_info(const mgx_model* m, mgx_model_info* o) {
   o->max_nv = MGX_MAX_NV; o->max_nbody = 4096; o->max_ncon = m->L.max_ncon; o->max_nefc = m->L.max_nefc;
   o->max_njnt = 1 << 20; o->precision = m->precision; o->lds_bytes_per_env = m->L.bytes;
   o->lds_bytes_rows = m->Ls.bytes; o->lds_bytes_finish = m->Lf.bytes;
-  return MGX_OK;
-}
-
-int mgx_step(const mgx_model* m, const mgx_state* s, mgx_frames* frames, int n_env, int nsub, const uint8_t* mask,
-             void* stream) {
-  if (!m || n_env < 0 || nsub < 0) return fail(MGX_E_ARG, "bad argument");
-  int rc = check_state(s);
-  if (rc) return rc;
-  if (n_env == 0 || nsub == 0) return MGX_OK;
-  mgx_frames fr{};
-  if (frames) fr = *frames;
-  hipStream_t st = (hipStream_t)stream;
-  if (m->precision == MGX_F32)
-    hipLaunchKernelGGL(k_step<float>, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, fr, n_env, nsub, mask);
-  else
-    hipLaunchKernelGGL(k_step<double>, dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, fr, n_env, nsub, mask);
-  HIPCHK(hipGetLastError());
-  return MGX_OK;
-}
-
-int mgx_reset_data(const mgx_model* m, const mgx_state* s, int n_env, const uint8_t* mask, void* stream) {
-  if (!m || n_env < 0) return fail(MGX_E_ARG, "bad argument");
-  int rc = check_state(s);
-  if (rc) return rc;
-  if (n_env == 0) return MGX_OK;
-  hipStream_t st = (hipStream_t)stream;
-  if (m->precision == MGX_F32) hipLaunchKernelGGL(k_reset<float>, dim3(n_env), dim3(64), 0, st, m->mf, *s, n_env, mask);
-  else hipLaunchKernelGGL(k_reset<double>, dim3(n_env), dim3(64), 0, st, m->md, *s, n_env, mask);
-  HIPCHK(hipGetLastError());
-  return MGX_OK;
-}
-
-int mgx_debug_layout(const mgx_model* m, int32_t* offsets, int32_t n) {
-  if (!m || !offsets) return fail(MGX_E_ARG, "null argument");
-  int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
-  int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
-  int nM = m->precision == MGX_F32 ? m->mf.nM : m->md.nM;
-  int ng = m->precision == MGX_F32 ? m->mf.ngeom : m->md.ngeom;
-  DbgOff o = dbg_offsets(nb, nv, nM, ng, m->L.max_ncon, m->L.max_nefc);
-  const int* src = (const int*)&o;
-  int cnt = (int)(sizeof(DbgOff) / sizeof(int));
-  for (int i = 0; i < n && i < cnt; i++) offsets[i] = src[i];
-  return cnt;
-}
-
-int mgx_debug_forward(const mgx_model* m, const mgx_state* s, int n_env, void* dbg, void* stream) {
-  if (!m || !dbg) return fail(MGX_E_ARG, "null argument");
-  int rc = check_state(s);
-  if (rc) return rc;
-  if (n_env <= 0) return MGX_OK;
-  hipStream_t st = (hipStream_t)stream;
-  if (m->precision == MGX_F32) {
-    DbgOff o = dbg_offsets(m->mf.nbody, m->mf.nv, m->mf.nM, m->mf.ngeom, m->L.max_ncon, m->L.max_nefc);
-    hipLaunchKernelGGL(k_debug_forward<float>, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, n_env, (float*)dbg, o);
-  } else {
-    DbgOff o = dbg_offsets(m->md.nbody, m->md.nv, m->md.nM, m->md.ngeom, m->L.max_ncon, m->L.max_nefc);
-    hipLaunchKernelGGL(k_debug_forward<double>, dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, n_env, (double*)dbg, o);
-  }
-  HIPCHK(hipGetLastError());
+  o->scratch_bytes_per_env = m->L.gB ? m->L.gB_stride * (m->precision == MGX_F32 ? 4 : 8) : 0;
   return MGX_OK;
 }
 
 int mgx_soccer_configure(mgx_model* m, const mgx_soccer_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");
+  if (m->L.gB || (m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the soccer kernels need an Euler model whose rows fit LDS");
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
   if (m->precision == MGX_F32) fill_ids(m->sf, ids, m->mf, nullptr);
   else fill_ids(m->sd, ids, m->md, nullptr);
@@ -932,6 +767,7 @@ int mgx_soccer_step(const mgx_model* m, const mgx_state* s, const mgx_soccer_env
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
   if (e->workspace) {
+    if (!m->staged_ok) return fail(MGX_E_UNSUPPORTED, "staged step: model exceeds the staged solver's capacity");
     if (e->banks < 0 || e->banks > 16) return fail(MGX_E_ARG, "banks must be in [0, 16]");
     if (m->precision == MGX_F32)
       return soccer_step_staged<float>(m, m->mf, m->mfs, m->mff, m->sf, s, e, action, obs, reward, terminated,
@@ -983,6 +819,7 @@ int mgx_soccer_reset(const mgx_model* m, const mgx_state* s, const mgx_soccer_en
 
 int64_t mgx_soccer_workspace_bytes(const mgx_model* m, int n_env, int banks) {
   if (!m || n_env <= 0 || banks < 0 || banks > 16) return fail(MGX_E_ARG, "bad argument");
+  if (!m->staged_ok) return fail(MGX_E_UNSUPPORTED, "staged step: model exceeds the staged solver's capacity");
   return (int64_t)make_pipe(m, nullptr, n_env, banks, nullptr);
 }
 

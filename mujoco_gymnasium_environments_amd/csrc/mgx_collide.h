@@ -129,6 +129,121 @@ __device__ __forceinline__ int capsule_box(const T* cp, const T* cm, const T* cs
   return n;
 }
 
+// ---- cylinders (bipedal_rescue: sphere / capsule / box vs static cylinders) [ext]. MuJoCo
+// sends these pairs through its general convex collider (one contact per pair); these are
+// the oracle's closed forms on the exact (convex) cylinder signed distance (oracle/mjref.c).
+template <typename T>
+__device__ __forceinline__ T cyl_sd(const T* p, T r, T hh, T* e) {
+  T rho = sqrt(p[0] * p[0] + p[1] * p[1]);
+  T dr = rho - r, dz = fabs(p[2]) - hh;
+  T ux = 1, uy = 0, sz = p[2] >= 0 ? (T)1 : (T)-1;
+  if (rho > minval<T>()) { ux = p[0] / rho; uy = p[1] / rho; }
+  if (dr > 0 && dz > 0) {
+    T L = sqrt(dr * dr + dz * dz);
+    e[0] = ux * dr / L; e[1] = uy * dr / L; e[2] = sz * dz / L;
+    return L;
+  }
+  if (dr >= dz) { e[0] = ux; e[1] = uy; e[2] = 0; return dr; }
+  e[0] = 0; e[1] = 0; e[2] = sz;
+  return dz;
+}
+
+template <typename T>
+__device__ __forceinline__ int sphere_cyl_core(const T* c, T R, const T* yp, const T* ym, const T* ys, T margin, Con<T>* out) {
+  T tmp[3] = {c[0] - yp[0], c[1] - yp[1], c[2] - yp[2]}, pl[3], e[3], ew[3];
+  mulmatTvec3(pl, ym, tmp);
+  T dist = cyl_sd(pl, ys[0], ys[1], e) - R;
+  if (dist > margin) return 0;
+  mulmatvec3(ew, ym, e);
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = -ew[k]; out->pos[k] = c[k] - ew[k] * (R + (T)0.5 * dist); }
+  return 1;
+}
+
+template <typename T>
+__device__ __forceinline__ int capsule_cyl(const T* cp, const T* cm, const T* cs, const T* yp, const T* ym, const T* ys, T margin,
+                                           Con<T>* out) {
+  T a[3], b[3], al[3], bl[3], tmp[3], e[3], p[3];
+  seg_ends(cp, cm, cs[1], a, b);
+  for (int k = 0; k < 3; k++) tmp[k] = a[k] - yp[k];
+  mulmatTvec3(al, ym, tmp);
+  for (int k = 0; k < 3; k++) tmp[k] = b[k] - yp[k];
+  mulmatTvec3(bl, ym, tmp);
+  T lo = 0, hi = 1;
+  const T gr = (T)0.6180339887498949;
+  T x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), f1, f2;
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+  f1 = cyl_sd(p, ys[0], ys[1], e);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+  f2 = cyl_sd(p, ys[0], ys[1], e);
+  for (int it = 0; it < 40; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+      f1 = cyl_sd(p, ys[0], ys[1], e);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+      f2 = cyl_sd(p, ys[0], ys[1], e);
+    }
+  }
+  T ts = (T)0.5 * (lo + hi);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + ts * (bl[k] - al[k]);
+  T fs = cyl_sd(p, ys[0], ys[1], e), f0 = cyl_sd(al, ys[0], ys[1], e), fb = cyl_sd(bl, ys[0], ys[1], e);
+  T t = ts;
+  if (f0 <= fs && f0 <= fb) t = 0;
+  else if (fb < fs) t = 1;
+  T cw[3];
+  for (int k = 0; k < 3; k++) cw[k] = a[k] + t * (b[k] - a[k]);
+  return sphere_cyl_core(cw, cs[0], yp, ym, ys, margin, out);
+}
+
+template <typename T>
+__device__ __forceinline__ int cyl_box(const T* yp, const T* ym, const T* ys, const T* bp, const T* bm, const T* h, T margin,
+                                       Con<T>* out) {
+  T best = (T)1e30, bn[3] = {0, 0, 1}, bpos[3] = {0, 0, 0};
+  T v[3], w[3], tmp[3], pl[3], e[3], ew[3];
+  for (int i = 0; i < 8; i++) {
+    v[0] = (i & 1) ? h[0] : -h[0]; v[1] = (i & 2) ? h[1] : -h[1]; v[2] = (i & 4) ? h[2] : -h[2];
+    mulmatvec3(w, bm, v);
+    for (int k = 0; k < 3; k++) { w[k] += bp[k]; tmp[k] = w[k] - yp[k]; }
+    mulmatTvec3(pl, ym, tmp);
+    T sd = cyl_sd(pl, ys[0], ys[1], e);
+    if (sd < best) {
+      best = sd;
+      mulmatvec3(ew, ym, e);
+      for (int k = 0; k < 3; k++) { bn[k] = ew[k]; bpos[k] = w[k] - (T)0.5 * sd * ew[k]; }
+    }
+  }
+  T q[3] = {yp[0], yp[1], yp[2]};
+  for (int it = 0; it < 3; it++) {
+    for (int k = 0; k < 3; k++) tmp[k] = q[k] - bp[k];
+    mulmatTvec3(pl, bm, tmp);
+    box_sd(pl, h, e);
+    T d[3], dl[3];
+    mulmatvec3(ew, bm, e);
+    for (int k = 0; k < 3; k++) d[k] = -ew[k];
+    mulmatTvec3(dl, ym, d);
+    T rxy = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+    T sl[3] = {0, 0, dl[2] >= 0 ? ys[1] : -ys[1]};
+    if (rxy > minval<T>()) { sl[0] = ys[0] * dl[0] / rxy; sl[1] = ys[0] * dl[1] / rxy; }
+    mulmatvec3(q, ym, sl);
+    for (int k = 0; k < 3; k++) q[k] += yp[k];
+    for (int k = 0; k < 3; k++) tmp[k] = q[k] - bp[k];
+    mulmatTvec3(pl, bm, tmp);
+    T sd = box_sd(pl, h, e);
+    if (sd < best) {
+      best = sd;
+      mulmatvec3(ew, bm, e);
+      for (int k = 0; k < 3; k++) { bn[k] = -ew[k]; bpos[k] = q[k] - (T)0.5 * sd * ew[k]; }
+    }
+  }
+  if (best > margin) return 0;
+  out->dist = best;
+  for (int k = 0; k < 3; k++) { out->n[k] = bn[k]; out->pos[k] = bpos[k]; }
+  return 1;
+}
+
 template <typename T>
 __device__ __forceinline__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T (*out)[2]) {
   int m = 0;
@@ -315,6 +430,9 @@ __device__ __forceinline__ int collide_pair(int t1, int t2, const T* p1, const T
     return n;
   }
   if (t1 == GPLANE && t2 == GBOX) return plane_box(p1, m1, p2, m2, s2, margin, out);
+  if (t1 == GSPHERE && t2 == GCYLINDER) return sphere_cyl_core(p1, s1[0], p2, m2, s2, margin, out);
+  if (t1 == GCAPSULE && t2 == GCYLINDER) return capsule_cyl(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GCYLINDER && t2 == GBOX) return cyl_box(p1, m1, s1, p2, m2, s2, margin, out);
   return 0;
 }
 

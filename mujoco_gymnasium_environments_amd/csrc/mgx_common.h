@@ -38,6 +38,11 @@ struct Layout {
   // staged pipeline: reals [0, carry_reals) and ints [0, carry_ints) are handed from the row
   // builder to the finisher through HBM; B rows are built chunk_rows at a time
   int staged, carry_reals, carry_ints, chunk_rows;
+  // RK4 stage storage (X[0] positions, dX velocities; integrator == RK4 only)
+  int rk;
+  // 1: the monolithic kernel keeps B rows in per-env global scratch (gB_stride reals per env)
+  // instead of LDS, for models whose rows do not fit the LDS budget
+  int gB, gB_stride;
 };
 
 // Device-resident model: pointers into one device allocation.

@@ -24,12 +24,15 @@ struct mgx_model {
   mgx::ParkourIds<float> pkf;
   mgx::ParkourIds<double> pkd;
   int npair;
+  bool staged_ok = false;  // the staged soccer pipeline supports this model's capacities
 };
 
 namespace mgx {
 // records the message returned by mgx_last_error() and returns `code`
 int host_fail(int code, const std::string& msg);
 int host_check_state(const mgx_state* s);
+// dynamic-LDS attributes of the generic step kernels (mgx_step.hip)
+int step_kernels_configure(const mgx_model* m);
 }  // namespace mgx
 
 #define MGX_HIPCHK(x)                                                                                   \

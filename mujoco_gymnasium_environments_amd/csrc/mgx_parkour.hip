@@ -138,6 +138,8 @@ int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
   int nu = m->precision == MGX_F32 ? m->mf.nu : m->md.nu;
   int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
+  if (m->L.gB || (m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the parkour kernels need an Euler model whose rows fit LDS");
   if (ids->n_leg != 16 || nu < 16 || nq < 7) return fail(MGX_E_ARG, "parkour needs 16 leg actuators and a free root");
   if (ids->torso < 0 || ids->torso >= nb) return fail(MGX_E_ARG, "torso body id out of range");
   for (int i = 0; i < 4; i++)

@@ -27,6 +27,7 @@ struct Env {
   T *efc, *efc_margin, *efc_blk;
   T *Bm;
   int Bs;
+  T *rk;  // RK4: X[0] positions [nq] then the dX velocity vector [nv]
   int *con_geom, *con_pair, *act_list, *efc_type, *efc_id, *con_efcadr;
   int ncon, nefc, niter, overflow;
   // dof-lane registers
@@ -35,8 +36,9 @@ struct Env {
   uint64_t ancmask;
 };
 
-template <typename T>
-__device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem) {
+// GB: B rows in global scratch (gB = this env's slice) instead of LDS (Layout.gB)
+template <typename T, bool GB = false>
+__device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem, T* gB = nullptr) {
   T* R = reinterpret_cast<T*>(smem);
   const Layout& L = m.L;
   e.qpos = R + L.qpos; e.qvel = R + L.qvel; e.ctrl = R + L.ctrl; e.xfrc = R + L.xfrc;
@@ -47,7 +49,10 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.vec0 = R + L.vec0; e.vec1 = R + L.vec1; e.vec2 = R + L.vec2; e.vec3 = R + L.vec3; e.geom_xpos = R + L.geom_xpos;
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.cacc = R + L.cacc; e.rowc = R + L.rowc; e.con_dist = R + L.con_dist;
   e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
-  e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bm = R + L.Bmat; e.Bs = L.Bstride;
+  e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bs = L.Bstride;
+  if constexpr (GB) e.Bm = gB;
+  else e.Bm = R + L.Bmat;
+  e.rk = R + L.rk;
   int* I = reinterpret_cast<int*>(R + L.reals);
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
   e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id; e.con_efcadr = I + L.con_efcadr;
@@ -897,6 +902,76 @@ __device__ __forceinline__ void quat_integrate(T* q, const T* w, T h) {
   mulquat(q, q, qr);
 }
 
+// mj_integratePos [ext]: qpos <- qpos '+' h vel (free: position + quaternion, ball: quaternion)
+template <typename T>
+__device__ __forceinline__ void integrate_pos(const DevModel<T>& m, T* qpos, const T* vel, T h) {
+  int l = lane_id();
+  for (int j = l; j < m.njnt; j += 64) {
+    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j], t = m.jnt_type[j];
+    if (t == JFREE) {
+      for (int k = 0; k < 3; k++) qpos[a + k] += h * vel[da + k];
+      quat_integrate(qpos + a + 3, vel + da + 3, h);
+    } else if (t == JBALL) {
+      quat_integrate(qpos + a, vel + da, h);
+    } else {
+      qpos[a] += h * vel[da];
+    }
+  }
+  wsync();
+}
+
+template <typename T>
+__device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e);
+
+// mj_RungeKutta(m, d, 4) [ext], after forward() at X[0] (oracle/mjref.c rk4): stage i runs the
+// forward pass at X[i] = X[0] '+' h sum_j A_ij X'[j]; the final mj_advance uses
+// dX = sum_j B_j X'[j]. Velocities and accelerations stay in dof-lane registers; X[0]
+// positions and the dX velocity vector (integratePos input) sit in the rk LDS region. The
+// frames left in LDS are those of the last stage, as MuJoCo leaves them in mjData.
+template <typename T>
+__device__ __forceinline__ void rk4(const DevModel<T>& m, Env<T>& e) {
+  const T A[9] = {(T)0.5, 0, 0, 0, (T)0.5, 0, 0, 0, (T)1};
+  const T B[4] = {(T)(1.0 / 6.0), (T)(1.0 / 3.0), (T)(1.0 / 3.0), (T)(1.0 / 6.0)};
+  const int l = lane_id(), nq = m.nq;
+  const bool dl = l < m.nv;
+  T* q0 = e.rk;
+  T* dxv = e.rk + ((nq + 3) & ~3);
+  const T h = m.timestep, t0 = e.time;
+  for (int k = l; k < nq; k += 64) q0[k] = e.qpos[k];
+  T v[4], f[4];
+  v[0] = dl ? e.qvel[l] : (T)0;
+  f[0] = dl ? e.qacc : (T)0;
+  for (int i = 1; i < 4; i++) {
+    T C = 0, dv = 0, da = 0;
+    for (int j = 0; j < i; j++) {
+      T a = A[(i - 1) * 3 + j];
+      C += a;
+      dv += a * v[j];
+      da += a * f[j];
+    }
+    wsync();
+    if (dl) dxv[l] = dv;
+    for (int k = l; k < nq; k += 64) e.qpos[k] = q0[k];
+    wsync();
+    integrate_pos(m, e.qpos, dxv, h);
+    v[i] = v[0] + h * da;
+    if (dl) e.qvel[l] = v[i];
+    e.time = t0 + C * h;
+    wsync();
+    forward(m, e);
+    f[i] = dl ? e.qacc : (T)0;
+  }
+  T dv = 0, da = 0;
+  for (int j = 0; j < 4; j++) { dv += B[j] * v[j]; da += B[j] * f[j]; }
+  e.qacc_ws = e.qacc;  // mj_advance saves the last evaluation's qacc for the warmstart
+  wsync();
+  for (int k = l; k < nq; k += 64) e.qpos[k] = q0[k];
+  if (dl) { dxv[l] = dv; e.qvel[l] = v[0] + h * da; }
+  wsync();
+  integrate_pos(m, e.qpos, dxv, h);
+  e.time = t0 + h;
+}
+
 template <typename T>
 __device__ __forceinline__ void euler(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
@@ -910,20 +985,8 @@ __device__ __forceinline__ void euler(const DevModel<T>& m, Env<T>& e) {
   }
   if (l < m.nv) e.qvel[l] += m.timestep * qa;
   wsync();
-  for (int j = l; j < m.njnt; j += 64) {
-    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j], t = m.jnt_type[j];
-    T h = m.timestep;
-    if (t == JFREE) {
-      for (int k = 0; k < 3; k++) e.qpos[a + k] += h * e.qvel[da + k];
-      quat_integrate(e.qpos + a + 3, e.qvel + da + 3, h);
-    } else if (t == JBALL) {
-      quat_integrate(e.qpos + a, e.qvel + da, h);
-    } else {
-      e.qpos[a] += h * e.qvel[da];
-    }
-  }
+  integrate_pos(m, e.qpos, e.qvel, m.timestep);
   e.time += m.timestep;
-  wsync();
 }
 
 // ---------------------------------------------------------------- forward + step
@@ -963,8 +1026,9 @@ __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
 #endif
 }
 
-// returns the number of bad-state resets performed (0..3)
-template <typename T>
+// returns the number of bad-state resets performed (0..3). RK: the model's integrator is RK4
+// (a compile-time choice so Euler kernels do not carry the RK4 stages).
+template <typename T, bool RK = false>
 __device__ __forceinline__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
   int warn = 0;
   if (any_bad(e.qpos, m.nq)) { reset_env(m, e); warn++; }
@@ -974,6 +1038,10 @@ __device__ __forceinline__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
     reset_env(m, e);
     warn++;
     forward(m, e);
+  }
+  if constexpr (RK) {
+    rk4(m, e);
+    return warn;
   }
   e.qacc_ws = e.qacc;
   MGX_STAMP_DECL

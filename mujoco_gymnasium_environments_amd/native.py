@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = ["mgx_api.hip", "mgx_parkour.hip"]
+SOURCES = ["mgx_api.hip", "mgx_step.hip", "mgx_parkour.hip"]
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
            "mgx_internal.h"]
 

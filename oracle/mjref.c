@@ -589,6 +589,128 @@ static int capsule_box(const double *cp, const double *cm, const double *cs, con
   return n;
 }
 
+/* ---- cylinders (bipedal_rescue: sphere/capsule/box vs static cylinders) [ext]
+ * MuJoCo routes these pairs through its general convex collider (one contact per pair);
+ * this restatement keeps the one-contact semantics with closed forms on the exact
+ * cylinder signed distance, which is convex, so 1-D searches along segments are exact. */
+
+/* signed distance of a cylinder-local point (radius r, half-height hh, axis z);
+ * e = outward unit normal of the closest surface feature (cylinder frame) */
+static double cyl_sd(const double *p, double r, double hh, double *e) {
+  double rho = sqrt(p[0] * p[0] + p[1] * p[1]);
+  double dr = rho - r, dz = fabs(p[2]) - hh;
+  double ux = 1, uy = 0, sz = p[2] >= 0 ? 1 : -1;
+  if (rho > MINVAL) { ux = p[0] / rho; uy = p[1] / rho; }
+  if (dr > 0 && dz > 0) { /* rim region */
+    double L = sqrt(dr * dr + dz * dz);
+    e[0] = ux * dr / L; e[1] = uy * dr / L; e[2] = sz * dz / L;
+    return L;
+  }
+  if (dr >= dz) { e[0] = ux; e[1] = uy; e[2] = 0; return dr; }
+  e[0] = 0; e[1] = 0; e[2] = sz;
+  return dz;
+}
+
+/* sphere (center c world, radius R) vs cylinder geom; normal from sphere to cylinder */
+static int sphere_cyl_core(const double *c, double R, const double *yp, const double *ym, const double *ys,
+                           double margin, rcon *out) {
+  double tmp[3] = {c[0] - yp[0], c[1] - yp[1], c[2] - yp[2]}, pl[3], e[3], ew[3];
+  mulmatTvec3(pl, ym, tmp);
+  double dist = cyl_sd(pl, ys[0], ys[1], e) - R;
+  if (dist > margin) return 0;
+  mulmatvec3(ew, ym, e);
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = -ew[k]; out->pos[k] = c[k] - ew[k] * (R + 0.5 * dist); }
+  return 1;
+}
+
+/* capsule (geom1) vs cylinder (geom2): the deepest point of the capsule segment (golden
+ * section over the convex profile, or an endpoint) as a sphere-cylinder contact */
+static int capsule_cyl(const double *cp, const double *cm, const double *cs, const double *yp, const double *ym,
+                       const double *ys, double margin, rcon *out) {
+  double a[3], b[3], al[3], bl[3], tmp[3], e[3], p[3];
+  seg_ends(cp, cm, cs[1], a, b);
+  for (int k = 0; k < 3; k++) tmp[k] = a[k] - yp[k];
+  mulmatTvec3(al, ym, tmp);
+  for (int k = 0; k < 3; k++) tmp[k] = b[k] - yp[k];
+  mulmatTvec3(bl, ym, tmp);
+  double lo = 0, hi = 1;
+  const double gr = 0.6180339887498949;
+  double x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), f1, f2;
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+  f1 = cyl_sd(p, ys[0], ys[1], e);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+  f2 = cyl_sd(p, ys[0], ys[1], e);
+  for (int it = 0; it < 40; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
+      f1 = cyl_sd(p, ys[0], ys[1], e);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+      for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
+      f2 = cyl_sd(p, ys[0], ys[1], e);
+    }
+  }
+  double ts = 0.5 * (lo + hi);
+  for (int k = 0; k < 3; k++) p[k] = al[k] + ts * (bl[k] - al[k]);
+  double fs = cyl_sd(p, ys[0], ys[1], e), f0 = cyl_sd(al, ys[0], ys[1], e), fb = cyl_sd(bl, ys[0], ys[1], e);
+  double t = ts;
+  if (f0 <= fs && f0 <= fb) t = 0;
+  else if (fb < fs) t = 1;
+  double cw[3];
+  for (int k = 0; k < 3; k++) cw[k] = a[k] + t * (b[k] - a[k]);
+  return sphere_cyl_core(cw, cs[0], yp, ym, ys, margin, out);
+}
+
+/* cylinder (geom1) vs box (geom2): the deeper of (a) the box vertex deepest in the
+ * cylinder and (b) the cylinder support point deepest in the box, found by 3 fixed-point
+ * steps d <- -(box normal at the current point); one contact, normal from cylinder to box */
+static int cyl_box(const double *yp, const double *ym, const double *ys, const double *bp, const double *bm,
+                   const double *h, double margin, rcon *out) {
+  double best = 1e300, bn[3] = {0, 0, 1}, bpos[3] = {0, 0, 0};
+  double v[3], w[3], tmp[3], pl[3], e[3], ew[3];
+  for (int i = 0; i < 8; i++) {
+    v[0] = (i & 1) ? h[0] : -h[0]; v[1] = (i & 2) ? h[1] : -h[1]; v[2] = (i & 4) ? h[2] : -h[2];
+    mulmatvec3(w, bm, v);
+    for (int k = 0; k < 3; k++) { w[k] += bp[k]; tmp[k] = w[k] - yp[k]; }
+    mulmatTvec3(pl, ym, tmp);
+    double sd = cyl_sd(pl, ys[0], ys[1], e);
+    if (sd < best) {
+      best = sd;
+      mulmatvec3(ew, ym, e);
+      for (int k = 0; k < 3; k++) { bn[k] = ew[k]; bpos[k] = w[k] - 0.5 * sd * ew[k]; }
+    }
+  }
+  double q[3] = {yp[0], yp[1], yp[2]};
+  for (int it = 0; it < 3; it++) {
+    for (int k = 0; k < 3; k++) tmp[k] = q[k] - bp[k];
+    mulmatTvec3(pl, bm, tmp);
+    box_sd(pl, h, e);
+    double d[3], dl[3];
+    mulmatvec3(ew, bm, e);
+    for (int k = 0; k < 3; k++) d[k] = -ew[k];
+    mulmatTvec3(dl, ym, d);
+    double rxy = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+    double sl[3] = {0, 0, dl[2] >= 0 ? ys[1] : -ys[1]};
+    if (rxy > MINVAL) { sl[0] = ys[0] * dl[0] / rxy; sl[1] = ys[0] * dl[1] / rxy; }
+    mulmatvec3(q, ym, sl);
+    for (int k = 0; k < 3; k++) q[k] += yp[k];
+    for (int k = 0; k < 3; k++) tmp[k] = q[k] - bp[k];
+    mulmatTvec3(pl, bm, tmp);
+    double sd = box_sd(pl, h, e);
+    if (sd < best) {
+      best = sd;
+      mulmatvec3(ew, bm, e);
+      for (int k = 0; k < 3; k++) { bn[k] = -ew[k]; bpos[k] = q[k] - 0.5 * sd * ew[k]; }
+    }
+  }
+  if (best > margin) return 0;
+  out->dist = best;
+  for (int k = 0; k < 3; k++) { out->n[k] = bn[k]; out->pos[k] = bpos[k]; }
+  return 1;
+}
+
 /* box (geom1) vs box (geom2): separating-axis test over 15 axes, then face clipping
  * (reference face vs incident face, up to 8 points) or one edge-edge contact. */
 static int clip_poly(double (*in)[2], int n, int axis, double lim, double sgn, double (*out)[2]) {
@@ -785,7 +907,11 @@ static int collide_geoms(const mgx_model_desc *m, ref_data *d, int g1, int g2, d
     return n;
   }
   if (t1 == GPLANE && t2 == GBOX) return plane_box(p1, m1, p2, m2, s2, margin, out);
-  return 0; /* unsupported pair types (cylinder, ellipsoid): not used by the headline task */
+  if (t1 == GSPHERE && t2 == GCYLINDER) return sphere_cyl_core(p1, s1[0], p2, m2, s2, margin, out);
+  if (t1 == GCAPSULE && t2 == GCYLINDER) return capsule_cyl(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GCYLINDER && t2 == GBOX) return cyl_box(p1, m1, s1, p2, m2, s2, margin, out);
+  return 0; /* unsupported pair types (plane-cylinder, cylinder-cylinder, ellipsoid): no task of
+               configs 1-4 has them */
 }
 
 static int add_contacts(const mgx_model_desc *m, ref_data *d, int pi, rcon *rc, int n) {
@@ -1214,12 +1340,61 @@ static void euler(const mgx_model_desc *m, ref_data *d) {
   d->time[0] += m->timestep;
 }
 
+/* mj_RungeKutta(m, d, 4) [ext]: classic RK4 Butcher tableau A = [.5; 0 .5; 0 0 1],
+ * B = [1/6 1/3 1/3 1/6]. Stage i evaluates mj_forwardSkip at X[i] = X[0] '+' h sum_j A_ij X'[j]
+ * (positions through integratePos); the final update is mj_advance with dX = sum_j B_j X'[j]:
+ * qvel += h dX_acc, qpos = integratePos(qpos0, dX_vel, h). The forward-pass outputs left in
+ * d (xpos, contacts, qacc) are those of the LAST stage evaluation, as in MuJoCo; the warmstart
+ * saved for the next step is that last stage's qacc (mj_advance copies d->qacc). */
+static void rk4(const mgx_model_desc *m, ref_data *d) {
+  static const double A[9] = {0.5, 0, 0, 0, 0.5, 0, 0, 0, 1.0};
+  static const double B[4] = {1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0};
+  int nq = m->nq, nv = m->nv;
+  double h = m->timestep, t0 = d->time[0];
+  double *X[4], *F[4];
+  double *buf = malloc(sizeof(double) * (4 * (nq + nv) + 4 * nv + 2 * nv));
+  for (int i = 0; i < 4; i++) { X[i] = buf + i * (nq + nv); F[i] = buf + 4 * (nq + nv) + i * nv; }
+  double *dX = buf + 4 * (nq + nv) + 4 * nv;
+  memcpy(X[0], d->qpos, sizeof(double) * nq);
+  memcpy(X[0] + nq, d->qvel, sizeof(double) * nv);
+  memcpy(F[0], d->qacc, sizeof(double) * nv);
+  for (int i = 1; i < 4; i++) {
+    double C = 0;
+    for (int j = 0; j < i; j++) C += A[(i - 1) * 3 + j];
+    memset(dX, 0, sizeof(double) * 2 * nv);
+    for (int j = 0; j < i; j++) {
+      double a = A[(i - 1) * 3 + j];
+      for (int k = 0; k < nv; k++) { dX[k] += a * X[j][nq + k]; dX[nv + k] += a * F[j][k]; }
+    }
+    memcpy(X[i], X[0], sizeof(double) * (nq + nv));
+    integrate_pos(m, X[i], dX, h);
+    for (int k = 0; k < nv; k++) X[i][nq + k] += h * dX[nv + k];
+    memcpy(d->qpos, X[i], sizeof(double) * nq);
+    memcpy(d->qvel, X[i] + nq, sizeof(double) * nv);
+    d->time[0] = t0 + C * h;
+    ref_forward(m, d);
+    memcpy(F[i], d->qacc, sizeof(double) * nv);
+  }
+  memset(dX, 0, sizeof(double) * 2 * nv);
+  for (int j = 0; j < 4; j++)
+    for (int k = 0; k < nv; k++) { dX[k] += B[j] * X[j][nq + k]; dX[nv + k] += B[j] * F[j][k]; }
+  d->time[0] = t0;
+  memcpy(d->qpos, X[0], sizeof(double) * nq);
+  memcpy(d->qvel, X[0] + nq, sizeof(double) * nv);
+  /* mj_advance */
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * nv);
+  for (int k = 0; k < nv; k++) d->qvel[k] += h * dX[nv + k];
+  integrate_pos(m, d->qpos, dX, h);
+  d->time[0] += h;
+  free(buf);
+}
+
 static int check_bad(const double *x, int n) {
   for (int i = 0; i < n; i++) if (isbad(x[i])) return 1;
   return 0;
 }
 
-/* mj_step: checkPos, checkVel, forward, checkAcc, Euler [ext] */
+/* mj_step: checkPos, checkVel, forward, checkAcc, then Euler or RK4 [ext] */
 void ref_step(const mgx_model_desc *m, ref_data *d) {
   if (check_bad(d->qpos, m->nq)) { ref_reset(m, d); d->warning[0]++; }
   if (check_bad(d->qvel, m->nv)) { ref_reset(m, d); d->warning[0]++; }
@@ -1228,6 +1403,10 @@ void ref_step(const mgx_model_desc *m, ref_data *d) {
     ref_reset(m, d);
     d->warning[0]++;
     ref_forward(m, d);
+  }
+  if (m->integrator == 1) {
+    rk4(m, d);
+    return;
   }
   memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * m->nv);
   euler(m, d);

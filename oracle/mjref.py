@@ -26,8 +26,10 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            build()
+        if os.path.exists(os.path.join(HERE, "Makefile")):
+            build()  # make: rebuilds when mjref.c / mjref.h / include/mgx.h changed
+        elif not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(LIB_PATH)
         _lib = C.CDLL(LIB_PATH)
         _lib.ref_create.restype = C.c_void_p
         _lib.ref_create.argtypes = [C.c_void_p, C.c_int, C.c_int]

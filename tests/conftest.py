@@ -41,3 +41,15 @@ def parkour_model():
 def parkour_packed(parkour_model):
     from mujoco_gymnasium_environments_amd import cabi
     return cabi.pack_model(parkour_model)
+
+
+@pytest.fixture(scope="session")
+def bipedal_model():
+    from mujoco_gymnasium_environments_amd.envs.bipedal import bipedal_model as load
+    return load()
+
+
+@pytest.fixture(scope="session")
+def bipedal_packed(bipedal_model):
+    from mujoco_gymnasium_environments_amd import cabi
+    return cabi.pack_model(bipedal_model)

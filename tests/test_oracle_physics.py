@@ -113,3 +113,84 @@ def test_joint_limit_row():
     assert int(s.nefc[0]) == 1 and s.efc_type[0] == 3
     assert abs(s.qpos[0] - 0.5) < 0.02               # rests on the upper limit (soft constraint)
     assert s.efc_force[0] > 0
+
+
+def test_rk4_ballistic_exact():
+    """RK4 integrates constant acceleration exactly: z = z0 + v0 t - g t^2 / 2 (no h-term
+    error, unlike semi-implicit Euler above)."""
+    m, pk, s = sim_of(HDR.replace('solver="PGS"', 'solver="PGS" integrator="RK4"') +
+                      '<worldbody><body pos="0 0 10"><freejoint/><geom type="sphere" size="0.1" mass="2"/>'
+                      '</body></worldbody></mujoco>')
+    assert m.integrator == 1
+    s.qvel[0:3] = [1.0, 0.0, 5.0]
+    s.step(50)
+    t = 0.5
+    np.testing.assert_allclose(s.qpos[:3], [t, 0, 10 + 5 * t - 5 * t * t], atol=1e-12)
+    np.testing.assert_allclose(s.qvel[2], 5 - 10 * t, atol=1e-12)
+
+
+def test_rk4_pendulum_matches_manual_rk4():
+    """One mj_step with RK4 equals a hand-rolled classic RK4 on (q, qdot) whose derivative is
+    the oracle's own forward-dynamics qacc (Butcher tableau of mj_RungeKutta)."""
+    xml = ('<mujoco><compiler angle="radian"/><option timestep="0.05" gravity="0 0 -9.81" integrator="RK4"/>'
+           '<worldbody><body><joint type="hinge" axis="0 1 0"/><geom type="capsule" fromto="0 0 0 0.6 0 0" '
+           'size="0.05" mass="1.5"/></body></worldbody></mujoco>')
+    m, pk, s = sim_of(xml)
+    m2 = mjcf.compile_xml(xml.replace(' integrator="RK4"', ''))
+    probe = RefSim(cabi.pack_model(m2))
+
+    def f(q, v):
+        probe.qpos[0], probe.qvel[0] = q, v
+        probe.forward()
+        return float(probe.qacc[0])
+    q, v = 0.3, -0.7
+    s.qpos[0], s.qvel[0] = q, v
+    h = 0.05
+    k1v, k1a = v, f(q, v)
+    k2v, k2a = v + 0.5 * h * k1a, f(q + 0.5 * h * k1v, v + 0.5 * h * k1a)
+    k3v, k3a = v + 0.5 * h * k2a, f(q + 0.5 * h * k2v, v + 0.5 * h * k2a)
+    k4v, k4a = v + h * k3a, f(q + h * k3v, v + h * k3a)
+    qn = q + h * (k1v / 6 + k2v / 3 + k3v / 3 + k4v / 6)
+    vn = v + h * (k1a / 6 + k2a / 3 + k3a / 3 + k4a / 6)
+    s.step()
+    assert abs(s.qpos[0] - qn) < 1e-13 and abs(s.qvel[0] - vn) < 1e-13
+
+
+CYL_SCENE = ('<mujoco><compiler angle="radian"/><option timestep="0.01" gravity="0 0 0"/><worldbody>'
+             '<geom name="cyl" type="cylinder" size="0.5 0.3" pos="1 2 0.3" {cylrot}/>'
+             '<body pos="{pos}" {rot}><freejoint/><geom name="probe" type="{ptype}" size="{psize}" mass="1"/></body>'
+             '</worldbody></mujoco>')
+
+
+def _cyl_contacts(ptype, psize, pos, rot="", cylrot=""):
+    xml = CYL_SCENE.format(ptype=ptype, psize=psize, pos=pos, rot=rot, cylrot=cylrot)
+    m, pk, s = sim_of(xml)
+    s.forward()
+    return m, s.contacts()
+
+
+@pytest.mark.parametrize("ptype,psize,pos,rot,dist,normal", [
+    # sphere above the top cap: dist = z - hh - R, normal from sphere (geom1) to cylinder
+    ("sphere", "0.2", "1.1 2.1 0.79", "", 0.79 - 0.6 - 0.2, [0, 0, -1]),
+    # sphere beside the lateral surface (pointing -x from the axis)
+    ("sphere", "0.2", "0.32 2 0.3", "", 0.68 - 0.5 - 0.2, [1, 0, 0]),
+    # capsule lying across the cap (axis along x): deepest segment point above the cap
+    ("capsule", "0.1 0.4", "1 2 0.695", 'euler="0 1.5707963267948966 0"', 0.695 - 0.6 - 0.1, [0, 0, -1]),
+])
+def test_cylinder_pairs_known_answers(ptype, psize, pos, rot, dist, normal):
+    m, c = _cyl_contacts(ptype, psize, pos, rot)
+    assert len(c["dist"]) == 1
+    assert abs(c["dist"][0] - dist) < 1e-9
+    np.testing.assert_allclose(c["frame"][0][:3], normal, atol=1e-9)
+
+
+def test_cylinder_box_cap_and_side():
+    # box resting on the top cap: the box vertices are the deepest features
+    m, c = _cyl_contacts("box", "0.2 0.2 0.1", "1 2 0.695")
+    assert len(c["dist"]) == 1 and abs(c["dist"][0] - (0.695 - 0.1 - 0.6)) < 1e-9
+    np.testing.assert_allclose(c["frame"][0][:3], [0, 0, 1], atol=1e-9)  # cylinder (geom1) -> box
+    # cylinder lying on its side (axis along y) under a wide flat box: the side line is deepest
+    m, c = _cyl_contacts("box", "1 1 0.1", "1 2 0.895", cylrot='euler="1.5707963267948966 0 0"')
+    # cylinder center z 0.3, radius 0.5 -> top of the side at 0.8; box bottom at 0.795
+    assert len(c["dist"]) == 1 and abs(c["dist"][0] - (0.795 - 0.8)) < 1e-9
+    np.testing.assert_allclose(c["frame"][0][:3], [0, 0, 1], atol=1e-9)
