@@ -443,6 +443,135 @@ def parkour_envlogic_vectors(env, n, seed=4321, max_contacts=14):
     return {k: np.asarray(v) for k, v in cols.items()}
 
 
+# ------------------------------------------------------------------------------- bipedal
+def bipedal_env():
+    install_stubs()
+    mod = load_module(f"{REF}/bipedal_rescue_env/rescue_env.py", "ref_rescue_env2")
+    return mod.BipedalRescueEnv(render_mode=None)
+
+
+def bipedal_reset_vectors(env, seeds):
+    """reset(seed) (rescue_env.py:347-396): qpos after _randomize_initial_state (the stub
+    mj_step does not move the state)."""
+    import contextlib
+    import io
+    rows = []
+    for s in seeds:
+        with contextlib.redirect_stdout(io.StringIO()):
+            env.reset(seed=int(s))
+        rows.append(env.data.qpos.copy())
+    return dict(seeds=np.asarray(seeds, np.int64), qpos=np.stack(rows))
+
+
+def bipedal_envlogic_vectors(env, n, seed=777, max_contacts=24):
+    """Random synthetic MjData-like states -> the reference's own step() (rescue_env.py:416-471)
+    with physics stubbed out: clip + ctrl, energy, victim pickup / rescue, obs, reward,
+    termination, truncation, stats, and the attributes that persist across resets (B3)."""
+    import contextlib
+    import io
+    c = env.model._c
+    rng = np.random.default_rng(seed)
+    torso, victims = env.torso_id, env.victim_ids
+    nb = c.nbody
+    cols = {}
+
+    def put(k, v):
+        cols.setdefault(k, []).append(v)
+    for i in range(n):
+        d = env.data
+        d.reset()
+        scen = i % 12
+        d.qpos[:] = rng.normal(scale=0.7, size=c.nq)
+        d.qvel[:] = rng.normal(scale=rng.choice([0.5, 5.0]), size=c.nv)
+        xpos = rng.uniform(-3, 3, (nb, 3))
+        rx, ry = rng.choice([rng.uniform(-27, 27), rng.uniform(-6, 6), rng.uniform(17, 23)]), rng.uniform(-27, 27) \
+            if scen in (0, 1) else rng.uniform(-4, 4)
+        xpos[torso] = [rx, ry, rng.uniform(0.3, 2.5)]
+        for k, v in enumerate(victims):
+            if scen in (2, 3, 4) and k < 3:  # victims near the robot: pickups
+                xpos[v] = xpos[torso] + [rng.uniform(-1.0, 1.0), rng.uniform(-1.0, 1.0), rng.uniform(-1, 0)]
+            else:
+                xpos[v] = [rng.uniform(-12, 12), rng.uniform(-12, 12), rng.uniform(0, 1)]
+        if scen in (5, 6):  # in the safe zone (20, 0), radius 3
+            xpos[torso][:2] = [20 + rng.uniform(-3.2, 3.2), rng.uniform(-3.2, 3.2)]
+        if scen == 7:  # in a fire zone
+            xpos[torso][:2] = [-5 + rng.uniform(-1.6, 1.6), -3 + rng.uniform(-1.6, 1.6)]
+        d.xpos[:] = xpos
+        q = rng.normal(size=4)
+        if scen % 3:
+            q = np.array([1.0, *rng.normal(scale=0.3, size=3)])
+        d.xquat[:] = np.tile(q / np.linalg.norm(q), (nb, 1))
+        ncon = int(rng.integers(0, max_contacts + 1))
+        dists = rng.choice([rng.uniform(-0.05, 0.01), rng.uniform(-0.3, 0.01)], size=ncon)
+        d.contact = [FakeContact(0, 1, dd, np.zeros(5)) for dd in dists]
+        d.ncon = ncon
+        perm = list(rng.permutation(5))
+        nres = int(rng.integers(0, 6)) if scen != 8 else 4
+        rescued = [int(x) for x in perm[:nres]]
+        rest = perm[nres:]
+        ncar = int(rng.integers(0, min(3, len(rest)) + 1))
+        carried = [int(x) for x in rest[:ncar]]
+        env.victims_rescued = list(rescued)
+        env.victims_carried = list(carried)
+        env.carrying_victims = bool(carried) if scen != 9 else bool(rng.random() < 0.5)
+        env.current_step = int(rng.choice([0, 1, 9998, 9999, 10000, int(rng.integers(0, 10000))]))
+        env.current_energy = np.float32(rng.choice([1000.0, rng.uniform(0.0, 3.0), rng.uniform(0, 1000)])) \
+            if scen != 10 else 1000.0
+        env.closest_victim_distance = float(rng.choice([np.inf, rng.uniform(0, 15)]))
+        persist = {}
+        for k, gen in (("_prev_rescued_count", lambda: int(rng.integers(0, 6))),
+                       ("_prev_carried_count", lambda: int(rng.integers(0, 3))),
+                       ("_prev_safe_zone_distance", lambda: float(rng.uniform(0, 30))),
+                       ("_fall_timer", lambda: int(rng.choice([0, 99, 100, 101, int(rng.integers(0, 200))])))):
+            if rng.random() < 0.75:
+                setattr(env, k, gen())
+                persist[k] = getattr(env, k)
+            elif hasattr(env, k):
+                delattr(env, k)
+        es = env.episode_stats
+        es.update(victims_rescued=len(rescued), distance_traveled=float(rng.uniform(0, 50)),
+                  energy_used=np.float32(rng.uniform(0, 100)), falls=int(rng.integers(0, 10)),
+                  collisions=int(rng.integers(0, 10)),
+                  time_to_first_rescue=None if rng.random() < 0.5 else float(rng.uniform(0, 100)))
+        env.prev_robot_pos = xpos[torso] + rng.normal(scale=0.2, size=3)
+        inp = dict(qpos=d.qpos.copy(), qvel=d.qvel.copy(), xpos=xpos, xquat=d.xquat.copy(), ncon=ncon,
+                   con_dist=_pad(dists, max_contacts), rescued_mask_in=sum(1 << v for v in rescued),
+                   carried_in=_pad(np.array(carried, dtype=np.float64), 5, None, -1.0),
+                   rescued_in=_pad(np.array(rescued, dtype=np.float64), 5, None, -1.0),
+                   carrying_in=env.carrying_victims, current_step_in=env.current_step,
+                   energy_in=float(env.current_energy), closest_in=env.closest_victim_distance,
+                   prev_rescued_in=persist.get("_prev_rescued_count", -1),
+                   prev_carried_in=persist.get("_prev_carried_count", -1),
+                   prev_sz_in=persist.get("_prev_safe_zone_distance", np.nan),
+                   fall_timer_in=persist.get("_fall_timer", -1),
+                   stats_in=np.array([es["victims_rescued"], es["distance_traveled"], es["energy_used"],
+                                      np.nan if es["time_to_first_rescue"] is None else es["time_to_first_rescue"],
+                                      es["falls"], es["collisions"]], dtype=np.float64),
+                   prev_robot_pos_in=env.prev_robot_pos.copy())
+        lim = env.action_space.high
+        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim * rng.choice([1.0, 0.01])).astype(np.float32)
+        with contextlib.redirect_stdout(io.StringIO()):
+            obs, reward, term, trunc, info = env.step(action)
+        es = env.episode_stats
+        out = dict(action=action, obs=obs, reward=float(reward), terminated=bool(term), truncated=bool(trunc),
+                   ctrl_out=d.ctrl.copy(), rescued_out=_pad(np.array(env.victims_rescued, dtype=np.float64), 5, None, -1),
+                   carried_out=_pad(np.array(env.victims_carried, dtype=np.float64), 5, None, -1),
+                   carrying_out=env.carrying_victims, current_step_out=env.current_step,
+                   energy_out=float(env.current_energy), energy_is_f32=isinstance(env.current_energy, np.float32),
+                   closest_out=float(env.closest_victim_distance),
+                   prev_rescued_out=getattr(env, "_prev_rescued_count", -1),
+                   prev_carried_out=getattr(env, "_prev_carried_count", -1),
+                   prev_sz_out=getattr(env, "_prev_safe_zone_distance", np.nan),
+                   fall_timer_out=getattr(env, "_fall_timer", -1),
+                   stats_out=np.array([es["victims_rescued"], es["distance_traveled"], es["energy_used"],
+                                       np.nan if es["time_to_first_rescue"] is None else es["time_to_first_rescue"],
+                                       es["falls"], es["collisions"]], dtype=np.float64),
+                   prev_robot_pos_out=env.prev_robot_pos.copy(), upright=bool(info["robot_upright"]))
+        for k, v in {**inp, **out}.items():
+            put(k, v)
+    return {k: np.asarray(v) for k, v in cols.items()}
+
+
 def main():
     install_stubs()
     dump_xml()
@@ -452,6 +581,9 @@ def main():
     penv = parkour_env()
     np.savez_compressed(f"{HERE}/parkour_reset.npz", **parkour_reset_vectors(penv, list(range(0, 40)) + [12345]))
     np.savez_compressed(f"{HERE}/parkour_envlogic.npz", **parkour_envlogic_vectors(penv, 500))
+    benv = bipedal_env()
+    np.savez_compressed(f"{HERE}/bipedal_reset.npz", **bipedal_reset_vectors(benv, list(range(0, 40)) + [4242]))
+    np.savez_compressed(f"{HERE}/bipedal_envlogic.npz", **bipedal_envlogic_vectors(benv, 600))
     print("fixtures written to", HERE)
 
 
