@@ -284,6 +284,79 @@ typedef struct mgx_parkour_logic_io {
 int mgx_parkour_logic_test(const mgx_model *m, const mgx_parkour_logic_io *io, const mgx_parkour_env *e, int n_env,
                            void *stream);
 
+/* ---- bipedal_rescue env logic fused with physics (RK4) ------------------------------- */
+/* Index tables (bipedal_rescue_env/rescue_env.py:280-323, :473-508). */
+typedef struct mgx_bipedal_ids {
+  int32_t torso;                 /* body id of 'torso' */
+  int32_t victims[5];            /* body ids of victim1..5 */
+  int32_t obs_qposadr[26];       /* jnt_qposadr of joint_names (rescue_env.py:298-308) */
+  int32_t obs_dofadr[26];        /* jnt_dofadr of the same joints */
+  int32_t root_x, root_y, root_z;/* qpos addresses of the root slides (:481-492) */
+  int32_t root_dof;              /* jnt_dofadr of root_x (_get_robot_velocity :731-737) */
+  int32_t victim_x[5], victim_y[5]; /* qpos addresses of victim{i}_x / _y (:495-508) */
+  int32_t n_act;                 /* 26 actuators written from the action */
+  int32_t max_episode_steps;     /* 10000 (rescue_env.py:41) */
+} mgx_bipedal_ids;
+
+/* Persistent per-env task state (device, env-major). Victim lists are bitmasks (bit i =
+ * victim i+1); "absent attribute" sentinels reproduce the lazily created attributes that
+ * survive reset() (quirk B3). */
+typedef struct mgx_bipedal_env {
+  int32_t *step;             /* [N] current_step */
+  float *energy;             /* [N] current_energy (float32, as numpy leaves it) */
+  float *energy_used;        /* [N] episode_stats['energy_used'] (float32) */
+  int32_t *rescued;          /* [N] victims_rescued bitmask */
+  int32_t *carried;          /* [N] victims_carried bitmask */
+  uint8_t *carrying;         /* [N] carrying_victims */
+  double *closest;           /* [N] closest_victim_distance (+inf after reset) */
+  int32_t *prev_rescued;     /* [N] _prev_rescued_count, -1 = absent; survives reset */
+  int32_t *prev_carried;     /* [N] _prev_carried_count, -1 = absent; survives reset */
+  double *prev_sz;           /* [N] _prev_safe_zone_distance, NaN = absent; survives reset */
+  int32_t *fall_timer;       /* [N] _fall_timer, -1 = absent; survives reset */
+  int32_t *victims_rescued;  /* [N] episode_stats['victims_rescued'] */
+  double *distance;          /* [N] episode_stats['distance_traveled'] */
+  double *ttfr;              /* [N] episode_stats['time_to_first_rescue'], NaN = None */
+  int32_t *falls;            /* [N] episode_stats['falls'] */
+  int32_t *collisions;       /* [N] episode_stats['collisions'] */
+  double *prev_robot_pos;    /* [N][3] */
+  int32_t *episode;          /* [N] episodes started (keys device reset draws); nullable with host draws */
+  void *rollout;             /* [N][4] reward, terminated, truncated, env steps (nullable) */
+} mgx_bipedal_env;
+
+int mgx_bipedal_configure(mgx_model *m, const mgx_bipedal_ids *ids);
+
+/* One env step for N envs (rescue_env.py:416-471): clip to +-100, ctrl[:26], float32 energy,
+ * one RK4 mj_step, victim pickup / rescue, observation [N][102] float32, reward [N] float64,
+ * terminated / truncated, stats. autoreset as mgx_parkour_step (Philox draws keyed by
+ * (seed, env_offset + env, episode)). */
+int mgx_bipedal_step(const mgx_model *m, const mgx_state *s, const mgx_bipedal_env *e, const float *action,
+                     float *obs, double *reward, uint8_t *terminated, uint8_t *truncated, float *final_obs,
+                     int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t *env_mask,
+                     void *stream);
+
+/* reset() for masked envs (rescue_env.py:347-396): mj_resetData, tracking reset, the 12
+ * position draws (`draws` [N][12] real in reference order; NULL = device Philox), 10 settle
+ * mj_step's, obs, prev_robot_pos. */
+int mgx_bipedal_reset(const mgx_model *m, const mgx_state *s, const mgx_bipedal_env *e, const void *draws,
+                      float *obs, uint64_t seed, int env_offset, int n_env, const uint8_t *env_mask, void *stream);
+
+/* Test hook: bipedal env logic only (clip/ctrl/energy, interactions, obs, reward,
+ * termination, stats) on caller-supplied frames and contact distances (no physics). */
+typedef struct mgx_bipedal_logic_io {
+  const void *qpos, *qvel, *xpos, *xquat; /* [N][nq] [N][nv] [N][nbody][3] [N][nbody][4] */
+  const int32_t *ncon;                    /* [N] */
+  const void *con_dist;                   /* [N][max_contacts] */
+  int32_t max_contacts;
+  int32_t pad0;
+  void *ctrl;                             /* out [N][nu] */
+  const float *action;                    /* [N][26] */
+  float *obs;                             /* [N][102] */
+  double *reward;
+  uint8_t *terminated, *truncated, *upright;
+} mgx_bipedal_logic_io;
+int mgx_bipedal_logic_test(const mgx_model *m, const mgx_bipedal_logic_io *io, const mgx_bipedal_env *e, int n_env,
+                           void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,13 +8,16 @@ Public surface:
   envs.HumanoidSoccerEnv     drop-in gymnasium-style single env
   envs.ParkourVectorEnv      batched quadruped_parkour (10 substeps per env step)
   envs.QuadrupedParkourEnv   drop-in gymnasium-style single env
+  envs.BipedalVectorEnv      batched bipedal_rescue (RK4, rows in global scratch)
+  envs.BipedalRescueEnv      drop-in gymnasium-style single env
 The compute path is libmgx.so (HIP, gfx950); there is no CPU fallback.
 """
 __version__ = "0.1.0"
 
 
 def __getattr__(name):  # lazy: importing the package must not require a GPU
-    if name in ("HumanoidSoccerEnv", "SoccerVectorEnv", "register_envs", "ParkourVectorEnv", "QuadrupedParkourEnv"):
+    if name in ("HumanoidSoccerEnv", "SoccerVectorEnv", "register_envs", "ParkourVectorEnv", "QuadrupedParkourEnv",
+                "BipedalVectorEnv", "BipedalRescueEnv"):
         from . import envs
         return getattr(envs, name)
     raise AttributeError(name)

@@ -108,6 +108,27 @@ class MgxParkourLogicIO(C.Structure):
                 ("truncated", C.c_void_p)]
 
 
+class MgxBipedalIds(C.Structure):
+    _fields_ = [("torso", C.c_int32), ("victims", C.c_int32 * 5), ("obs_qposadr", C.c_int32 * 26),
+                ("obs_dofadr", C.c_int32 * 26), ("root_x", C.c_int32), ("root_y", C.c_int32), ("root_z", C.c_int32),
+                ("root_dof", C.c_int32), ("victim_x", C.c_int32 * 5), ("victim_y", C.c_int32 * 5),
+                ("n_act", C.c_int32), ("max_episode_steps", C.c_int32)]
+
+
+class MgxBipedalEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ["step", "energy", "energy_used", "rescued", "carried", "carrying", "closest", "prev_rescued",
+                 "prev_carried", "prev_sz", "fall_timer", "victims_rescued", "distance", "ttfr", "falls", "collisions",
+                 "prev_robot_pos", "episode", "rollout"]]
+
+
+class MgxBipedalLogicIO(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("xpos", C.c_void_p), ("xquat", C.c_void_p),
+                ("ncon", C.c_void_p), ("con_dist", C.c_void_p), ("max_contacts", C.c_int32), ("pad0", C.c_int32),
+                ("ctrl", C.c_void_p), ("action", C.c_void_p), ("obs", C.c_void_p), ("reward", C.c_void_p),
+                ("terminated", C.c_void_p), ("truncated", C.c_void_p), ("upright", C.c_void_p)]
+
+
 class MgxSoccerIds(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ["torso", "ball", "goalkeeper", "ball_geom", "right_foot", "left_foot", "field_geom",

@@ -1,11 +1,13 @@
 // mgx_internal.h — host-side definitions shared by the translation units of libmgx.so
-// (mgx_api.hip: model, physics and soccer; mgx_parkour.hip: quadruped_parkour).
+// (mgx_api.hip: model, physics and soccer; mgx_step.hip: generic step; mgx_parkour.hip:
+// quadruped_parkour; mgx_bipedal.hip: bipedal_rescue).
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <string>
 
 #include "../../include/mgx.h"
+#include "mgx_bipedal.h"
 #include "mgx_parkour.h"
 #include "mgx_staged.h"
 
@@ -23,6 +25,8 @@ struct mgx_model {
   bool parkour_ok = false;
   mgx::ParkourIds<float> pkf;
   mgx::ParkourIds<double> pkd;
+  bool bipedal_ok = false;
+  mgx::BipedalIds bp;
   int npair;
   bool staged_ok = false;  // the staged soccer pipeline supports this model's capacities
 };

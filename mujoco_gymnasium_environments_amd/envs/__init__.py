@@ -1,4 +1,5 @@
 """Task environments. humanoid_soccer is the headline task (BASELINE.json); quadruped_parkour is
-the low-DoF bring-up task (BASELINE configs 1-2)."""
+the low-DoF bring-up task (BASELINE configs 1-2); bipedal_rescue is the RK4 scaling task (config 4)."""
+from .bipedal import BipedalRescueEnv, BipedalVectorEnv  # noqa: F401
 from .parkour import ParkourVectorEnv, QuadrupedParkourEnv  # noqa: F401
 from .soccer import HumanoidSoccerEnv, SoccerVectorEnv, register_envs  # noqa: F401

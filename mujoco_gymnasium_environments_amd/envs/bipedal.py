@@ -1,21 +1,59 @@
-"""bipedal_rescue_env on MI355X (BASELINE configs[3]): model loader and capacities.
+"""bipedal_rescue_env on MI355X (BASELINE configs[3]): a batched VectorEnv and a drop-in
+gymnasium-style Env.
+
+Mirrors the reference interface bipedal_rescue_env/rescue_env.py:
+  * ``BipedalRescueEnv`` — same constructor / ``reset(seed, options)`` / ``step(action)`` /
+    spaces / ``metadata`` / ``render`` / ``close`` / ``info`` surface as the reference class
+    (rescue_env.py:28-793), batch size 1, gymnasium seeding (PCG64 over SeedSequence) and the
+    same 12 position draws per reset (:473-508).
+  * ``BipedalVectorEnv`` — N envs on one GPU, device tensors ``[N, ...]``, same-step autoreset
+    with Philox reset draws keyed by (seed, global env index, episode).
+Both run one fused HIP launch per env step (libmgx.so ``mgx_bipedal_step``): clip, float32
+energy, one RK4 mj_step, victim pickup / rescue, observation / reward / termination / stats.
 
 The composed model is the output of the reference's own composition code
-(bipedal_rescue_env/rescue_env.py:121-277, tests/golden/make_fixtures.py): RK4 integrator
-(rescue_env.py:148), PGS, nq = nv = 63, 41 bodies, 89 geoms, 3185 candidate pairs including
-static cylinders. Under random actions it holds up to ~130 contacts / ~520 constraint rows
-(oracle rollouts), so its rows live in global scratch (Layout.gB) rather than LDS.
+(rescue_env.py:121-277, tests/golden/make_fixtures.py): RK4 integrator (rescue_env.py:148),
+PGS, nq = nv = 63, 41 bodies, 89 geoms, 3185 candidate pairs including static cylinders.
+Under random actions it holds up to ~130 contacts / ~520 constraint rows (oracle rollouts),
+so its rows live in global scratch (Layout.gB) rather than LDS.
 """
 from __future__ import annotations
 
+import ctypes as C
 import functools
 import os
+from typing import Any, Dict, Optional, Tuple
 
-from .. import mjcf
+import numpy as np
+import torch
+
+from .. import cabi, mjcf
+from ..batch import PhysicsBatch, _ptr, stream_handle
+from ..native import check, lib
+from ..seeding import np_random
+from ..spaces import Box, EnvBase
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "bipedal_rescue.xml")
 EFC_CAPACITY = 512
 CON_CAPACITY = 128
+
+# rescue_env.py:298-308
+JOINT_NAMES = [
+    'neck_pitch', 'neck_yaw',
+    'right_shoulder_pitch', 'right_shoulder_roll', 'right_elbow', 'right_wrist',
+    'right_finger1_joint', 'right_finger2_joint',
+    'left_shoulder_pitch', 'left_shoulder_roll', 'left_elbow', 'left_wrist',
+    'left_finger1_joint', 'left_finger2_joint',
+    'right_hip_roll', 'right_hip_pitch', 'right_hip_yaw', 'right_knee_joint',
+    'right_ankle_pitch', 'right_ankle_roll',
+    'left_hip_roll', 'left_hip_pitch', 'left_hip_yaw', 'left_knee_joint',
+    'left_ankle_pitch', 'left_ankle_roll']
+OBS_DIM = 102
+N_ACT = 26
+MAX_EPISODE_STEPS = 10000          # rescue_env.py:41
+ACTION_LIMIT = 100.0               # rescue_env.py:328-333
+SAFE_ZONE_POS = np.array([20.0, 0.0, 0.0])
+ENERGY_LIMIT = 1000.0
 
 
 @functools.lru_cache(maxsize=None)
@@ -25,3 +63,242 @@ def bipedal_model() -> mjcf.Model:
     m.efc_capacity = EFC_CAPACITY
     m.con_capacity = CON_CAPACITY
     return m
+
+
+class BipedalTables:
+    """Index tables looked up exactly as rescue_env.py:280-323 and :473-508 do."""
+
+    def __init__(self, m: mjcf.Model, max_episode_steps: int = MAX_EPISODE_STEPS):
+        self.model = m
+        self.torso = m.name2id("body", "torso")
+        self.victims = [m.name2id("body", f"victim{i}") for i in range(1, 6)]
+        self.joints = [m.name2id("joint", n) for n in JOINT_NAMES]
+        q = lambda name: int(m.jnt_qposadr[m.name2id("joint", name)])  # noqa: E731
+        self.root_x, self.root_y, self.root_z = q("root_x"), q("root_y"), q("root_z")
+        self.root_dof = int(m.jnt_dofadr[m.name2id("joint", "root_x")])
+        self.victim_x = [q(f"victim{i}_x") for i in range(1, 6)]
+        self.victim_y = [q(f"victim{i}_y") for i in range(1, 6)]
+        self.max_episode_steps = max_episode_steps
+
+    def ids_struct(self) -> cabi.MgxBipedalIds:
+        m, s = self.model, cabi.MgxBipedalIds()
+        s.torso = self.torso
+        for i in range(5):
+            s.victims[i] = self.victims[i]
+            s.victim_x[i] = self.victim_x[i]
+            s.victim_y[i] = self.victim_y[i]
+        for i, j in enumerate(self.joints):
+            s.obs_qposadr[i] = int(m.jnt_qposadr[j])
+            s.obs_dofadr[i] = int(m.jnt_dofadr[j])
+        s.root_x, s.root_y, s.root_z, s.root_dof = self.root_x, self.root_y, self.root_z, self.root_dof
+        s.n_act = N_ACT
+        s.max_episode_steps = self.max_episode_steps
+        return s
+
+    @staticmethod
+    def reset_draws(rng: np.random.Generator) -> np.ndarray:
+        """The 12 uniform draws of one reset, in reference order (rescue_env.py:476-508)."""
+        d = [rng.uniform(-5.0, 5.0), rng.uniform(-5.0, 5.0)]
+        for _ in range(5):
+            d += [rng.uniform(-1.0, 1.0), rng.uniform(-1.0, 1.0)]
+        return np.array(d)
+
+
+class BipedalVectorEnv:
+    """``num_envs`` bipedal_rescue envs stepping in lockstep on one GPU."""
+
+    metadata = {'render_modes': [], 'render_fps': 50}
+
+    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
+                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
+        self.num_envs = num_envs
+        self.device = torch.device(device)
+        self.model = bipedal_model()
+        self.tables = BipedalTables(self.model, max_episode_steps)
+        self.batch = PhysicsBatch(self.model, num_envs, precision=precision, device=device)
+        self.native = self.batch.native
+        self.autoreset = autoreset
+        self.seed_value = int(seed) & ((1 << 64) - 1)
+        self.env_offset = env_offset
+        dev, N = self.device, num_envs
+        i32 = dict(dtype=torch.int32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.step_count = torch.zeros(N, **i32)
+        self.energy = torch.full((N,), ENERGY_LIMIT, dtype=torch.float32, device=dev)
+        self.energy_used = torch.zeros(N, dtype=torch.float32, device=dev)
+        self.rescued = torch.zeros(N, **i32)
+        self.carried = torch.zeros(N, **i32)
+        self.carrying = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self.closest = torch.full((N,), float("inf"), **f64)
+        # attributes the reference creates lazily and never clears (quirk B3): -1 / NaN = absent
+        self.prev_rescued = torch.full((N,), -1, **i32)
+        self.prev_carried = torch.full((N,), -1, **i32)
+        self.prev_sz = torch.full((N,), float("nan"), **f64)
+        self.fall_timer = torch.full((N,), -1, **i32)
+        self.victims_rescued = torch.zeros(N, **i32)
+        self.distance = torch.zeros(N, **f64)
+        self.ttfr = torch.full((N,), float("nan"), **f64)
+        self.falls = torch.zeros(N, **i32)
+        self.collisions = torch.zeros(N, **i32)
+        self.prev_robot_pos = torch.zeros(N, 3, **f64)
+        self.episode = torch.zeros(N, **i32)
+        self.rollout = torch.zeros(N, 4, dtype=self.batch.dtype, device=dev)
+        self.obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
+        self.final_obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
+        self.reward = torch.zeros(N, **f64)
+        self.terminated = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self.truncated = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self._env = cabi.MgxBipedalEnv(*[t.data_ptr() for t in (
+            self.step_count, self.energy, self.energy_used, self.rescued, self.carried, self.carrying, self.closest,
+            self.prev_rescued, self.prev_carried, self.prev_sz, self.fall_timer, self.victims_rescued, self.distance,
+            self.ttfr, self.falls, self.collisions, self.prev_robot_pos, self.episode, self.rollout)])
+        ids = self.tables.ids_struct()
+        check(lib().mgx_bipedal_configure(self.native.handle, C.byref(ids)), "mgx_bipedal_configure")
+        self.action_space = Box(low=-ACTION_LIMIT, high=ACTION_LIMIT, shape=(N_ACT,), dtype=np.float32)
+
+    def reset(self, seed: Optional[int] = None, env_mask: Optional[torch.Tensor] = None,
+              draws: Optional[np.ndarray] = None, stream=None) -> Tuple[torch.Tensor, Dict[str, Any]]:
+        """reset() for all (or masked) envs. ``draws`` [N,12] (host, reference order) gives exact
+        gymnasium seeding; otherwise device Philox draws keyed by (seed, env, episode)."""
+        if seed is not None:
+            self.seed_value = int(seed) & ((1 << 64) - 1)
+            self.episode.zero_()
+        d = None
+        if draws is not None:
+            d = torch.as_tensor(np.asarray(draws).reshape(self.num_envs, 12), dtype=self.batch.dtype).to(self.device)
+        check(lib().mgx_bipedal_reset(self.native.handle, C.byref(self.batch.state), C.byref(self._env), _ptr(d),
+                                      _ptr(self.obs), self.seed_value, self.env_offset, self.num_envs, _ptr(env_mask),
+                                      stream_handle(stream)), "mgx_bipedal_reset")
+        return self.obs, self.info()
+
+    def step(self, actions: torch.Tensor, stream=None):
+        """One env step (one RK4 mj_step) for every env. ``actions`` float32 [N, 26]."""
+        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        assert actions.shape == (self.num_envs, N_ACT), actions.shape
+        check(lib().mgx_bipedal_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
+                                     _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
+                                     _ptr(self.truncated), _ptr(self.final_obs) if self.autoreset else None,
+                                     1 if self.autoreset else 0, self.seed_value, self.env_offset, self.num_envs,
+                                     None, stream_handle(stream)), "mgx_bipedal_step")
+        return self.obs, self.reward, self.terminated, self.truncated, self.info()
+
+    def info(self) -> Dict[str, Any]:
+        """Device-tensor views of the reference's info dict (rescue_env.py:447-456)."""
+        return {
+            'victims_rescued': self.victims_rescued,
+            'distance_traveled': self.distance,
+            'energy_used': self.energy_used,
+            'time_to_first_rescue': self.ttfr,
+            'falls': self.falls,
+            'collisions': self.collisions,
+            'robot_position': self.prev_robot_pos,
+            'victims_remaining': 5 - _popcount5(self.rescued),
+            'victims_carried': _popcount5(self.carried),
+            'energy_remaining': self.energy,
+            'final_observation': self.final_obs,
+            'episode': self.episode,
+            'bad_state_resets': self.batch.warning,
+        }
+
+    def close(self):
+        pass
+
+
+def _popcount5(x: torch.Tensor) -> torch.Tensor:
+    c = torch.zeros_like(x)
+    for b in range(5):
+        c += (x >> b) & 1
+    return c
+
+
+class BipedalRescueEnv(EnvBase):
+    """Drop-in for bipedal_rescue_env.rescue_env.BipedalRescueEnv, simulated by libmgx."""
+
+    metadata = {'render_modes': ['human', 'rgb_array', 'depth_array'], 'render_fps': 50}
+
+    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f32", **kwargs):
+        super().__init__()
+        self.render_mode = render_mode
+        self.dt = 0.02
+        self.max_episode_steps = MAX_EPISODE_STEPS
+        self.world_size = 50.0
+        self.safe_zone_radius = 3.0
+        self.safe_zone_pos = SAFE_ZONE_POS.copy()
+        self.robot_height = 1.2
+        self.carry_capacity = 2
+        self.energy_limit = ENERGY_LIMIT
+        self.num_victims = 5
+        self.victim_weights = [60, 30, 50, 55, 65]
+        self.victim_priorities = [0.8, 1.0, 0.7, 0.9, 1.0]
+        self.fire_zones = [{'pos': np.array([-5.0, -3.0, 0.0]), 'radius': 1.5},
+                           {'pos': np.array([8.0, 6.0, 0.0]), 'radius': 1.2}]
+        self._vec = BipedalVectorEnv(1, device=device, precision=precision, autoreset=False,
+                                     max_episode_steps=self.max_episode_steps)
+        self.model = self._vec.model
+        self.num_actuators = N_ACT
+        self.action_space = Box(low=-ACTION_LIMIT, high=ACTION_LIMIT, shape=(N_ACT,), dtype=np.float32)
+        self.observation_space = Box(low=-np.inf, high=np.inf, shape=(OBS_DIM,), dtype=np.float32)
+        self.viewer = None
+        self.np_random = None
+        self.current_step = 0
+        self.seed()
+
+    def seed(self, seed: Optional[int] = None) -> list:
+        self.np_random, seed = np_random(seed)
+        return [seed]
+
+    def reset(self, seed: Optional[int] = None, options: Optional[dict] = None):
+        if seed is not None:
+            self.seed(seed)
+        draws = self._vec.tables.reset_draws(self.np_random)[None]
+        obs, _ = self._vec.reset(draws=draws)
+        torch.cuda.synchronize(self._vec.device)
+        self.current_step = 0
+        info = self._info()
+        return obs[0].cpu().numpy().copy(), {k: info[k] for k in
+                                              ('episode_stats', 'robot_position', 'victims_remaining',
+                                               'energy_remaining')}
+
+    def step(self, action: np.ndarray):
+        a = torch.from_numpy(np.asarray(action, dtype=np.float32).reshape(1, -1)).to(self._vec.device)
+        obs, rew, term, trunc, _ = self._vec.step(a)
+        torch.cuda.synchronize(self._vec.device)
+        self.current_step = int(self._vec.step_count[0])
+        info = self._info()
+        return obs[0].cpu().numpy().copy(), float(rew[0]), bool(term[0]), bool(trunc[0]), info
+
+    def _info(self) -> Dict[str, Any]:
+        v = self._vec
+        ttfr = float(v.ttfr[0])
+        stats = {'victims_rescued': int(v.victims_rescued[0]), 'distance_traveled': float(v.distance[0]),
+                 'energy_used': np.float32(v.energy_used[0].item()),
+                 'time_to_first_rescue': None if np.isnan(ttfr) else ttfr,
+                 'falls': int(v.falls[0]), 'collisions': int(v.collisions[0])}
+        up = v.obs[0, 55:59].double().cpu().numpy()
+        w, x, y, z = up
+        return {'episode_stats': stats, 'robot_position': v.prev_robot_pos[0].cpu().numpy().copy(),
+                'victims_remaining': 5 - bin(int(v.rescued[0])).count("1"),
+                'victims_carried': bin(int(v.carried[0])).count("1"),
+                'energy_remaining': np.float32(v.energy[0].item()),
+                'robot_upright': bool(w * w - x * x - y * y + z * z > 0.7)}
+
+    def render(self):
+        return None  # rescue_env.py:779-783 (viewer sync only)
+
+    def close(self):
+        self.viewer = None
+
+
+def register_envs() -> bool:
+    """Register BipedalRescue-v0 with gymnasium when installed (rescue_env.py:793-804)."""
+    try:
+        import gymnasium as gym  # type: ignore
+    except Exception:  # noqa: BLE001
+        return False
+    try:
+        gym.register(id='BipedalRescue-v0', entry_point='mujoco_gymnasium_environments_amd.envs.bipedal:BipedalRescueEnv',
+                     max_episode_steps=10000, reward_threshold=20000.0)
+    except Exception:  # noqa: BLE001 - already registered
+        pass
+    return True
