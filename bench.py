@@ -16,6 +16,11 @@ metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
 --task parkour benchmarks BASELINE configs[1] instead (quadruped_parkour, 4096 envs/GPU): one
 step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obstacle motors,
 obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
+
+--task bipedal benchmarks BASELINE configs[3] (bipedal_rescue, 8192 envs/GPU by default): one
+step = BipedalVectorEnv.step = mgx_bipedal_step (clip, float32 energy, one RK4 mj_step with the
+constraint rows in per-env global scratch, victim interactions, obs/reward/termination/stats,
+same-step autoreset), actions U(-100, 100)^26.
 """
 from __future__ import annotations
 
@@ -35,6 +40,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 PMC_PROFILE = "r01_v4_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
+PMC_PROFILE_BIPEDAL = "r01_bipedal_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
@@ -44,6 +50,31 @@ ALG_BYTES_PER_ENV_STEP = 4 * (2 * 121 + 33 + 2 * 3 + 2 * 11 + 80) + 8 + 2
 # + er_kind (u8) + reached/fall/stuck/step (int32), write obs 95, reward (fp64), flags (u8)
 PARKOUR_ALG_BYTES = 4 * (2 * 112 + 2 * 2 + 16 + 2 * 4 + 95) + 2 * 8 + 2 + 2 * 16 + 8 + 2
 PARKOUR_METRIC = "env steps/sec (whole node), quadruped_parkour 4096 envs/GPU (BASELINE configs[1])"
+# bipedal: r/w qpos 63 + qvel 63 + qacc_warmstart 63 and ctrl 26 (fp32), read
+# action 26, r/w nine int32 task scalars, energy + energy_used (fp32), carrying (u8), closest,
+# prev_sz, distance, prev_robot_pos[3] (fp64), read ttfr (fp64), write obs 102 (fp32), reward
+# (fp64), flags (u8)
+BIPEDAL_ALG_BYTES = 4 * (2 * 189 + 2 * 26 + 26 + 2 * 9 + 2 * 2 + 102) + 2 + 8 * (2 * 6 + 1 + 1) + 2
+BIPEDAL_METRIC = "env steps/sec (whole node), bipedal_rescue 8192 envs/GPU (BASELINE configs[3])"
+
+
+def _pmc_traffic(name: str, envs: int, precision: str, mode: str):
+    """HBM bytes per step from a committed tools/profile_round.sh summary of the same config."""
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        with open(path) as f:
+            p = json.load(f)
+        if p.get("envs") == envs and p.get("precision") == precision and p.get("mode") == mode:
+            return p.get("hbm_bytes_per_step")
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
+def _finite(x: float):
+    """JSON-safe mean: the bipedal approach term is +inf on the first step after a reset
+    (rescue_env.py:632-635), which makes a rollout's reward sum infinite."""
+    return round(x, 3) if np.isfinite(x) else None
 
 
 def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
@@ -158,22 +189,72 @@ def cpu_baseline_parkour(n_envs: int, n_steps: int, seed: int = 0) -> dict:
             "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
 
 
+def cpu_baseline_bipedal(n_envs: int, n_steps: int, seed: int = 0) -> dict:
+    """Oracle port on one host core: mjref (C, fp64) RK4 physics + numpy env logic."""
+    from mujoco_gymnasium_environments_amd import cabi
+    from mujoco_gymnasium_environments_amd.envs.bipedal import bipedal_model
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.bipedal_logic import BipedalLogic, BipedalTables
+    from oracle.mjref import RefSim
+    m = bipedal_model()
+    pk = cabi.pack_model(m)
+    L = BipedalLogic(BipedalTables(m))
+    rng = np.random.default_rng(seed)
+    acts = rng.uniform(-100, 100, (64, 26)).astype(np.float32)
+    total = 0
+    t0 = time.perf_counter()
+    for e in range(n_envs):
+        sim = RefSim(pk)
+        er = np_random(seed + e)[0]
+        s = dict(prev_rescued=-1, prev_carried=-1, prev_sz=float("nan"), fall_timer=-1)
+
+        def view():
+            s.update(qpos=sim.qpos, qvel=sim.qvel, ctrl=sim.ctrl, xpos=sim.xpos.reshape(-1, 3),
+                     xquat=sim.xquat.reshape(-1, 4), con_dist=sim.contacts()["dist"])
+
+        def reset():
+            sim.reset()
+            view()
+            L.apply_reset(s, L.t.reset_draws(er))
+            sim.step(10)
+            view()
+            L.after_reset(s)
+            L.obs(s)
+        reset()
+        for k in range(n_steps):
+            a = L.pre(s, acts[k % 64])
+            sim.step()
+            view()
+            _, _, term, trunc = L.post(s, a)
+            total += 1
+            if term or trunc:
+                reset()
+    dt = time.perf_counter() - t0
+    return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of bipedal_rescue, U(-100,100) actions, "
+                      f"oracle/mjref.c fp64 RK4 physics + oracle/bipedal_logic.py; CPU MuJoCo unavailable "
+                      f"(not installed)",
+            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default 4096; 8192 for bipedal)")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-envs", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
-    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour"])
+    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal"])
     args = ap.parse_args()
-    if args.task == "parkour":
+    if args.task != "soccer":
         args.mono = True  # one fused wave-per-env launch per step
+    if args.envs <= 0:
+        args.envs = 8192 if args.task == "bipedal" else 4096
 
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     world, rank, local = world_from_env()
@@ -194,6 +275,10 @@ def main():
         env = ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
         lim = torch.as_tensor(action_limits(), dtype=torch.float32, device=dev)
         pool = [((torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * lim).contiguous() for _ in range(16)]
+    elif args.task == "bipedal":
+        from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+        env = BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
+        pool = [((torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0).contiguous() for _ in range(16)]
     else:
         from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
         env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
@@ -229,7 +314,29 @@ def main():
     acc, elapsed = reduce_rollout(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
     value = total_steps / elapsed
-    if rank == 0 and args.task == "parkour":
+    if rank == 0 and args.task == "bipedal":
+        bytes_per_launch = BIPEDAL_ALG_BYTES * N
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        out = {
+            "metric": BIPEDAL_METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (U(-100,100) actions, Philox reset draws)",
+            "config": {"workload": "bipedal_rescue_env, 8192 envs/GPU (BASELINE configs[3])", "envs_per_gpu": N,
+                       "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
+                       "integrator": "RK4", "step_kernels": "mono", "episodes_started": int(acc[1].item()),
+                       "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "mean_reward": _finite(acc[2].item() / total_steps)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(PMC_PROFILE_BIPEDAL, N, args.precision,
+                                                                                  "mono"),
+                         "kernel": "mgx_bipedal_step = k_bipedal<float,0,GB>", "alg_bytes_per_step": bytes_per_launch,
+                         "launch_ms": round(launch_ms, 4)},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_bipedal(max(1, args.cpu_envs // 8), args.cpu_steps // 10)
+        print(json.dumps(out))
+    elif rank == 0 and args.task == "parkour":
         bytes_per_launch = PARKOUR_ALG_BYTES * N
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         out = {
@@ -241,7 +348,7 @@ def main():
                        "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
                        "substeps_per_step": 10, "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
-                       "mean_reward": round(acc[2].item() / total_steps, 3)},
+                       "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "mgx_parkour_step = k_parkour<float,0>", "alg_bytes_per_step": bytes_per_launch,
@@ -274,7 +381,7 @@ def main():
                        "autoreset": "same-step", "step_kernels": mode, "reset_banks": 0 if args.mono else args.banks,
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
-                       "mean_reward": round(acc[2].item() / total_steps, 3)},
+                       "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ("mgx_soccer_step = k_soccer_rows + k_pgs_groups + k_soccer_finish + k_soccer_fixup"

@@ -15,7 +15,8 @@ import shutil
 import sys
 
 STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_finish", "k_soccer_fixup", "k_soccer<float, 0>",
-                "k_soccer<double, 0>"]
+                "k_soccer<double, 0>", "k_bipedal<float, 0, true>", "k_bipedal<float, 0, false>",
+                "k_parkour<float, 0>"]
 
 
 def step_kernel(name):
@@ -69,6 +70,7 @@ def main(out, tag):
             res["envs"] = b["config"]["envs_per_gpu"]
             res["precision"] = b["dtype"]
             res["mode"] = b["config"].get("step_kernels", "staged")
+            res["task"] = b["config"]["workload"].split("_env")[0]
     fetch = counter_means(os.path.join(out, "pmc_fetch"), "FETCH_SIZE")
     write = counter_means(os.path.join(out, "pmc_write"), "WRITE_SIZE")
     if fetch and write:
