@@ -177,18 +177,18 @@ def dump_xml():
     out["quadruped_parkour"] = parkour.QuadrupedParkourEnv._combine_models(
         o, f"{a}/quadruped.xml", f"{a}/parkour_course.xml", f"{a}/terrain_variations.xml")
 
-    for key, path, modname, cls in [
-        ("bipedal_rescue", "bipedal_rescue_env/rescue_env.py", "ref_rescue_env", "BipedalRescueEnv"),
-        ("humanoid_dancing", "humanoid_dancing_env/dancing_env.py", "ref_dancing_env", "HumanoidDancingEnv"),
-    ]:
-        try:
-            mod = load_module(f"{REF}/{path}", modname)
-            o = object.__new__(getattr(mod, cls))
-            o.dt = getattr(o, "dt", 0.02)
-            getattr(mod, cls)._load_xml_models(o)
-            out[key] = o.xml_string
-        except Exception as e:  # noqa: BLE001 - record and continue; later rounds widen
-            print(f"[fixtures] {key}: composition failed: {e!r}")
+    bip = load_module(f"{REF}/bipedal_rescue_env/rescue_env.py", "ref_rescue_env")
+    o = object.__new__(bip.BipedalRescueEnv)
+    o.dt = 0.02
+    bip.BipedalRescueEnv._load_xml_models(o)
+    out["bipedal_rescue"] = o.xml_string
+    # the dancing composition reads constructor attributes (floor_radius, ...): run the
+    # reference constructor itself (stub mujoco) and keep the string it compiled
+    import contextlib
+    import io
+    dan = load_module(f"{REF}/humanoid_dancing_env/dancing_env.py", "ref_dancing_env")
+    with contextlib.redirect_stdout(io.StringIO()):
+        out["humanoid_dancing"] = dan.HumanoidDancingEnv(render_mode=None).xml_string
     # construction / martial arts / assembly load their on-disk assets unchanged; those files
     # are read from /root/reference by the tests that need them, never copied into the repo.
     os.makedirs(f"{HERE}/xml", exist_ok=True)
@@ -198,7 +198,7 @@ def dump_xml():
     # the package ships the composed soccer / parkour models it simulates
     pkg_assets = f"{REPO}/mujoco_gymnasium_environments_amd/assets"
     os.makedirs(pkg_assets, exist_ok=True)
-    for k in ("humanoid_soccer", "quadruped_parkour"):
+    for k in ("humanoid_soccer", "quadruped_parkour", "bipedal_rescue", "humanoid_dancing"):
         with open(f"{pkg_assets}/{k}.xml", "w") as f:
             f.write(out[k])
     return out
@@ -572,6 +572,136 @@ def bipedal_envlogic_vectors(env, n, seed=777, max_contacts=24):
     return {k: np.asarray(v) for k, v in cols.items()}
 
 
+# ------------------------------------------------------------------------------- dancing
+MOVES = ['basic_step', 'spin', 'jump', 'moonwalk', 'robot_wave', 'freeze', 'hip_hop_bounce', 'breakdance_toprock',
+         'salsa_basic', 'ballet_pirouette']   # dancing_env.py:57-68 key order
+
+
+def dancing_env():
+    import contextlib
+    import io
+    install_stubs()
+    mod = load_module(f"{REF}/humanoid_dancing_env/dancing_env.py", "ref_dancing_env2")
+    with contextlib.redirect_stdout(io.StringIO()):
+        return mod.HumanoidDancingEnv(render_mode=None)
+
+
+def _dance_state(env):
+    es = env.episode_stats
+    return dict(current_step=env.current_step, t_beat=float(env.time_since_last_beat), beat_count=env.beat_count,
+                measure=env.current_measure, disco=float(env.disco_ball_rotation),
+                spotlight=np.asarray(env.spotlight_position, dtype=np.float64).copy(),
+                combo=float(env.combo_multiplier), score=float(env.performance_score),
+                move_idx=env.current_move_idx, move_start=float(env.move_start_time),
+                hist=_pad(np.array([MOVES.index(x) for x in env.move_history[-3:]], dtype=np.float64), 3, None, -1.0),
+                hist_len=len(env.move_history), crowd=float(env.crowd_excitement), applause=float(env.applause_level),
+                stats=np.array([es['energy_used'], es['time_on_beat'], es['longest_combo'], es['crowd_rating'],
+                                es['total_score']], dtype=np.float64),
+                fall_start=getattr(env, 'fall_start_step', 0), fall_present=hasattr(env, 'fall_start_step'),
+                prev_jvel=np.asarray(env.prev_joint_vel, dtype=np.float64).copy())
+
+
+def dancing_reset_vectors(env, seeds):
+    """reset(seed) (dancing_env.py:763-831): the 20-move sequence draws and the initial pose
+    (the stub mj_step does not move the state)."""
+    rows = []
+    for s in seeds:
+        env.reset(seed=int(s))
+        rows.append(dict(qpos=env.data.qpos.copy(),
+                         moves=np.array([MOVES.index(d['move']) for d in env.dance_sequence], dtype=np.int64),
+                         durations=np.array([d['duration'] for d in env.dance_sequence])))
+    return dict(seeds=np.asarray(seeds, np.int64), qpos=np.stack([r["qpos"] for r in rows]),
+                moves=np.stack([r["moves"] for r in rows]), durations=np.stack([r["durations"] for r in rows]))
+
+
+def dancing_envlogic_vectors(env, n, seed=999, max_contacts=16):
+    """Random synthetic MjData-like states -> the reference's own step() (dancing_env.py:833-894)
+    with physics stubbed out: clip + ctrl, rhythm, spotlight, obs, reward, termination, stats,
+    crowd, move transitions and the fall_start_step attribute that survives reset."""
+    c = env.model._c
+    rng = np.random.default_rng(seed)
+    torso = env.torso_id
+    nb = c.nbody
+    cand = c.pair_geom
+    cols = {}
+
+    def put(k, v):
+        cols.setdefault(k, []).append(v)
+    env.reset(seed=0)
+    for i in range(n):
+        d = env.data
+        scen = i % 10
+        d.qpos[:] = rng.normal(scale=rng.choice([0.3, 1.5]), size=c.nq)
+        d.qvel[:] = rng.normal(scale=rng.choice([0.05, 0.3, 3.0]), size=c.nv)
+        d.xpos[:] = rng.uniform(-3, 3, (nb, 3))
+        d.xpos[torso] = [rng.normal(scale=0.2), rng.normal(scale=0.2), 1.8] if scen != 9 else \
+            [rng.uniform(-20, 20), rng.uniform(-20, 20), rng.uniform(-1, 6)]
+        q = rng.normal(size=4)
+        if scen % 3:
+            q = np.array([1.0, *rng.normal(scale=0.3, size=3)])
+        d.xquat[:] = np.tile(q / np.linalg.norm(q), (nb, 1))
+        d.subtree_com[:] = rng.uniform(-12, 12, (nb, 3))
+        ncon = int(rng.integers(0, max_contacts + 1))
+        pairs = []
+        for _ in range(ncon):
+            if rng.random() < 0.4:
+                pairs.append((int(rng.choice([0, 1])), int(rng.choice([env.right_foot_id, env.left_foot_id]))))
+            else:
+                g1, g2 = cand[int(rng.integers(0, len(cand)))]
+                pairs.append((int(g1), int(g2)))
+        d.contact = [FakeContact(g1, g2, rng.uniform(-0.05, 0.01), np.zeros(5)) for g1, g2 in pairs]
+        d.ncon = ncon
+        env.current_step = int(rng.choice([0, 1, 3599, int(rng.integers(0, 3600))]))
+        env.time_since_last_beat = float(rng.choice([rng.uniform(0, 0.5), rng.uniform(0.47, 0.5), rng.uniform(0, 0.06),
+                                                     rng.uniform(0.08, 0.12), rng.uniform(0.38, 0.42)]))
+        env.beat_count = int(rng.integers(0, 500))
+        env.current_measure = env.beat_count // 4
+        env.disco_ball_rotation = float(rng.uniform(0, 6.3))
+        env.spotlight_position = np.array([rng.normal(), rng.normal(), rng.uniform(4, 6)])
+        env.combo_multiplier = float(rng.choice([1.0, 10.0, rng.uniform(1, 10), 1.02]))
+        env.performance_score = float(rng.normal(scale=1000))
+        env.dance_sequence = [{'move': MOVES[int(rng.integers(0, 10))], 'duration': float(rng.uniform(1, 3))}
+                              for _ in range(20)]
+        env.current_move_idx = int(rng.choice([0, 19, 20, int(rng.integers(0, 21))]))
+        now = env.current_step * env.dt
+        env.move_start_time = float(now - rng.choice([rng.uniform(0, 3.5), rng.uniform(0, 0.2)]))
+        hl = int(rng.integers(0, 6))
+        env.move_history = [MOVES[int(rng.integers(0, 10))] if rng.random() < 0.7 else MOVES[k % 10] for k in range(hl)]
+        env.crowd_excitement = float(rng.choice([0.5, rng.uniform(0, 1), 0.9999, 0.0]))
+        env.applause_level = env.crowd_excitement * 100.0
+        es = env.episode_stats
+        es.update(energy_used=float(rng.choice([0.0, rng.uniform(0, 1500)])), time_on_beat=float(rng.uniform(0, 10)),
+                  longest_combo=int(rng.integers(0, 11)), crowd_rating=float(rng.uniform(0, 1)),
+                  total_score=float(rng.normal(scale=100)))
+        if rng.random() < 0.5:
+            env.fall_start_step = int(env.current_step - rng.choice([0, 119, 120, 121, int(rng.integers(0, 300))]))
+        elif hasattr(env, 'fall_start_step'):
+            delattr(env, 'fall_start_step')
+        env.prev_joint_vel = d.qvel[6:] + rng.normal(scale=rng.choice([0.01, 0.3, 3.0]), size=c.nv - 6)
+        inp = {k + "_in": v for k, v in _dance_state(env).items()}
+        inp.update(qpos=d.qpos.copy(), qvel=d.qvel.copy(), xpos=d.xpos.copy(), xquat=d.xquat.copy(),
+                   subtree_com=d.subtree_com.copy(), ncon=ncon,
+                   con_geom=_pad(np.array(pairs, dtype=np.float64).reshape(-1, 2), max_contacts, 2, -1.0),
+                   moves=np.array([MOVES.index(x['move']) for x in env.dance_sequence], dtype=np.int64),
+                   durations=np.array([x['duration'] for x in env.dance_sequence]))
+        lim = env.action_space.high
+        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim * rng.choice([1.0, 0.01, 0.1])).astype(np.float32)
+        obs, reward, term, trunc, info = env.step(action)
+        out = {k + "_out": v for k, v in _dance_state(env).items()}
+        out.update(action=action, obs=obs, reward=float(reward), reward_is_f64=isinstance(reward, np.float64),
+                   terminated=bool(term), truncated=bool(trunc), ctrl_out=d.ctrl.copy())
+        for k, v in {**inp, **out}.items():
+            put(k, v)
+    return {k: np.asarray(v) for k, v in cols.items()}
+
+
+def main_dancing():
+    install_stubs()
+    denv = dancing_env()
+    np.savez_compressed(f"{HERE}/dancing_reset.npz", **dancing_reset_vectors(denv, list(range(0, 40)) + [777]))
+    np.savez_compressed(f"{HERE}/dancing_envlogic.npz", **dancing_envlogic_vectors(denv, 600))
+
+
 def main():
     install_stubs()
     dump_xml()
@@ -584,8 +714,12 @@ def main():
     benv = bipedal_env()
     np.savez_compressed(f"{HERE}/bipedal_reset.npz", **bipedal_reset_vectors(benv, list(range(0, 40)) + [4242]))
     np.savez_compressed(f"{HERE}/bipedal_envlogic.npz", **bipedal_envlogic_vectors(benv, 600))
+    main_dancing()
     print("fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "dancing":
+        main_dancing()
+    else:
+        main()
