@@ -357,6 +357,67 @@ typedef struct mgx_bipedal_logic_io {
 int mgx_bipedal_logic_test(const mgx_model *m, const mgx_bipedal_logic_io *io, const mgx_bipedal_env *e, int n_env,
                            void *stream);
 
+/* ---- humanoid_dancing env logic fused with physics (RK4) ----------------------------- */
+/* Index tables (humanoid_dancing_env/dancing_env.py:680-720). */
+typedef struct mgx_dancing_ids {
+  int32_t torso;                     /* body id of 'torso' */
+  int32_t right_foot, left_foot;     /* geom ids (foot indicators, :1249-1266) */
+  int32_t floor, stage;              /* geom ids of 'dance_floor' / 'stage' */
+  int32_t n_act;                     /* 29 actuators written from the action */
+  int32_t max_episode_steps;         /* 3600 (dancing_env.py:42) */
+  int32_t n_range;                   /* joints i whose jnt_range normalises qpos[7 + i] (29) */
+  double jnt_lo[32], jnt_hi[32];     /* jnt_range of joint_names[i] (:1038-1050, :1169-1177) */
+} mgx_dancing_ids;
+
+/* Persistent per-env task state (device, env-major, fp64 / int32 whatever the physics
+ * precision). scal [N][18]: 0 time_since_last_beat, 1 disco_ball_rotation, 2-4
+ * spotlight_position, 5 combo_multiplier, 6 performance_score, 7 move_start_time, 8
+ * crowd_excitement, 9 applause_level, 10-14 episode_stats (energy_used, time_on_beat,
+ * longest_combo, crowd_rating, total_score), 15-17 torso xpos of the last forward pass.
+ * ints [N][8]: 0 current_step, 1 beat_count, 2 current_measure, 3 current_move_idx,
+ * 4 len(move_history), 5 fall_start_step, 6 fall_start_step present (survives reset), 7 unused.
+ * Spotlight, disco rotation and fall_start_step are never reset (as in the reference). */
+typedef struct mgx_dancing_env {
+  double *scal;         /* [N][18] */
+  int32_t *ints;        /* [N][8] */
+  int32_t *hist;        /* [N][3] the last <= 3 entries of move_history (move indices, -1 pad) */
+  int32_t *moves;       /* [N][20] dance_sequence move indices (dancing_env.py:57-68 order) */
+  double *durations;    /* [N][20] dance_sequence durations */
+  double *prev_jvel;    /* [N][nv - 6] prev_joint_vel */
+  int32_t *episode;     /* [N] episodes started (keys device reset draws); nullable with host draws */
+  void *rollout;        /* [N][4] reward, terminated, truncated, env steps (nullable) */
+} mgx_dancing_env;
+
+int mgx_dancing_configure(mgx_model *m, const mgx_dancing_ids *ids);
+
+/* One env step for N envs (dancing_env.py:833-894): clip to +-200, ctrl, rhythm, spotlight,
+ * one RK4 mj_step, observation [N][94] float32, reward [N] float64, terminated / truncated,
+ * stats, crowd, move transition; autoreset as mgx_parkour_step. */
+int mgx_dancing_step(const mgx_model *m, const mgx_state *s, const mgx_dancing_env *e, const float *action,
+                     float *obs, double *reward, uint8_t *terminated, uint8_t *truncated, float *final_obs,
+                     int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t *env_mask,
+                     void *stream);
+
+/* reset() for masked envs (dancing_env.py:763-831): `draws` [N][40] real = (move index,
+ * duration) x 20 in reference order (NULL = device Philox); initial pose, 10 settle steps, obs. */
+int mgx_dancing_reset(const mgx_model *m, const mgx_state *s, const mgx_dancing_env *e, const void *draws,
+                      float *obs, uint64_t seed, int env_offset, int n_env, const uint8_t *env_mask, void *stream);
+
+/* Test hook: dancing env logic only on caller-supplied frames and contact lists. */
+typedef struct mgx_dancing_logic_io {
+  const void *qpos, *qvel, *xpos, *xquat, *subtree_com;  /* [N][nq] [N][nv] [N][nbody][3|4|3] */
+  const int32_t *ncon, *con_geom;                        /* [N], [N][max_contacts][2] */
+  int32_t max_contacts;
+  int32_t pad0;
+  void *ctrl;                                            /* out [N][nu] */
+  const float *action;                                   /* [N][29] */
+  float *obs;                                            /* [N][94] */
+  double *reward;
+  uint8_t *terminated, *truncated;
+} mgx_dancing_logic_io;
+int mgx_dancing_logic_test(const mgx_model *m, const mgx_dancing_logic_io *io, const mgx_dancing_env *e, int n_env,
+                           void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,8 @@ Public surface:
   envs.QuadrupedParkourEnv   drop-in gymnasium-style single env
   envs.BipedalVectorEnv      batched bipedal_rescue (RK4, rows in global scratch)
   envs.BipedalRescueEnv      drop-in gymnasium-style single env
+  envs.DancingVectorEnv      batched humanoid_dancing (RK4)
+  envs.HumanoidDancingEnv    drop-in gymnasium-style single env
 The compute path is libmgx.so (HIP, gfx950); there is no CPU fallback.
 """
 __version__ = "0.1.0"
@@ -17,7 +19,8 @@ __version__ = "0.1.0"
 
 def __getattr__(name):  # lazy: importing the package must not require a GPU
     if name in ("HumanoidSoccerEnv", "SoccerVectorEnv", "register_envs", "ParkourVectorEnv", "QuadrupedParkourEnv",
-                "BipedalVectorEnv", "BipedalRescueEnv"):
+                "BipedalVectorEnv", "BipedalRescueEnv",
+                "DancingVectorEnv", "HumanoidDancingEnv"):
         from . import envs
         return getattr(envs, name)
     raise AttributeError(name)

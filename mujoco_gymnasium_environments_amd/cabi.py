@@ -129,6 +129,24 @@ class MgxBipedalLogicIO(C.Structure):
                 ("terminated", C.c_void_p), ("truncated", C.c_void_p), ("upright", C.c_void_p)]
 
 
+class MgxDancingIds(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ["torso", "right_foot", "left_foot", "floor", "stage", "n_act",
+                                         "max_episode_steps", "n_range"]] + \
+               [("jnt_lo", C.c_double * 32), ("jnt_hi", C.c_double * 32)]
+
+
+class MgxDancingEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ["scal", "ints", "hist", "moves", "durations", "prev_jvel", "episode", "rollout"]]
+
+
+class MgxDancingLogicIO(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("xpos", C.c_void_p), ("xquat", C.c_void_p),
+                ("subtree_com", C.c_void_p), ("ncon", C.c_void_p), ("con_geom", C.c_void_p),
+                ("max_contacts", C.c_int32), ("pad0", C.c_int32), ("ctrl", C.c_void_p), ("action", C.c_void_p),
+                ("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p), ("truncated", C.c_void_p)]
+
+
 class MgxSoccerIds(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ["torso", "ball", "goalkeeper", "ball_geom", "right_foot", "left_foot", "field_geom",

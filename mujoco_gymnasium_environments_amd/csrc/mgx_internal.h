@@ -1,6 +1,6 @@
 // mgx_internal.h — host-side definitions shared by the translation units of libmgx.so
 // (mgx_api.hip: model, physics and soccer; mgx_step.hip: generic step; mgx_parkour.hip:
-// quadruped_parkour; mgx_bipedal.hip: bipedal_rescue).
+// quadruped_parkour; mgx_bipedal.hip: bipedal_rescue; mgx_dancing.hip: humanoid_dancing).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -8,6 +8,7 @@
 
 #include "../../include/mgx.h"
 #include "mgx_bipedal.h"
+#include "mgx_dancing.h"
 #include "mgx_parkour.h"
 #include "mgx_staged.h"
 
@@ -27,6 +28,8 @@ struct mgx_model {
   mgx::ParkourIds<double> pkd;
   bool bipedal_ok = false;
   mgx::BipedalIds bp;
+  bool dancing_ok = false;
+  mgx::DancingIds dn;
   int npair;
   bool staged_ok = false;  // the staged soccer pipeline supports this model's capacities
 };

@@ -1,5 +1,7 @@
 """Task environments. humanoid_soccer is the headline task (BASELINE.json); quadruped_parkour is
-the low-DoF bring-up task (BASELINE configs 1-2); bipedal_rescue is the RK4 scaling task (config 4)."""
+the low-DoF bring-up task (BASELINE configs 1-2); bipedal_rescue is the RK4 scaling task (config 4);
+humanoid_dancing is a config-5 task (RK4, cylinder floor)."""
 from .bipedal import BipedalRescueEnv, BipedalVectorEnv  # noqa: F401
+from .dancing import DancingVectorEnv, HumanoidDancingEnv  # noqa: F401
 from .parkour import ParkourVectorEnv, QuadrupedParkourEnv  # noqa: F401
 from .soccer import HumanoidSoccerEnv, SoccerVectorEnv, register_envs  # noqa: F401

@@ -15,9 +15,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = ["mgx_api.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip"]
+SOURCES = ["mgx_api.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip"]
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
-           "mgx_bipedal.h", "mgx_internal.h"]
+           "mgx_bipedal.h", "mgx_dancing.h", "mgx_internal.h"]
 
 MGX_OK = 0
 MGX_F32 = 0
@@ -94,6 +94,13 @@ _SIGS = {
     "mgx_bipedal_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxBipedalEnv), _VP, _VP, C.c_uint64,
                            C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_bipedal_logic_test": ([_VP, C.POINTER(cabi.MgxBipedalLogicIO), C.POINTER(cabi.MgxBipedalEnv), C.c_int, _VP],
+                               C.c_int),
+    "mgx_dancing_configure": ([_VP, C.POINTER(cabi.MgxDancingIds)], C.c_int),
+    "mgx_dancing_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxDancingEnv), _VP, _VP, _VP, _VP, _VP,
+                          _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_dancing_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxDancingEnv), _VP, _VP, C.c_uint64,
+                           C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_dancing_logic_test": ([_VP, C.POINTER(cabi.MgxDancingLogicIO), C.POINTER(cabi.MgxDancingEnv), C.c_int, _VP],
                                C.c_int),
 }
 EXPORTS = tuple(_SIGS)

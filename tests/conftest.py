@@ -53,3 +53,15 @@ def bipedal_model():
 def bipedal_packed(bipedal_model):
     from mujoco_gymnasium_environments_amd import cabi
     return cabi.pack_model(bipedal_model)
+
+
+@pytest.fixture(scope="session")
+def dancing_model():
+    from mujoco_gymnasium_environments_amd.envs.dancing import dancing_model as load
+    return load()
+
+
+@pytest.fixture(scope="session")
+def dancing_packed(dancing_model):
+    from mujoco_gymnasium_environments_amd import cabi
+    return cabi.pack_model(dancing_model)

@@ -18,12 +18,16 @@ pytestmark = pytest.mark.gpu
 N = 8
 
 
-@pytest.fixture(scope="module", params=["soccer", "parkour", "bipedal"])
-def case(request, soccer_model, soccer_packed, parkour_model, parkour_packed, bipedal_model, bipedal_packed):
+@pytest.fixture(scope="module", params=["soccer", "parkour", "bipedal", "dancing"])
+def case(request, soccer_model, soccer_packed, parkour_model, parkour_packed, bipedal_model, bipedal_packed,
+         dancing_model, dancing_packed):
     """(model, packed model, oracle states): humanoid_soccer (dt 0.02, 5 primitive pair types) and
     quadruped_parkour (dt 0.001, plane pairs, ~30 contacts / ~128 rows when grounded)."""
     if request.param == "soccer":
         return soccer_model, soccer_packed, oracle_states(soccer_packed, N, seed=7)
+    if request.param == "dancing":  # RK4, rows in LDS, cylinder floor / stage
+        return dancing_model, dancing_packed, oracle_states(dancing_packed, N, seed=7, max_steps=40,
+                                                           action_scale=50.0)
     if request.param == "bipedal":  # RK4, rows in global scratch, cylinder pairs
         return bipedal_model, bipedal_packed, oracle_states(bipedal_packed, N, seed=7, max_steps=40,
                                                            action_scale=30.0)
@@ -119,15 +123,16 @@ def test_one_step(case, prec):
             f"qvel env {i}"
 
 
-@pytest.mark.parametrize("task,nsub,nstep", [("soccer", 1, 200), ("parkour", 10, 100), ("bipedal", 1, 60)])
+@pytest.mark.parametrize("task,nsub,nstep", [("soccer", 1, 200), ("parkour", 10, 100), ("bipedal", 1, 60),
+                                             ("dancing", 1, 100)])
 def test_rollout_f64_zero_action(task, nsub, nstep, soccer_model, soccer_packed, parkour_model, parkour_packed,
-                                 bipedal_model, bipedal_packed):
+                                 bipedal_model, bipedal_packed, dancing_model, dancing_packed):
     """Non-chaotic settle from qpos0 (zero ctrl): trajectories agree over 200 soccer steps /
     1000 parkour substeps (100 env steps of 10 mj_step's each, parkour_env.py:367-368)."""
     import torch
     from oracle.mjref import RefSim
     model, packed = {"soccer": (soccer_model, soccer_packed), "parkour": (parkour_model, parkour_packed),
-                     "bipedal": (bipedal_model, bipedal_packed)}[task]
+                     "bipedal": (bipedal_model, bipedal_packed), "dancing": (dancing_model, dancing_packed)}[task]
     b = _batch(model, "f64", n=2)
     o = RefSim(packed)
     worst = 0.0

@@ -18,9 +18,8 @@ KEYS = ["current_step", "t_beat", "beat_count", "measure", "disco", "spotlight",
 
 
 @pytest.fixture(scope="module")
-def model():
-    from mujoco_gymnasium_environments_amd.envs.dancing import dancing_model
-    return dancing_model()
+def model(dancing_model):
+    return dancing_model
 
 
 @pytest.fixture(scope="module")
