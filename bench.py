@@ -17,6 +17,11 @@ metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
 step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obstacle motors,
 obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
 
+--task mixed benchmarks BASELINE configs[4] over the tasks this build simulates (soccer,
+parkour, bipedal, dancing; the three Newton-solver tasks are not built yet): 1024 envs per task
+on one GPU, each task's fused step on its own HIP stream so the ragged models overlap on the
+chip; one step = one env step of every task; value = all tasks' env steps / wall time.
+
 --task bipedal benchmarks BASELINE configs[3] (bipedal_rescue, 8192 envs/GPU by default): one
 step = BipedalVectorEnv.step = mgx_bipedal_step (clip, float32 energy, one RK4 mj_step with the
 constraint rows in per-env global scratch, victim interactions, obs/reward/termination/stats,
@@ -56,6 +61,11 @@ PARKOUR_METRIC = "env steps/sec (whole node), quadruped_parkour 4096 envs/GPU (B
 # (fp64), flags (u8)
 BIPEDAL_ALG_BYTES = 4 * (2 * 189 + 2 * 26 + 26 + 2 * 9 + 2 * 2 + 102) + 2 + 8 * (2 * 6 + 1 + 1) + 2
 BIPEDAL_METRIC = "env steps/sec (whole node), bipedal_rescue 8192 envs/GPU (BASELINE configs[3])"
+# dancing: r/w qpos/qvel/qacc_warmstart 29 each and ctrl 29 (fp32), action 29, r/w 18 fp64 + 8
+# int32 task scalars + 3 hist, prev_jvel 23 (fp64), read the 20-move sequence (int32 + fp64),
+# obs 94, reward, flags
+DANCING_ALG_BYTES = 4 * (2 * 87 + 2 * 29 + 29 + 2 * 8 + 2 * 3 + 20 + 94) + 8 * (2 * 18 + 2 * 23 + 20 + 1) + 2
+MIXED_METRIC = "env steps/sec (whole node), all tasks mixed, 1024 envs each on 1 MI355X (BASELINE configs[4])"
 
 
 def _pmc_traffic(name: str, envs: int, precision: str, mode: str):
@@ -237,6 +247,96 @@ def cpu_baseline_bipedal(n_envs: int, n_steps: int, seed: int = 0) -> dict:
             "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
 
 
+def bench_mixed(args, dev, world, rank, dist):
+    """BASELINE configs[4]: every built task, N envs each, one HIP stream per task."""
+    from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout
+    from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+    from mujoco_gymnasium_environments_amd.envs.dancing import DancingVectorEnv
+    from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv, action_limits
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    N = args.envs
+    off = env_offset(rank, N)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000 + rank)
+    plim = torch.as_tensor(action_limits(), dtype=torch.float32, device=dev)
+    tasks = {
+        "humanoid_soccer": (SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=11, env_offset=off,
+                                            banks=args.banks), lambda: torch.rand(N, 33, device=dev, generator=g) * 300 - 150,
+                            ALG_BYTES_PER_ENV_STEP),
+        "quadruped_parkour": (ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=12, env_offset=off),
+                              lambda: (torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim, PARKOUR_ALG_BYTES),
+        "bipedal_rescue": (BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=13, env_offset=off),
+                           lambda: (torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0, BIPEDAL_ALG_BYTES),
+        "humanoid_dancing": (DancingVectorEnv(N, device=str(dev), precision=args.precision, seed=14, env_offset=off),
+                             lambda: (torch.rand(N, 29, device=dev, generator=g) * 2 - 1) * 200.0, DANCING_ALG_BYTES),
+    }
+    streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
+    pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
+    for k, (env, _, _) in tasks.items():
+        env.reset()
+    torch.cuda.synchronize(dev)
+
+    def one_step(i, ev=None):
+        for k, (env, _, _) in tasks.items():
+            with torch.cuda.stream(streams[k]):
+                if ev is not None:
+                    ev[k][0].record(streams[k])
+                env.step(pools[k][i % 8], stream=streams[k])
+                if ev is not None:
+                    ev[k][1].record(streams[k])
+    for i in range(args.warmup):
+        one_step(i)
+    torch.cuda.synchronize(dev)
+    for env, _, _ in tasks.values():
+        env.rollout.zero_()
+    evs = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in tasks}
+           for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(i, evs[i])
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in tasks}
+    acc = torch.zeros(6, dtype=torch.float64, device=dev)
+    for env, _, _ in tasks.values():
+        ro = env.rollout.double().sum(0)
+        acc[0] += ro[3]
+        acc[2] += ro[0] if torch.isfinite(ro[0]) else 0.0
+        acc[3] += ro[1]
+        acc[4] += ro[2]
+        acc[5] += float(env.batch.warning.sum().item())
+    acc, elapsed = reduce_rollout(acc, elapsed)
+    total = acc[0].item()
+    if rank == 0:
+        dom = max(per, key=per.get)
+        bytes_dom = tasks[dom][2] * N
+        achieved = bytes_dom / (per[dom] * 1e-3) / 1e9
+        out = {
+            "metric": MIXED_METRIC, "value": round(total / elapsed, 1), "unit": "env_steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (uniform actions within each task's action_space, Philox reset draws)",
+            "config": {"workload": "all tasks mixed, 1024 envs each on 1 GPU (BASELINE configs[4])",
+                       "tasks": list(tasks), "tasks_missing": ["humanoid_construction", "humanoid_martial_arts",
+                                                               "robotic_arm_assembly"],
+                       "envs_per_task": N, "global_batch": N * len(tasks) * world,
+                       "parallelism": f"dp{world} (env shards), one HIP stream per task",
+                       "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},
+                       "bad_state_resets": int(acc[5].item())},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": f"{dom} step (dominant stream)",
+                         "alg_bytes_per_step": bytes_dom, "launch_ms": round(per[dom], 4)},
+        }
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,12 +349,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
-    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal"])
+    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed"])
     args = ap.parse_args()
     if args.task != "soccer":
         args.mono = True  # one fused wave-per-env launch per step
     if args.envs <= 0:
-        args.envs = 8192 if args.task == "bipedal" else 4096
+        args.envs = {"bipedal": 8192, "mixed": 1024}.get(args.task, 4096)
 
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     world, rank, local = world_from_env()
@@ -268,6 +368,8 @@ def main():
     torch.cuda.set_device(dev)
 
     N = args.envs
+    if args.task == "mixed":
+        return bench_mixed(args, dev, world, rank, dist)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     if args.task == "parkour":

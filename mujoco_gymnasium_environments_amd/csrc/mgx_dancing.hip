@@ -4,6 +4,7 @@
 // (mgx_step.hip): a dancing env step is clip + rhythm + spotlight -> one RK4 mj_step (four
 // forward passes, rows in LDS) -> observation / reward / termination / stats / crowd / move
 // transition, with same-step autoreset (10 settle steps), all in one launch.
+#define MGX_DANCE_TRACE_TU 1
 #include "mgx_internal.h"
 
 using namespace mgx;
@@ -27,10 +28,8 @@ __device__ __forceinline__ void dancing_reset_philox(const DevModel<T>& m, Env<T
   int E = de.episode[env];
   dancing_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)E, e.vec3);
   wsync();
-  T d[2 * MGX_DANCE_SEQ];
-  for (int j = 0; j < 2 * MGX_DANCE_SEQ; j++) d[j] = e.vec3[j];
-  wsync();
-  int warn = dancing_reset_body<T, true>(m, e, ids, d, de, env, obs);
+  // the reset body consumes the draws (LDS) before its physics overwrites the vec regions
+  int warn = dancing_reset_body<T, true>(m, e, ids, e.vec3, de, env, obs);
   store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
               (T*)s.time, env);
   if (l == 0) {
@@ -59,11 +58,13 @@ __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, m
       dancing_reset_philox<T, GB>(m, e, ids, s, de, obs, seed, env_offset, env);
       return;
     }
+    DTRACE(0, 1);
     load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    T d[2 * MGX_DANCE_SEQ];
-    for (int j = 0; j < 2 * MGX_DANCE_SEQ; j++) d[j] = draws[2 * MGX_DANCE_SEQ * (size_t)env + j];
-    int warn = dancing_reset_body<T, true>(m, e, ids, d, de, env, obs);
+    DTRACE(0, 2);
+    int warn = dancing_reset_body<T, true>(m, e, ids, draws + 2 * MGX_DANCE_SEQ * (size_t)env, de, env, obs);
+    DTRACE(0, 3);
     store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+    DTRACE(0, 4);
     if (l == 0) {
       if (s.warning) s.warning[env] += warn;
       if (de.episode) de.episode[env] += 1;
@@ -150,6 +151,12 @@ void launch(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const 
 }  // namespace
 
 extern "C" {
+
+int mgx_debug_dancing_trace(void* host_pinned) {
+  int* p = (int*)host_pinned;
+  MGX_HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dance_trace), &p, sizeof(p)));
+  return MGX_OK;
+}
 
 int mgx_dancing_configure(mgx_model* m, const mgx_dancing_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");

@@ -184,7 +184,8 @@ class BipedalVectorEnv:
         return self.obs, self.reward, self.terminated, self.truncated, self.info()
 
     def info(self) -> Dict[str, Any]:
-        """Device-tensor views of the reference's info dict (rescue_env.py:447-456)."""
+        """Device-tensor views of the reference's info dict (rescue_env.py:447-456); views only, so
+        the step path launches no extra kernels."""
         return {
             'victims_rescued': self.victims_rescued,
             'distance_traveled': self.distance,
@@ -193,8 +194,8 @@ class BipedalVectorEnv:
             'falls': self.falls,
             'collisions': self.collisions,
             'robot_position': self.prev_robot_pos,
-            'victims_remaining': 5 - _popcount5(self.rescued),
-            'victims_carried': _popcount5(self.carried),
+            'victims_rescued_mask': self.rescued,   # victims_remaining = 5 - popcount (views only)
+            'victims_carried_mask': self.carried,
             'energy_remaining': self.energy,
             'final_observation': self.final_obs,
             'episode': self.episode,

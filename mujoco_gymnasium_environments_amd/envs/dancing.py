@@ -168,7 +168,7 @@ class DancingVectorEnv:
     def info(self) -> Dict[str, Any]:
         """Device-tensor views of the reference's info dict (dancing_env.py:868-878)."""
         return {
-            'beat_phase': self.scal[:, 0] / BEAT,
+            'time_since_last_beat': self.scal[:, 0],   # beat_phase = / 0.5 (views only)
             'combo_multiplier': self.scal[:, 5],
             'crowd_excitement': self.scal[:, 8],
             'performance_score': self.scal[:, 6],

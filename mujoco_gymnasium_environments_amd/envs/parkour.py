@@ -154,20 +154,28 @@ class ParkourVectorEnv:
         return self.obs, self.reward, self.terminated, self.truncated, self.info()
 
     def info(self) -> Dict[str, Any]:
-        """Device-tensor views of the reference's info dict (parkour_env.py:797-815)."""
-        x = self.last_position[:, 0].double()
-        completion = ((x - START_POS[0]) / (FINISH_POS[0] - START_POS[0])).clamp(0.0, 1.0)
+        """Device-tensor views of the reference's info dict (parkour_env.py:797-815). Views only
+        (no kernels on the step path): ``reached_mask`` holds checkpoints_reached as a bitmask
+        (``checkpoints_reached()`` counts it) and ``last_position`` the torso position
+        course_completion derives from (``course_completion()``)."""
         return {
             'step_count': self.step_count,
             'episode_reward': self.episode_reward,
             'max_forward_progress': self.max_progress,
-            'checkpoints_reached': _popcount(self.reached),
+            'reached_mask': self.reached,
             'fall_count': self.fall_count,
-            'course_completion': completion,
+            'last_position': self.last_position,
             'final_observation': self.final_obs,
             'episode': self.episode,
             'bad_state_resets': self.batch.warning,
         }
+
+    def checkpoints_reached(self) -> torch.Tensor:
+        return _popcount(self.reached)
+
+    def course_completion(self) -> torch.Tensor:
+        x = self.last_position[:, 0].double()
+        return ((x - START_POS[0]) / (FINISH_POS[0] - START_POS[0])).clamp(0.0, 1.0)
 
     def close(self):
         pass
