@@ -1199,13 +1199,156 @@ static void constraint_force_from_jar(ref_data *d, const double *jar) {
   for (int r = 0; r < d->nefc[0]; r++) d->efc_force[r] = jar[r] < 0 ? -d->efc_D[r] * jar[r] : 0;
 }
 
-/* mj_fwdConstraint with warmstart + mj_solPGS [ext] */
+/* ---- mj_solNewton [ext]: the primal problem over accelerations a,
+ *   minimise  0.5 (a - a0)' M (a - a0) + sum_r s_r(J_r a - aref_r),
+ *   s_r(x) = 0.5 D_r x^2 for x < 0 (contacts, pyramid rows and limits are one-sided), D = 1/R,
+ * whose minimiser is unique (M and D positive). Each iteration: H = M + J_A' D_A J_A over the
+ * active rows, dense Cholesky, p = -H^-1 g, then the exact line search on the convex
+ * piecewise-quadratic f(alpha) (safeguarded Newton on the monotone piecewise-linear f').
+ * Warmstart from qacc_warmstart when its cost is below qacc_smooth's; stop on scaled
+ * improvement or gradient below tolerance, or after `iterations`. The converged minimiser is
+ * what any exact solver returns, so this restatement pins the device Newton solver. */
+static double newton_cost(const mgx_model_desc *m, ref_data *d, const double *a, const double *M, double *x,
+                          double *grad) {
+  int nv = m->nv, ne = d->nefc[0];
+  double c = 0;
+  for (int i = 0; i < nv; i++) {
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += M[i * nv + k] * (a[k] - d->qacc_smooth[k]);
+    if (grad) grad[i] = s;
+    c += 0.5 * (a[i] - d->qacc_smooth[i]) * s;
+  }
+  for (int r = 0; r < ne; r++) {
+    const double *J = d->efc_J + (size_t)r * nv;
+    double s = -d->efc_aref[r];
+    for (int k = 0; k < nv; k++) s += J[k] * a[k];
+    x[r] = s;
+    if (s < 0) {
+      double Dr = 1 / d->efc_R[r];
+      c += 0.5 * Dr * s * s;
+      if (grad) for (int k = 0; k < nv; k++) grad[k] += Dr * s * J[k];
+    }
+  }
+  return c;
+}
+
+static void newton_solve(const mgx_model_desc *m, ref_data *d) {
+  int nv = m->nv, ne = d->nefc[0];
+  double *M = malloc(sizeof(double) * (3 * nv * nv + 6 * nv + 3 * ne));
+  double *H = M + nv * nv, *a = H + nv * nv, *g = a + nv, *p = g + nv, *Mp = p + nv, *tmp = Mp + nv;
+  double *x = tmp + 2 * nv, *jp = x + ne, *xt = jp + ne;
+  (void)xt;
+  /* dense M from the tree-sparse qM */
+  memset(M, 0, sizeof(double) * nv * nv);
+  for (int i = 0; i < nv; i++) {
+    int adr = m->dof_Madr[i], t = 0;
+    for (int j = i; j >= 0; j = m->dof_parentid[j], t++) {
+      M[i * nv + j] = d->qM[adr + t];
+      M[j * nv + i] = d->qM[adr + t];
+    }
+  }
+  double scale = 1 / (m->meaninertia * (nv > 1 ? nv : 1));
+  /* warmstart */
+  double c0 = newton_cost(m, d, d->qacc_smooth, M, x, NULL);
+  double cw = newton_cost(m, d, d->qacc_warmstart, M, x, NULL);
+  memcpy(a, cw < c0 ? d->qacc_warmstart : d->qacc_smooth, sizeof(double) * nv);
+  double cost = newton_cost(m, d, a, M, x, g);
+  int iter = 0;
+  while (iter < m->iterations) {
+    double gn = 0;
+    for (int k = 0; k < nv; k++) gn += g[k] * g[k];
+    if (scale * sqrt(gn) < m->tolerance) break;
+    /* H = M + J_A' D_A J_A, Cholesky (lower, in place) */
+    memcpy(H, M, sizeof(double) * nv * nv);
+    for (int r = 0; r < ne; r++) {
+      if (x[r] >= 0) continue;
+      const double *J = d->efc_J + (size_t)r * nv;
+      double Dr = 1 / d->efc_R[r];
+      for (int i = 0; i < nv; i++) {
+        if (J[i] == 0) continue;
+        for (int k = 0; k <= i; k++) H[i * nv + k] += Dr * J[i] * J[k];
+      }
+    }
+    for (int k = 0; k < nv; k++) {
+      double s = H[k * nv + k];
+      for (int j = 0; j < k; j++) s -= H[k * nv + j] * H[k * nv + j];
+      s = sqrt(s > MINVAL ? s : MINVAL);
+      H[k * nv + k] = s;
+      for (int i = k + 1; i < nv; i++) {
+        double t = H[i * nv + k];
+        for (int j = 0; j < k; j++) t -= H[i * nv + j] * H[k * nv + j];
+        H[i * nv + k] = t / s;
+      }
+    }
+    for (int i = 0; i < nv; i++) { /* L y = -g */
+      double s = -g[i];
+      for (int j = 0; j < i; j++) s -= H[i * nv + j] * tmp[j];
+      tmp[i] = s / H[i * nv + i];
+    }
+    for (int i = nv - 1; i >= 0; i--) { /* L' p = y */
+      double s = tmp[i];
+      for (int j = i + 1; j < nv; j++) s -= H[j * nv + i] * p[j];
+      p[i] = s / H[i * nv + i];
+    }
+    /* exact line search: f'(al) = (a-a0)'Mp + al p'Mp + sum_{x+al jp<0} D (x + al jp) jp */
+    double g0 = 0, pMp = 0;
+    for (int i = 0; i < nv; i++) {
+      double s = 0;
+      for (int k = 0; k < nv; k++) s += M[i * nv + k] * p[k];
+      Mp[i] = s;
+      g0 += (a[i] - d->qacc_smooth[i]) * s;
+      pMp += p[i] * s;
+    }
+    for (int r = 0; r < ne; r++) {
+      const double *J = d->efc_J + (size_t)r * nv;
+      double s = 0;
+      for (int k = 0; k < nv; k++) s += J[k] * p[k];
+      jp[r] = s;
+    }
+    double al = 1, lo = 0, hi = 1e300;
+    for (int ls = 0; ls < 50; ls++) {
+      double d1 = g0 + al * pMp, d2 = pMp;
+      for (int r = 0; r < ne; r++) {
+        double xr = x[r] + al * jp[r];
+        if (xr < 0) {
+          double Dr = 1 / d->efc_R[r];
+          d1 += Dr * xr * jp[r];
+          d2 += Dr * jp[r] * jp[r];
+        }
+      }
+      if (d1 < 0) lo = al; else hi = al;
+      double nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
+      if (!(nxt > lo && nxt < hi)) nxt = hi < 1e300 ? 0.5 * (lo + hi) : 2 * al;
+      if (fabs(nxt - al) <= 1e-15 * (1 + fabs(al))) { al = nxt; break; }
+      al = nxt;
+    }
+    for (int k = 0; k < nv; k++) a[k] += al * p[k];
+    double cnew = newton_cost(m, d, a, M, x, g);
+    double improvement = scale * (cost - cnew);
+    cost = cnew;
+    iter++;
+    if (improvement < m->tolerance) break;
+  }
+  d->solver_niter[0] = iter;
+  memcpy(d->qacc, a, sizeof(double) * nv);
+  for (int r = 0; r < ne; r++) d->efc_force[r] = x[r] < 0 ? -x[r] / d->efc_R[r] : 0;
+  memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+  for (int r = 0; r < ne; r++)
+    for (int k = 0; k < nv; k++) d->qfrc_constraint[k] += d->efc_J[(size_t)r * nv + k] * d->efc_force[r];
+  free(M);
+}
+
+/* mj_fwdConstraint with warmstart + mj_solPGS (or mj_solNewton) [ext] */
 static void fwd_constraint(const mgx_model_desc *m, ref_data *d) {
   int nv = m->nv, ne = d->nefc[0];
   if (!ne) {
     memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
     memset(d->qfrc_constraint, 0, sizeof(double) * nv);
     d->solver_niter[0] = 0;
+    return;
+  }
+  if (m->solver == 2) {
+    newton_solve(m, d);
     return;
   }
   double *jar = d->scratch, *ARf = jar + ne;
