@@ -376,6 +376,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.cdof = take(6 * nv); L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon);
   L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged ? 1 : max_nefc);
   L.efc_blk = take(staged ? 1 : 2 * max_nefc);
+  L.hess = (!staged && d->solver == 2) ? take(nv * nv) : 0;
   // union: phase A (kinematics .. collision) arrays, then B rows on top (all rows for the
   // monolithic kernel, one chunk of rows for the staged row builder)
   int u0 = p;
@@ -641,8 +642,8 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   if (!d || !out) return fail(MGX_E_ARG, "null argument");
   if (precision != MGX_F32 && precision != MGX_F64) return fail(MGX_E_ARG, "precision must be MGX_F32 or MGX_F64");
   if (d->nv > MGX_MAX_NV) return fail(MGX_E_CAPACITY, "nv > 64 not supported by the wave-per-env kernel");
-  if (d->nbody > 4096 || d->solver != 0 || (d->integrator != 0 && d->integrator != 1))
-    return fail(MGX_E_UNSUPPORTED, "this build implements PGS with Euler or RK4 (solver=PGS)");
+  if (d->nbody > 4096 || (d->solver != 0 && d->solver != 2) || (d->integrator != 0 && d->integrator != 1))
+    return fail(MGX_E_UNSUPPORTED, "this build implements PGS or Newton with Euler or RK4");
   for (int p = 0; p < d->npair; p++)
     if (d->pair_condim[p] != 1 && d->pair_condim[p] != 3) return fail(MGX_E_UNSUPPORTED, "condim must be 1 or 3");
   mgx_model* m = new mgx_model();
@@ -666,7 +667,7 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024) m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false, true);
   // the staged soccer pipeline (register-ring solver) handles Euler models up to 192 rows
-  m->staged_ok = d->integrator == 0 && max_nefc <= 64 * MGX_EFC_SLOTS;
+  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS;
   m->Ls = make_layout(d, rb, max_ncon, m->staged_ok ? max_nefc : 4, 128, true);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;

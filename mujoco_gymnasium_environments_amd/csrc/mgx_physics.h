@@ -28,6 +28,7 @@ struct Env {
   T *Bm;
   int Bs;
   T *rk;  // RK4: X[0] positions [nq] then the dX velocity vector [nv]
+  T *hess;  // Newton: nv x nv Hessian / its Cholesky factor (row-major, lower)
   int *con_geom, *con_pair, *act_list, *efc_type, *efc_id, *con_efcadr;
   int ncon, nefc, niter, overflow;
   // dof-lane registers
@@ -53,6 +54,7 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   if constexpr (GB) e.Bm = gB;
   else e.Bm = R + L.Bmat;
   e.rk = R + L.rk;
+  e.hess = R + L.hess;
   int* I = reinterpret_cast<int*>(R + L.reals);
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
   e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id; e.con_efcadr = I + L.con_efcadr;
@@ -892,6 +894,180 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
   wsync();
 }
 
+// ---------------------------------------------------------------- constraint solver (Newton)
+// mj_solNewton [ext] (restated in oracle/mjref.c newton_solve), in the whitened coordinates of
+// the PGS path: u = D^1/2 L (qacc - qacc_smooth), so 0.5 (a-a0)'M(a-a0) = 0.5 |u|^2 and
+// J_r qacc - aref_r = B_r.u + b_r. Cost 0.5|u|^2 + sum_{x_r<0} 0.5 D_r x_r^2 (D = 1/R; limit and
+// pyramid-edge rows are one-sided). Per iteration: gradient g = u + sum_{x<0} D x B_r (lane =
+// dof); Hessian H = I + sum_{x<0} D B_r B_r' (row-major nv x nv in LDS, built lane = column);
+// in-place Cholesky (lane = column, one wave barrier per column); p = -H^-1 g by two triangular
+// sweeps on readlane; the exact line search along p on the convex piecewise-quadratic cost
+// (safeguarded Newton on its piecewise-linear derivative, as the oracle); MuJoCo's stop rules
+// (scaled dof-space gradient, scaled improvement). Row scalars: q[0] b, q[1] x (efc_force at
+// exit), q[2] R, q[3] B_r.p, q[4] D.
+template <typename T>
+__device__ __forceinline__ T usum(T x) { return readlane(wave_sum(x), 0); }
+
+template <typename T>
+__device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
+  const int l = lane_id();
+  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+  const int nv = m.nv;
+  const bool dl = l < nv;
+  const int lc = dl ? l : 0;
+  T sqrtD = dl ? sqrt(e.qLD[m.dof_Madr[l]]) : (T)0;
+  if (ne == 0) {
+    e.qacc = e.qacc_smooth;
+    e.qfrc_constraint = 0;
+    e.niter = 0;
+    return;
+  }
+  T qv = dl ? e.qvel[l] : (T)0;
+  T wv = sqrtD * mul_L(m, e, e.qLD, qv);
+  T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
+  T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
+  wsync();
+  if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww - ws; }
+  wsync();
+  T* efc = e.efc;
+  const T* Bm = e.Bm;
+  const int Bs = e.Bs;
+  // per row: aref, b = J qacc_smooth - aref, D; x at u = 0 (q[1]) and at the warmstart (q[3])
+  T c0p = 0, cwp = 0;
+  for (int r = l; r < ne; r += 64) {
+    const T* row = Bm + r * Bs;
+    T dv = 0, ds = 0, dw = 0;
+    for (int k = 0; k < nv; k++) {
+      T x = row[k];
+      dv += x * e.vec0[k]; ds += x * e.vec1[k]; dw += x * e.vec2[k];
+    }
+    T* q = efc + 8 * r;
+    T aref = -q[6] * dv - q[5];
+    q[5] = aref;
+    T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
+    q[0] = b; q[1] = b; q[3] = xw; q[4] = D;
+    if (b < 0) c0p += (T)0.5 * D * b * b;
+    if (xw < 0) cwp += (T)0.5 * D * xw * xw;
+  }
+  const T uw = dl ? e.vec2[l] : (T)0;
+  const T c0 = usum(c0p), cw = usum(cwp + (T)0.5 * uw * uw);
+  const bool warm = cw < c0;
+  T u = warm ? uw : (T)0;
+  T cost = warm ? cw : c0;
+  if (warm) for (int r = l; r < ne; r += 64) efc[8 * r + 1] = efc[8 * r + 3];
+  wsync();
+  T* H = e.hess;
+  const T scale = (T)1 / (m.meaninertia * (T)(nv > 1 ? nv : 1));
+  const T tol = m.tolerance;
+  const T eps = sizeof(T) == 4 ? (T)1e-7 : (T)1e-15;
+  const int maxit = m.iterations;
+  int iter = 0;
+  while (iter < maxit) {
+    T g = u;
+    for (int r = 0; r < ne; r++) {
+      T xr = efc[8 * r + 1];
+      if (xr < 0) g += efc[8 * r + 4] * xr * Bm[r * Bs + lc];
+    }
+    g = dl ? g : (T)0;
+    // MuJoCo's gradient rule is on the dof-space gradient M(a - a0) - J'f = L' D^1/2 g
+    T ga = mul_LT(m, e, e.qLD, sqrtD * g);
+    if (scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol) break;
+    // H = I + sum D B_r B_r', lower triangle, lane = column
+    for (int i = 0; i < nv; i++) {
+      T acc = l == i ? (T)1 : (T)0;
+      for (int r = 0; r < ne; r++) {
+        T xr = efc[8 * r + 1];
+        if (xr < 0) acc += efc[8 * r + 4] * Bm[r * Bs + i] * Bm[r * Bs + lc];
+      }
+      if (l <= i) H[i * nv + l] = acc;
+    }
+    wsync();
+    // Cholesky H = L L' in place, lane = column j: column k scaled, then H[i][j] -= L[i][k] L[j][k]
+    for (int k = 0; k < nv; k++) {
+      T hjk = (dl && l >= k) ? H[l * nv + k] : (T)0;
+      T dkk = readlane(hjk, k);
+      T s = sqrt(dkk > minval<T>() ? dkk : minval<T>());
+      T ljk = l == k ? s : hjk / s;
+      if (dl && l >= k) H[l * nv + k] = ljk;
+      for (int i = k + 1; i < nv; i++) {
+        T lik = readlane(ljk, i);
+        if (l > k && l <= i) H[i * nv + l] -= lik * ljk;
+      }
+      wsync();
+    }
+    // L y = -g, L' p = y
+    T y = -g;
+    for (int k = 0; k < nv; k++) {
+      T yk = readlane(y, k) / H[k * nv + k];
+      if (l == k) y = yk;
+      else if (dl && l > k) y -= H[l * nv + k] * yk;
+    }
+    T p = y;
+    for (int k = nv - 1; k >= 0; k--) {
+      T pk = readlane(p, k) / H[k * nv + k];
+      if (l == k) p = pk;
+      else if (l < k) p -= H[k * nv + l] * pk;
+    }
+    p = dl ? p : (T)0;
+    wsync();
+    if (dl) e.vec3[l] = p;
+    wsync();
+    for (int r = l; r < ne; r += 64) {
+      const T* row = Bm + r * Bs;
+      T s = 0;
+      for (int k = 0; k < nv; k++) s += row[k] * e.vec3[k];
+      efc[8 * r + 3] = s;
+    }
+    // exact line search: f'(al) = u.p + al p.p + sum_{x + al jp < 0} D (x + al jp) jp
+    const T g0 = usum(u * p), pp = usum(p * p);
+    T al = 1, lo = 0, hi = (T)1e30;
+    for (int ls = 0; ls < 50; ls++) {
+      T d1p = 0, d2p = 0;
+      for (int r = l; r < ne; r += 64) {
+        const T* q = efc + 8 * r;
+        T jp = q[3], xr = q[1] + al * jp;
+        if (xr < 0) { d1p += q[4] * xr * jp; d2p += q[4] * jp * jp; }
+      }
+      T d1 = g0 + al * pp + usum(d1p), d2 = pp + usum(d2p);
+      if (d1 < 0) lo = al; else hi = al;
+      T nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
+      if (!(nxt > lo && nxt < hi)) nxt = hi < (T)1e30 ? (T)0.5 * (lo + hi) : 2 * al;
+      bool done = fabs(nxt - al) <= eps * (1 + fabs(al));
+      al = nxt;
+      if (done) break;
+    }
+    u += al * p;
+    T cp = 0;
+    for (int r = l; r < ne; r += 64) {
+      T* q = efc + 8 * r;
+      T xr = q[1] + al * q[3];
+      q[1] = xr;
+      if (xr < 0) cp += (T)0.5 * q[4] * xr * xr;
+    }
+    T cnew = usum(cp + (T)0.5 * u * u);
+    T improvement = scale * (cost - cnew);
+    cost = cnew;
+    iter++;
+    wsync();
+    if (improvement < tol) break;
+  }
+  e.niter = iter;
+  for (int r = l; r < ne; r += 64) {
+    T* q = efc + 8 * r;
+    q[1] = q[1] < 0 ? -q[4] * q[1] : (T)0;
+  }
+  wsync();
+  // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = J'f = L' D^1/2 (sum f_r B_r)
+  T v = 0;
+  for (int r = 0; r < ne; r++) v += efc[8 * r + 1] * Bm[r * Bs + lc];
+  v = dl ? v : (T)0;
+  T z = dl ? u * e.diaginv * sqrtD : (T)0;
+  z = solve_L(m, e, e.qLD, z);
+  e.qacc = e.qacc_smooth + z;
+  e.qfrc_constraint = mul_LT(m, e, e.qLD, sqrtD * v);
+  wsync();
+}
+
 // ---------------------------------------------------------------- integration
 template <typename T>
 __device__ __forceinline__ void quat_integrate(T* q, const T* w, T h) {
@@ -920,7 +1096,7 @@ __device__ __forceinline__ void integrate_pos(const DevModel<T>& m, T* qpos, con
   wsync();
 }
 
-template <typename T>
+template <typename T, bool NT = false>
 __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e);
 
 // mj_RungeKutta(m, d, 4) [ext], after forward() at X[0] (oracle/mjref.c rk4): stage i runs the
@@ -928,7 +1104,7 @@ __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e);
 // dX = sum_j B_j X'[j]. Velocities and accelerations stay in dof-lane registers; X[0]
 // positions and the dX velocity vector (integratePos input) sit in the rk LDS region. The
 // frames left in LDS are those of the last stage, as MuJoCo leaves them in mjData.
-template <typename T>
+template <typename T, bool NT = false>
 __device__ __forceinline__ void rk4(const DevModel<T>& m, Env<T>& e) {
   const T A[9] = {(T)0.5, 0, 0, 0, (T)0.5, 0, 0, 0, (T)1};
   const T B[4] = {(T)(1.0 / 6.0), (T)(1.0 / 3.0), (T)(1.0 / 3.0), (T)(1.0 / 6.0)};
@@ -958,7 +1134,7 @@ __device__ __forceinline__ void rk4(const DevModel<T>& m, Env<T>& e) {
     if (dl) e.qvel[l] = v[i];
     e.time = t0 + C * h;
     wsync();
-    forward(m, e);
+    forward<T, NT>(m, e);
     f[i] = dl ? e.qacc : (T)0;
   }
   T dv = 0, da = 0;
@@ -990,7 +1166,8 @@ __device__ __forceinline__ void euler(const DevModel<T>& m, Env<T>& e) {
 }
 
 // ---------------------------------------------------------------- forward + step
-template <typename T>
+// NT: the model's solver is Newton (compile-time, so PGS kernels do not carry it)
+template <typename T, bool NT>
 __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
   // phase A (kinematics .. velocity) uses the LDS union region; phase B (constraint rows)
   // overwrites it with the B matrix once collision has consumed the geom frames
@@ -1014,7 +1191,8 @@ __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
   wsync();
   transform_rows(m, e);
   MGX_STAMP(7);
-  pgs(m, e);
+  if constexpr (NT) newton(m, e);
+  else pgs(m, e);
   MGX_STAMP(8);
 #ifdef MGX_PROFILE
   if (g_mgx_prof && lane_id() == 0) {
@@ -1028,19 +1206,19 @@ __device__ __forceinline__ void forward(const DevModel<T>& m, Env<T>& e) {
 
 // returns the number of bad-state resets performed (0..3). RK: the model's integrator is RK4
 // (a compile-time choice so Euler kernels do not carry the RK4 stages).
-template <typename T, bool RK = false>
+template <typename T, bool RK = false, bool NT = false>
 __device__ __forceinline__ int mj_step_env(const DevModel<T>& m, Env<T>& e) {
   int warn = 0;
   if (any_bad(e.qpos, m.nq)) { reset_env(m, e); warn++; }
   if (any_bad(e.qvel, m.nv)) { reset_env(m, e); warn++; }
-  forward(m, e);
+  forward<T, NT>(m, e);
   if (ballot(lane_id() < m.nv && isbad(e.qacc)) != 0ull) {
     reset_env(m, e);
     warn++;
-    forward(m, e);
+    forward<T, NT>(m, e);
   }
   if constexpr (RK) {
-    rk4(m, e);
+    rk4<T, NT>(m, e);
     return warn;
   }
   e.qacc_ws = e.qacc;

@@ -15,7 +15,7 @@ int fail(int code, const std::string& msg) { return host_fail(code, msg); }
 int check_state(const mgx_state* s) { return host_check_state(s); }
 
 // GB: B rows in global scratch (Layout.gB); RK: RK4 integrator
-template <typename T, bool GB, bool RK>
+template <typename T, bool GB, bool RK, bool NT>
 __global__ void __launch_bounds__(64) k_step(DevModel<T> m, mgx_state s, mgx_frames fr, int n_env, int nsub,
                                              const uint8_t* mask) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(64) k_step(DevModel<T> m, mgx_state s, mgx_fra
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   int warn = 0;
-  for (int k = 0; k < nsub; k++) warn += mj_step_env<T, RK>(m, e);
+  for (int k = 0; k < nsub; k++) warn += mj_step_env<T, RK, NT>(m, e);
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   int l = lane_id();
   if (l == 0 && s.warning) s.warning[env] += warn;
@@ -81,7 +81,7 @@ DbgOff dbg_offsets(int nb, int nv, int nM, int ng, int C, int E) {
   return o;
 }
 
-template <typename T, bool GB>
+template <typename T, bool GB, bool NT>
 __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s, int n_env, T* dbg, DbgOff o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int env = blockIdx.x;
@@ -116,7 +116,8 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   wsync();
   for (int r = l; r < e.nefc; r += 64)
     for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];
-  pgs(m, e);
+  if constexpr (NT) newton(m, e);
+  else pgs(m, e);
   wsync();
   for (int k = l; k < 3 * m.nbody; k += 64) { D[o.xpos + k] = e.xpos[k]; D[o.subtree_com + k] = e.subtree_com[k]; }
   for (int k = l; k < 4 * m.nbody; k += 64) D[o.xquat + k] = e.xquat[k];
@@ -143,22 +144,37 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
 
 template <typename T, bool GB, bool RK>
 int set_step_lds(const mgx_model* m) {
-  return mgx_set_lds(k_step<T, GB, RK>, m->L.bytes);
+  return mgx_set_lds(k_step<T, GB, RK, false>, m->L.bytes) | mgx_set_lds(k_step<T, GB, RK, true>, m->L.bytes);
+}
+
+// NT (Newton solver) is chosen from the model at launch
+template <typename T, bool GB, bool RK>
+void launch_step_v(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const mgx_frames& fr, int n_env,
+                   int nsub, const uint8_t* mask, hipStream_t st) {
+  if (M.solver == 2)
+    hipLaunchKernelGGL((k_step<T, GB, RK, true>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, fr, n_env, nsub, mask);
+  else
+    hipLaunchKernelGGL((k_step<T, GB, RK, false>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, fr, n_env, nsub, mask);
 }
 
 template <typename T>
 int launch_step(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const mgx_frames& fr, int n_env, int nsub,
                 const uint8_t* mask, hipStream_t st) {
   bool rk = M.integrator == 1;
-  if (m->L.gB && rk)
-    hipLaunchKernelGGL((k_step<T, true, true>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, fr, n_env, nsub, mask);
-  else if (m->L.gB)
-    hipLaunchKernelGGL((k_step<T, true, false>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, fr, n_env, nsub, mask);
-  else if (rk)
-    hipLaunchKernelGGL((k_step<T, false, true>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, fr, n_env, nsub, mask);
-  else
-    hipLaunchKernelGGL((k_step<T, false, false>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, fr, n_env, nsub, mask);
+  if (m->L.gB && rk) launch_step_v<T, true, true>(m, M, s, fr, n_env, nsub, mask, st);
+  else if (m->L.gB) launch_step_v<T, true, false>(m, M, s, fr, n_env, nsub, mask, st);
+  else if (rk) launch_step_v<T, false, true>(m, M, s, fr, n_env, nsub, mask, st);
+  else launch_step_v<T, false, false>(m, M, s, fr, n_env, nsub, mask, st);
   return MGX_OK;
+}
+
+template <typename T, bool GB>
+void launch_debug_v(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, int n_env, T* dbg, DbgOff o,
+                    hipStream_t st) {
+  if (M.solver == 2)
+    hipLaunchKernelGGL((k_debug_forward<T, GB, true>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, n_env, dbg, o);
+  else
+    hipLaunchKernelGGL((k_debug_forward<T, GB, false>), dim3(n_env), dim3(64), m->L.bytes, st, M, *s, n_env, dbg, o);
 }
 
 }  // namespace
@@ -169,10 +185,12 @@ int step_kernels_configure(const mgx_model* m) {
   if (m->precision == MGX_F32)
     return set_step_lds<float, false, false>(m) | set_step_lds<float, false, true>(m) |
            set_step_lds<float, true, false>(m) | set_step_lds<float, true, true>(m) |
-           mgx_set_lds(k_debug_forward<float, false>, m->L.bytes) | mgx_set_lds(k_debug_forward<float, true>, m->L.bytes);
+           mgx_set_lds(k_debug_forward<float, false, false>, m->L.bytes) | mgx_set_lds(k_debug_forward<float, true, false>, m->L.bytes) |
+           mgx_set_lds(k_debug_forward<float, false, true>, m->L.bytes) | mgx_set_lds(k_debug_forward<float, true, true>, m->L.bytes);
   return set_step_lds<double, false, false>(m) | set_step_lds<double, false, true>(m) |
          set_step_lds<double, true, false>(m) | set_step_lds<double, true, true>(m) |
-         mgx_set_lds(k_debug_forward<double, false>, m->L.bytes) | mgx_set_lds(k_debug_forward<double, true>, m->L.bytes);
+         mgx_set_lds(k_debug_forward<double, false, false>, m->L.bytes) | mgx_set_lds(k_debug_forward<double, true, false>, m->L.bytes) |
+         mgx_set_lds(k_debug_forward<double, false, true>, m->L.bytes) | mgx_set_lds(k_debug_forward<double, true, true>, m->L.bytes);
 }
 }  // namespace mgx
 
@@ -228,16 +246,12 @@ int mgx_debug_forward(const mgx_model* m, const mgx_state* s, int n_env, void* d
   hipStream_t st = (hipStream_t)stream;
   if (m->precision == MGX_F32) {
     DbgOff o = dbg_offsets(m->mf.nbody, m->mf.nv, m->mf.nM, m->mf.ngeom, m->L.max_ncon, m->L.max_nefc);
-    if (m->L.gB)
-      hipLaunchKernelGGL((k_debug_forward<float, true>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, n_env, (float*)dbg, o);
-    else
-      hipLaunchKernelGGL((k_debug_forward<float, false>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, n_env, (float*)dbg, o);
+    if (m->L.gB) launch_debug_v<float, true>(m, m->mf, s, n_env, (float*)dbg, o, st);
+    else launch_debug_v<float, false>(m, m->mf, s, n_env, (float*)dbg, o, st);
   } else {
     DbgOff o = dbg_offsets(m->md.nbody, m->md.nv, m->md.nM, m->md.ngeom, m->L.max_ncon, m->L.max_nefc);
-    if (m->L.gB)
-      hipLaunchKernelGGL((k_debug_forward<double, true>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, n_env, (double*)dbg, o);
-    else
-      hipLaunchKernelGGL((k_debug_forward<double, false>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, n_env, (double*)dbg, o);
+    if (m->L.gB) launch_debug_v<double, true>(m, m->md, s, n_env, (double*)dbg, o, st);
+    else launch_debug_v<double, false>(m, m->md, s, n_env, (double*)dbg, o, st);
   }
   HIPCHK(hipGetLastError());
   return MGX_OK;

@@ -194,3 +194,30 @@ def test_cylinder_box_cap_and_side():
     # cylinder center z 0.3, radius 0.5 -> top of the side at 0.8; box bottom at 0.795
     assert len(c["dist"]) == 1 and abs(c["dist"][0] - (0.795 - 0.8)) < 1e-9
     np.testing.assert_allclose(c["frame"][0][:3], [0, 0, 1], atol=1e-9)
+
+
+def test_box_resting_on_box_newton():
+    """Same rest state with the Newton solver (oracle/mjref.c newton_solve): the box settles,
+    the contacts carry m g, and the converged qacc agrees with a long PGS solve of the same
+    problem (both minimise one convex cost)."""
+    xml = HDR.replace('solver="PGS"', 'solver="Newton" tolerance="1e-10"') + (
+        '<worldbody><geom type="box" size="2 2 0.1"/>'
+        '<body pos="0 0 0.29"><freejoint/><geom type="box" size="0.2 0.3 0.2" mass="4"/></body>'
+        '</worldbody></mujoco>')
+    m, pk, s = sim_of(xml)
+    assert m.solver == 2
+    for _ in range(300):
+        s.step()
+    ne = int(s.nefc[0])
+    J = s.efc_J[:ne * m.nv].reshape(ne, m.nv)
+    assert abs((J.T @ s.efc_force[:ne])[2] - 40) < 1e-3 * 40
+    assert np.abs(s.qvel).max() < 1e-3
+    assert int(s.solver_niter[0]) <= m.iterations  # 0 at rest: the warmstart is already optimal
+    m2 = mjcf.compile_xml(xml.replace('solver="Newton" tolerance="1e-10"', 'solver="PGS" tolerance="1e-30"')
+                          .replace('iterations="100"', 'iterations="20000"'))
+    p = RefSim(cabi.pack_model(m2))
+    for f in ("qpos", "qvel", "qacc_warmstart"):
+        p.field(f)[:] = s.field(f)
+    s.forward()
+    p.forward()
+    np.testing.assert_allclose(s.qacc, p.qacc, atol=1e-6)
