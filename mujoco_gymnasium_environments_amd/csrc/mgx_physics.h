@@ -972,14 +972,24 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     // MuJoCo's gradient rule is on the dof-space gradient M(a - a0) - J'f = L' D^1/2 g
     T ga = mul_LT(m, e, e.qLD, sqrtD * g);
     if (scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol) break;
-    // H = I + sum D B_r B_r', lower triangle, lane = column
-    for (int i = 0; i < nv; i++) {
-      T acc = l == i ? (T)1 : (T)0;
+    // H = I + sum D B_r B_r', lower triangle, lane = column j, rows i in blocks of 8 held in
+    // registers: per active row one lane-indexed read B_rj and 8 broadcast reads B_ri
+    for (int i0 = 0; i0 < nv; i0 += 8) {
+      T acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc[k] = l == i0 + k ? (T)1 : (T)0;
       for (int r = 0; r < ne; r++) {
         T xr = efc[8 * r + 1];
-        if (xr < 0) acc += efc[8 * r + 4] * Bm[r * Bs + i] * Bm[r * Bs + lc];
+        if (xr < 0) {
+          const T* row = Bm + r * Bs;
+          T c = efc[8 * r + 4] * row[lc];
+#pragma unroll
+          for (int k = 0; k < 8; k++) acc[k] += c * row[i0 + k < nv ? i0 + k : nv - 1];
+        }
       }
-      if (l <= i) H[i * nv + l] = acc;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (i0 + k < nv && l <= i0 + k) H[(i0 + k) * nv + l] = acc[k];
     }
     wsync();
     // Cholesky H = L L' in place, lane = column j: column k scaled, then H[i][j] -= L[i][k] L[j][k]
