@@ -189,7 +189,7 @@ int mgx_dancing_step(const mgx_model* m, const mgx_state* s, const mgx_dancing_e
                      uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
   if (!m->dancing_ok) return fail(MGX_E_ARG, "mgx_dancing_configure not called");
-  if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null bipedal env buffer");
+  if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null dancing env buffer");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
@@ -210,7 +210,7 @@ int mgx_dancing_reset(const mgx_model* m, const mgx_state* s, const mgx_dancing_
                       uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !obs) return fail(MGX_E_ARG, "null argument");
   if (!m->dancing_ok) return fail(MGX_E_ARG, "mgx_dancing_configure not called");
-  if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null bipedal env buffer");
+  if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null dancing env buffer");
   if (!draws && !e->episode) return fail(MGX_E_ARG, "device draws need the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
@@ -231,7 +231,7 @@ int mgx_dancing_logic_test(const mgx_model* m, const mgx_dancing_logic_io* io, c
                            void* stream) {
   if (!m || !io || !e) return fail(MGX_E_ARG, "null argument");
   if (!m->dancing_ok) return fail(MGX_E_ARG, "mgx_dancing_configure not called");
-  if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null bipedal env buffer");
+  if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null dancing env buffer");
   if (io->max_contacts > m->L.max_ncon) return fail(MGX_E_CAPACITY, "max_contacts exceeds the contact capacity");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
