@@ -992,17 +992,22 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
         if (i0 + k < nv && l <= i0 + k) H[(i0 + k) * nv + l] = acc[k];
     }
     wsync();
-    // Cholesky H = L L' in place, lane = column j: column k scaled, then H[i][j] -= L[i][k] L[j][k]
+    // Cholesky H = L L' in place, left-looking, lane = row i: column k is
+    // L[i][k] = (H[i][k] - sum_{j<k} L[i][j] L[k][j]) / L[k][k]; a lane's own row is written only
+    // by itself, row k (broadcast reads) was finished by lane k before the barrier
     for (int k = 0; k < nv; k++) {
-      T hjk = (dl && l >= k) ? H[l * nv + k] : (T)0;
-      T dkk = readlane(hjk, k);
-      T s = sqrt(dkk > minval<T>() ? dkk : minval<T>());
-      T ljk = l == k ? s : hjk / s;
-      if (dl && l >= k) H[l * nv + k] = ljk;
-      for (int i = k + 1; i < nv; i++) {
-        T lik = readlane(ljk, i);
-        if (l > k && l <= i) H[i * nv + l] -= lik * ljk;
-      }
+      const bool act = dl && l >= k;
+      const int li = act ? l : k;
+      T s0 = H[li * nv + k], s1 = 0;
+      const T* Li = H + li * nv;
+      const T* Lk = H + k * nv;
+      int j = 0;
+      for (; j + 1 < k; j += 2) { s0 -= Li[j] * Lk[j]; s1 -= Li[j + 1] * Lk[j + 1]; }
+      if (j < k) s0 -= Li[j] * Lk[j];
+      T s = s0 + s1;
+      T dkk = readlane(s, k);
+      T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
+      if (act) H[l * nv + k] = l == k ? d : s / d;
       wsync();
     }
     // L y = -g, L' p = y
