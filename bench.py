@@ -44,6 +44,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
 PMC_PROFILE = "r01_v4_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
 PMC_PROFILE_BIPEDAL = "r01_bipedal_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
@@ -337,6 +338,42 @@ def bench_mixed(args, dev, world, rank, dist):
         dist.destroy_process_group()
 
 
+def soccer_flops(ro: torch.Tensor, nv: int) -> dict:
+    """SURVEY 8(d) algorithmic FLOPs of the soccer step from the in-kernel sums (dense-equivalent
+    count of the constraint phase: A = J M^-1 J' costs 2 nefc^2 nv, PGS 2 sweeps nefc^2; the
+    kinematics / CRB / RNE rest ~ 300 nbody is added as a constant)."""
+    steps = float(ro[3])
+    a = 2.0 * float(ro[6]) * nv
+    pgs = 2.0 * float(ro[7])
+    rest = 300.0 * 20 * steps
+    return {"flops_per_env_step": (a + pgs + rest) / max(steps, 1.0), "nefc_mean": float(ro[4]) / max(steps, 1.0),
+            "pgs_sweeps_mean": float(ro[5]) / max(steps, 1.0)}
+
+
+def f64_parity_line(args, dev, N, g) -> dict:
+    """The same step in parity precision (fp64, SURVEY §7 'report both'): a short timed run on the
+    staged fp64 kernels after the headline's timed region."""
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    env = SoccerVectorEnv(N, device=str(dev), precision="f64", seed=1234, staged=True, banks=args.banks)
+    pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(4)]
+    env.reset()
+    for k in range(5):
+        env.step(pool[k % 4])
+    torch.cuda.synchronize(dev)
+    steps = 20
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record()
+    for k in range(steps):
+        env.step(pool[k % 4])
+    b.record()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return {"value": round(N * steps / el, 1), "unit": "env_steps/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "launch_ms": round(a.elapsed_time(b) / steps, 4), "steps": steps, "dtype": "f64",
+            "note": "parity precision (tests/test_gpu_f32_staged.py: 1000-step drift vs the oracle < 1e-4)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -349,6 +386,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
+    ap.add_argument("--no-f64-line", action="store_true", help="skip the fp64 parity-precision line (soccer)")
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed"])
     args = ap.parse_args()
     if args.task != "soccer":
@@ -393,6 +431,7 @@ def main():
     # rollout metrics accumulate inside the kernel (env.rollout); read once after the timed region
     acc = torch.zeros(6, dtype=torch.float64, device=dev)  # env_steps, episodes, reward, term, trunc, bad
     env.rollout.zero_()
+    env.batch.overflow.zero_()
     ep0 = int(env.episode.sum().item())
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -413,6 +452,7 @@ def main():
     acc[1] = float(env.episode.sum().item() - ep0)
     acc[2], acc[3], acc[4] = ro[0], ro[1], ro[2]
     acc[5] = float(env.batch.warning.sum().item())
+    overflow_steps = int(env.batch.overflow.sum().item())
     acc, elapsed = reduce_rollout(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
     value = total_steps / elapsed
@@ -483,6 +523,7 @@ def main():
                        "autoreset": "same-step", "step_kernels": mode, "reset_banks": 0 if args.mono else args.banks,
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "capacity_overflow_steps": overflow_steps,
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -492,6 +533,16 @@ def main():
                          "note": "achieved = algorithmic bytes of one env step x envs / HIP-event time of the "
                                  "step's launches; traffic = PMC HBM bytes of those launches per step"},
         }
+        fl = soccer_flops(ro.cpu(), env.model.nv)
+        tf = fl["flops_per_env_step"] * N / (launch_ms * 1e-3) / 1e12
+        out["roofline_flops"] = {"bound": "valu", "achieved": round(tf, 4), "peak": VALU_PEAK_TFLOPS[args.precision],
+                                 "unit": "TFLOP/s", "frac": tf / VALU_PEAK_TFLOPS[args.precision],
+                                 "flops_per_env_step": round(fl["flops_per_env_step"]),
+                                 "nefc_mean": round(fl["nefc_mean"], 2), "pgs_sweeps_mean": round(fl["pgs_sweeps_mean"], 2),
+                                 "definition": "SURVEY 8(d) dense-equivalent: 2 nefc^2 nv (A) + 2 sweeps nefc^2 (PGS) "
+                                               "+ 300 nbody, summed per env step in the kernel"}
+        if not args.no_f64_line and world == 1 and args.precision == "f32":
+            out["f64_parity_mode"] = f64_parity_line(args, dev, N, g)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_steps)
         print(json.dumps(out))

@@ -107,6 +107,9 @@ typedef struct mgx_state {
   void *time;           /* [N] */
   int32_t *warning;     /* [N] count of bad-state auto-resets (mj_checkPos/Vel/Acc) */
   void *scratch;        /* [N][scratch_bytes_per_env] device bytes; NULL when the model needs none */
+  int32_t *overflow;    /* [N] or NULL: count of env steps whose contacts or constraint rows were
+                           truncated to the model's capacity (MuJoCo's mjWARN_CONTACTFULL /
+                           mjWARN_CNSTRFULL: warn and continue with the rows that fit) */
 } mgx_state;
 
 /* Per-step outputs of the forward pass that env logic reads (stale "pre-integration"
@@ -154,8 +157,9 @@ typedef struct mgx_soccer_env {
                                     when every reset passes host draws */
   uint8_t *flags;        /* [N][2]  ball_contact, robot_upright of the last step (info dict,
                                     soccer_env.py:438-439); nullable */
-  void *rollout;         /* [N][4]  running sums: reward, terminated, truncated, env steps
-                                    (the end-of-rollout metrics; nullable) */
+  void *rollout;         /* [N][8] fp64 running sums: reward, terminated, truncated, env steps,
+                                    nefc, PGS sweeps, nefc^2, sweeps*nefc^2 (the end-of-rollout
+                                    metrics and the SURVEY 8(d) FLOP count; nullable) */
   void *workspace;       /* nullable: staged-step workspace (mgx_soccer_workspace_bytes), bound
                             to (model, N, banks); holds the reset banks between calls */
   uint64_t workspace_bytes;

@@ -75,6 +75,7 @@ class PhysicsBatch:
         self.xfrc_applied = torch.zeros(n_env, m.nbody, 6, dtype=dt, device=self.device)
         self.time = torch.zeros(n_env, dtype=dt, device=self.device)
         self.warning = torch.zeros(n_env, dtype=torch.int32, device=self.device)
+        self.overflow = torch.zeros(n_env, dtype=torch.int32, device=self.device)
         self.xpos = torch.zeros(n_env, m.nbody, 3, dtype=dt, device=self.device)
         self.xquat = torch.zeros(n_env, m.nbody, 4, dtype=dt, device=self.device)
         self.subtree_com = torch.zeros(n_env, m.nbody, 3, dtype=dt, device=self.device)
@@ -87,7 +88,8 @@ class PhysicsBatch:
         self._state = cabi.MgxState(*[t.data_ptr() for t in (self.qpos, self.qvel, self.qacc_warmstart, self.ctrl,
                                                              self.qfrc_applied, self.xfrc_applied, self.time,
                                                              self.warning)],
-                                    self.scratch.data_ptr() if self.scratch is not None else None)
+                                    self.scratch.data_ptr() if self.scratch is not None else None,
+                                    self.overflow.data_ptr())
         self._frames = cabi.MgxFrames(*[t.data_ptr() for t in (self.xpos, self.xquat, self.subtree_com, self.ncon,
                                                               self.nefc, self.niter)])
 

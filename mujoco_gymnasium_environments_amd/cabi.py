@@ -62,7 +62,8 @@ class MgxModelInfo(C.Structure):
 class MgxState(C.Structure):
     _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("qacc_warmstart", C.c_void_p),
                 ("ctrl", C.c_void_p), ("qfrc_applied", C.c_void_p), ("xfrc_applied", C.c_void_p),
-                ("time", C.c_void_p), ("warning", C.c_void_p), ("scratch", C.c_void_p)]
+                ("time", C.c_void_p), ("warning", C.c_void_p), ("scratch", C.c_void_p),
+                ("overflow", C.c_void_p)]
 
 
 class MgxFrames(C.Structure):

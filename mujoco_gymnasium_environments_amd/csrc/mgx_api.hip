@@ -72,6 +72,7 @@ __device__ __forceinline__ void soccer_reset_philox(const DevModel<T>& m, Env<T>
               (T*)s.time, env);
   if (l == 0) {
     if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
     ev.episode[env] = E + 1;
   }
   wsync();
@@ -97,14 +98,20 @@ __device__ __forceinline__ void soccer_step_mono(const DevModel<T>& m, Env<T>& e
                           (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, o, reward + env,
                           terminated + env, truncated + env, ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
   if (ev.rollout && l == 0) {
-    T* ro = (T*)ev.rollout + 4 * (size_t)env;
-    ro[0] += (T)reward[env];
-    ro[1] += (T)terminated[env];
-    ro[2] += (T)truncated[env];
-    ro[3] += (T)1;
+    double* ro = (double*)ev.rollout + 8 * (size_t)env;
+    const double ne = e.nefc, it = e.niter;
+    ro[0] += reward[env];
+    ro[1] += terminated[env];
+    ro[2] += truncated[env];
+    ro[3] += 1.0;
+    ro[4] += ne;
+    ro[5] += it;
+    ro[6] += ne * ne;
+    ro[7] += it * ne * ne;
   }
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
   if (done && autoreset) {
     if (final_obs)
       for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];
@@ -164,6 +171,7 @@ __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, 
   if (ev.episode && lane_id() == 0) ev.episode[env] += 1;
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (lane_id() == 0 && s.warning) s.warning[env] += warn;
+  if (lane_id() == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
 }
 
 // ---- staged step kernels (mgx_staged.h)
@@ -239,17 +247,23 @@ __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T
   store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
               (T*)s.time, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
   const float* a = action + (size_t)env * m.nu;
   float* o = obs + (size_t)env * 80;
   bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, (T*)ev.prev_ball_pos + 3 * (size_t)env,
                           (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, o, reward + env,
                           terminated + env, truncated + env, ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
   if (ev.rollout && l == 0) {
-    T* ro = (T*)ev.rollout + 4 * (size_t)env;
-    ro[0] += (T)reward[env];
-    ro[1] += (T)terminated[env];
-    ro[2] += (T)truncated[env];
-    ro[3] += (T)1;
+    double* ro = (double*)ev.rollout + 8 * (size_t)env;
+    const double ne = e.nefc, it = e.nefc > 0 ? P.at<int>(P.o_niter)[env] : 0;
+    ro[0] += reward[env];
+    ro[1] += terminated[env];
+    ro[2] += truncated[env];
+    ro[3] += 1.0;
+    ro[4] += ne;
+    ro[5] += it;
+    ro[6] += ne * ne;
+    ro[7] += it * ne * ne;
   }
   if (done && autoreset) {
     if (final_obs)
@@ -549,7 +563,6 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.maxE = m->Ls.max_nefc; p.nv = nv; p.dpl = (nv + 7) / 8;  // solver: support entries per lane
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
-  p.brow = 16 * p.dpl;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t r = off; off = (off + bytes + 255) / 256 * 256; return r; };
@@ -577,20 +590,7 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 static int pgs_lds_bytes(const mgx_model* m) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nb3 = (m->Ls.max_nefc / 4 + 2) / 3 * 3;  // whole ring turns of 3 blocks
-  return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 1) * rb + MGX_PGS_SPW * nb3 * 16 + 64;
-}
-
-template <typename T>
-static void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale) {
-  static const int spw = getenv("MGX_PGS_SPW") ? atoi(getenv("MGX_PGS_SPW")) : MGX_PGS_SPW;  // debug: slots per wave
-  int grid = (slots + (spw < 0 ? -spw : spw) - 1) / (spw < 0 ? -spw : spw);
-  switch (P.dpl) {
-#define MGX_PGS_CASE(E) \
-    case E: hipLaunchKernelGGL((k_pgs_groups<T, E>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw); break;
-    MGX_PGS_CASE(1) MGX_PGS_CASE(2) MGX_PGS_CASE(3) MGX_PGS_CASE(4) MGX_PGS_CASE(5) MGX_PGS_CASE(6) MGX_PGS_CASE(7)
-    default: hipLaunchKernelGGL((k_pgs_groups<T, 8>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw); break;
-#undef MGX_PGS_CASE
-  }
+  return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 4) * rb + MGX_PGS_SPW * nb3 * 16 + 64;
 }
 
 template <typename T>
@@ -693,15 +693,7 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   if (m->staged_ok) {
     int pl = pgs_lds_bytes(m);
     if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
-    int r3 = precision == MGX_F32
-                 ? (set_lds(k_pgs_groups<float, 1>, pl) | set_lds(k_pgs_groups<float, 2>, pl) |
-                    set_lds(k_pgs_groups<float, 3>, pl) | set_lds(k_pgs_groups<float, 4>, pl) |
-                    set_lds(k_pgs_groups<float, 5>, pl) | set_lds(k_pgs_groups<float, 6>, pl) |
-                    set_lds(k_pgs_groups<float, 7>, pl) | set_lds(k_pgs_groups<float, 8>, pl))
-                 : (set_lds(k_pgs_groups<double, 1>, pl) | set_lds(k_pgs_groups<double, 2>, pl) |
-                    set_lds(k_pgs_groups<double, 3>, pl) | set_lds(k_pgs_groups<double, 4>, pl) |
-                    set_lds(k_pgs_groups<double, 5>, pl) | set_lds(k_pgs_groups<double, 6>, pl) |
-                    set_lds(k_pgs_groups<double, 7>, pl) | set_lds(k_pgs_groups<double, 8>, pl));
+    int r3 = pgs_configure_lds(precision, pl);
     if (r3 != MGX_OK) { delete m; return r3; }
   }
   *out = m;
@@ -732,6 +724,8 @@ int mgx_soccer_configure(mgx_model* m, const mgx_soccer_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");
   if (m->L.gB || (m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
     return fail(MGX_E_UNSUPPORTED, "the soccer kernels need an Euler model whose rows fit LDS");
+  if ((m->precision == MGX_F32 ? m->mf.solver : m->md.solver) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the soccer kernels solve with PGS (soccer_env.py:150-151)");
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
   if (m->precision == MGX_F32) fill_ids(m->sf, ids, m->mf, nullptr);
   else fill_ids(m->sd, ids, m->md, nullptr);

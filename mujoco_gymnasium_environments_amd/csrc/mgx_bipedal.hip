@@ -36,6 +36,7 @@ __device__ __forceinline__ void bipedal_reset_philox(const DevModel<T>& m, Env<T
               (T*)s.time, env);
   if (l == 0) {
     if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
     be.episode[env] = E + 1;
   }
 }
@@ -67,6 +68,7 @@ __global__ void __launch_bounds__(64) k_bipedal(DevModel<T> m, BipedalIds ids, m
     store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
     if (l == 0) {
       if (s.warning) s.warning[env] += warn;
+      if (s.overflow && e.overflow) s.overflow[env] += 1;
       if (be.episode) be.episode[env] += 1;
     }
     return;
@@ -85,6 +87,7 @@ __global__ void __launch_bounds__(64) k_bipedal(DevModel<T> m, BipedalIds ids, m
   }
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
   if (done && autoreset) {
     if (final_obs)
       for (int i = l; i < 102; i += 64) final_obs[(size_t)env * 102 + i] = obs[(size_t)env * 102 + i];
@@ -155,6 +158,8 @@ int mgx_bipedal_configure(mgx_model* m, const mgx_bipedal_ids* ids) {
   int nb = f32 ? m->mf.nbody : m->md.nbody;
   if ((f32 ? m->mf.integrator : m->md.integrator) != 1)
     return fail(MGX_E_UNSUPPORTED, "the bipedal kernels integrate with RK4 (rescue_env.py:148)");
+  if ((f32 ? m->mf.solver : m->md.solver) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the bipedal kernels solve with PGS (rescue_env.py:146)");
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
   if (ids->n_act != 26 || nu < 26) return fail(MGX_E_ARG, "bipedal needs 26 actuators written from the action");
   if (ids->torso < 0 || ids->torso >= nb) return fail(MGX_E_ARG, "torso body id out of range");

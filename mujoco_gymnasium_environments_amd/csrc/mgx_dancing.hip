@@ -34,6 +34,7 @@ __device__ __forceinline__ void dancing_reset_philox(const DevModel<T>& m, Env<T
               (T*)s.time, env);
   if (l == 0) {
     if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
     de.episode[env] = E + 1;
   }
 }
@@ -67,6 +68,7 @@ __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, m
     DTRACE(0, 4);
     if (l == 0) {
       if (s.warning) s.warning[env] += warn;
+      if (s.overflow && e.overflow) s.overflow[env] += 1;
       if (de.episode) de.episode[env] += 1;
     }
     return;
@@ -85,6 +87,7 @@ __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, m
   }
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
   if (done && autoreset) {
     if (final_obs)
       for (int i = l; i < MGX_DANCE_OBS; i += 64) final_obs[(size_t)env * MGX_DANCE_OBS + i] = obs[(size_t)env * MGX_DANCE_OBS + i];
@@ -165,6 +168,8 @@ int mgx_dancing_configure(mgx_model* m, const mgx_dancing_ids* ids) {
   int nb = f32 ? m->mf.nbody : m->md.nbody;
   if ((f32 ? m->mf.integrator : m->md.integrator) != 1)
     return fail(MGX_E_UNSUPPORTED, "the dancing kernels integrate with RK4 (dancing_env.py:179)");
+  if ((f32 ? m->mf.solver : m->md.solver) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the dancing kernels solve with PGS (dancing_env.py:177)");
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
   if (ids->n_act != 29 || nu < 29) return fail(MGX_E_ARG, "dancing needs 29 actuators written from the action");
   if (nv < 6 || nv > 64) return fail(MGX_E_ARG, "dancing observes qvel[6:] (6 < nv <= 64)");

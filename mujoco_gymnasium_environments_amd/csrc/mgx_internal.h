@@ -40,6 +40,10 @@ int host_fail(int code, const std::string& msg);
 int host_check_state(const mgx_state* s);
 // dynamic-LDS attributes of the generic step kernels (mgx_step.hip)
 int step_kernels_configure(const mgx_model* m);
+// the staged solver S2 (mgx_pgs.hip)
+template <typename T>
+void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale);
+int pgs_configure_lds(int precision, int bytes);
 }  // namespace mgx
 
 #define MGX_HIPCHK(x)                                                                                   \

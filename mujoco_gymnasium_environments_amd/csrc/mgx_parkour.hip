@@ -29,6 +29,7 @@ __device__ __forceinline__ void parkour_reset_philox(const DevModel<T>& m, Env<T
               (T*)s.time, env);
   if (l == 0) {
     if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
     ev.episode[env] = E + 1;
   }
 }
@@ -58,6 +59,7 @@ __global__ void __launch_bounds__(64) k_parkour(DevModel<T> m, ParkourIds<T> ids
     store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
     if (l == 0) {
       if (s.warning) s.warning[env] += warn;
+      if (s.overflow && e.overflow) s.overflow[env] += 1;
       if (ev.episode) ev.episode[env] += 1;
     }
     return;
@@ -77,6 +79,7 @@ __global__ void __launch_bounds__(64) k_parkour(DevModel<T> m, ParkourIds<T> ids
   }
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
+  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
   if (done && autoreset) {
     if (final_obs)
       for (int i = l; i < 95; i += 64) final_obs[(size_t)env * 95 + i] = obs[(size_t)env * 95 + i];
@@ -140,6 +143,8 @@ int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
   if (m->L.gB || (m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
     return fail(MGX_E_UNSUPPORTED, "the parkour kernels need an Euler model whose rows fit LDS");
+  if ((m->precision == MGX_F32 ? m->mf.solver : m->md.solver) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the parkour kernels solve with PGS (quadruped.xml:4)");
   if (ids->n_leg != 16 || nu < 16 || nq < 7) return fail(MGX_E_ARG, "parkour needs 16 leg actuators and a free root");
   if (ids->torso < 0 || ids->torso >= nb) return fail(MGX_E_ARG, "torso body id out of range");
   for (int i = 0; i < 4; i++)

@@ -962,16 +962,19 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   const T eps = sizeof(T) == 4 ? (T)1e-7 : (T)1e-15;
   const int maxit = m.iterations;
   int iter = 0;
-  while (iter < maxit) {
-    T g = u;
+  // whitened gradient g = u + sum_{x<0} D x B_r (lane = dof)
+  auto gradient = [&]() {
+    T gg = u;
     for (int r = 0; r < ne; r++) {
       T xr = efc[8 * r + 1];
-      if (xr < 0) g += efc[8 * r + 4] * xr * Bm[r * Bs + lc];
+      if (xr < 0) gg += efc[8 * r + 4] * xr * Bm[r * Bs + lc];
     }
-    g = dl ? g : (T)0;
-    // MuJoCo's gradient rule is on the dof-space gradient M(a - a0) - J'f = L' D^1/2 g
-    T ga = mul_LT(m, e, e.qLD, sqrtD * g);
-    if (scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol) break;
+    return dl ? gg : (T)0;
+  };
+  T g = gradient();
+  // mj_solNewton's loop order [ext]: update first, then test the scaled improvement and the
+  // scaled gradient at the new point, so at least one iteration runs
+  while (iter < maxit) {
     // H = I + sum D B_r B_r', lower triangle, lane = column j, rows i in blocks of 8 held in
     // registers: per active row one lane-indexed read B_rj and 8 broadcast reads B_ri
     for (int i0 = 0; i0 < nv; i0 += 8) {
@@ -1064,7 +1067,10 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     cost = cnew;
     iter++;
     wsync();
-    if (improvement < tol) break;
+    g = gradient();
+    // the gradient rule is on the dof-space gradient M(a - a0) - J'f = L' D^1/2 g
+    T ga = mul_LT(m, e, e.qLD, sqrtD * g);
+    if (improvement < tol || scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol) break;
   }
   e.niter = iter;
   for (int r = l; r < ne; r += 64) {

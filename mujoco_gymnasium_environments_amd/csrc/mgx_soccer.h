@@ -144,11 +144,74 @@ __device__ __forceinline__ bool soccer_upright(const Env<T>& e, const SoccerIds<
   return R[8] > (T)0.7;
 }
 
+// numpy's np.linalg.norm of a float64 3-vector: sqrt of the BLAS dot, which rounds as two FMAs
+__device__ __forceinline__ double norm3_np(double x, double y, double z) { return sqrt(fma(z, z, fma(y, y, x * x))); }
+
+// numpy float32 add.reduce of the squared clipped actions (soccer_env.py:674): pairwise sum,
+// 8 accumulators over the first 8*floor(n/8) values, tree (01)(23) / (45)(67), then the tail
+__device__ __forceinline__ float np_sumsq_clip_f32(const float* action, int n) {
+#pragma clang fp contract(off)
+  auto sq = [&](int u) {
+    float a = action[u];
+    a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);
+    return a * a;
+  };
+  if (n < 8) {
+    float res = 0.0f;
+    for (int u = 0; u < n; u++) res += sq(u);
+    return res;
+  }
+  float r[8];
+  for (int k = 0; k < 8; k++) r[k] = sq(k);
+  int i = 8;
+  for (; i + 8 <= n; i += 8)
+    for (int k = 0; k < 8; k++) r[k] += sq(i + k);
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += sq(i);
+  return res;
+}
+
+// _calculate_reward (soccer_env.py:633-690) with the reference's numpy arithmetic, lane-uniform:
+// the reward is a Python float until an np.float64 term (approach / forward progress, from
+// np.linalg.norm) is added; the energy term -0.1 * np.sum(np.square(a)) is np.float32, so a
+// still-Python-float reward becomes float32 there (NEP 50) and a later np.float64 term (ball
+// progress) promotes it back. Positions enter as float64 whatever the physics precision.
+__device__ __forceinline__ double soccer_reward_np(bool goal_now, bool ball_contact, bool upright, const double* bp,
+                                                   const double* tx, const double* pb, const double* pr,
+                                                   float energy) {
+#pragma clang fp contract(off)
+  double r = 0.0;
+  bool is64 = false;
+  if (goal_now) r += 10000.0;
+  if (ball_contact) r += 1000.0;
+  double cur_bd = norm3_np(bp[0] - tx[0], bp[1] - tx[1], bp[2] - tx[2]);
+  double prev_bd = norm3_np(pb[0] - pr[0], pb[1] - pr[1], pb[2] - pr[2]);
+  if (cur_bd < prev_bd && cur_bd > 2.0) { r += 500.0 * (prev_bd - cur_bd); is64 = true; }
+  if (upright) r += 200.0;
+  double prev_gd = norm3_np(pr[0] - 24.5, pr[1] - 0.0, pr[2] - 0.0);
+  double cur_gd = norm3_np(tx[0] - 24.5, tx[1] - 0.0, tx[2] - 0.0);
+  if (cur_gd < prev_gd) { r += 100.0 * (prev_gd - cur_gd); is64 = true; }
+  const float eterm = -0.1f * energy;
+  if (is64) {
+    r += (double)eterm;
+    if (!upright) r += -1000.0;
+  } else {
+    float rf = (float)r + eterm;
+    if (!upright) rf += -1000.0f;
+    r = (double)rf;
+  }
+  double prev_bgd = norm3_np(pb[0] - 24.5, pb[1] - 0.0, pb[2] - 0.0);
+  double cur_bgd = norm3_np(bp[0] - 24.5, bp[1] - 0.0, bp[2] - 0.0);
+  if (cur_bgd < prev_bgd) r += 300.0 * (prev_bgd - cur_bgd);
+  return r;
+}
+
 // Post-physics: step count, obs, reward, termination, stats, prev snapshots
 template <typename T>
 __device__ __forceinline__ bool soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
                             uint8_t* goal_scored, T* prev_ball, T* prev_robot, T* stats, float* obs, double* reward,
                             uint8_t* terminated, uint8_t* truncated, uint8_t* flags = nullptr) {
+#pragma clang fp contract(off)
   int l = lane_id();
   int st = *step + 1;
   soccer_obs(m, e, ids, st, obs);
@@ -157,45 +220,30 @@ __device__ __forceinline__ bool soccer_post(const DevModel<T>& m, Env<T>& e, con
   bool goal_now = bp[0] > (T)24 && fabs(bp[1]) < (T)3.66 && bp[2] < (T)2.44;
   bool ball_contact = soccer_ball_contact(e, ids);
   bool upright = soccer_upright(e, ids);
-  // energy term: sum of squares of the clipped float32 action
-  float part = 0.0f;
-  for (int u = l; u < m.nu; u += 64) {
-    float a = action[u];
-    a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);
-    part += a * a;
-  }
-  float energy = wave_sum(part);
-  T r = 0;
-  bool gs = *goal_scored != 0;
-  if (goal_now) { r += (T)10000; gs = true; }
-  if (ball_contact) r += (T)1000;
-  T cur_bd = norm3v(bp[0] - tx[0], bp[1] - tx[1], bp[2] - tx[2]);
-  T prev_bd = norm3v(prev_ball[0] - prev_robot[0], prev_ball[1] - prev_robot[1], prev_ball[2] - prev_robot[2]);
-  if (cur_bd < prev_bd && cur_bd > (T)2) r += (T)500 * (prev_bd - cur_bd);
-  if (upright) r += (T)200;
-  T prev_gd = norm3v(prev_robot[0] - (T)24.5, prev_robot[1], prev_robot[2]);
-  T cur_gd = norm3v(tx[0] - (T)24.5, tx[1], tx[2]);
-  if (cur_gd < prev_gd) r += (T)100 * (prev_gd - cur_gd);
-  r += (T)-0.1 * (T)energy;
-  if (!upright) r += (T)-1000;
-  T prev_bgd = norm3v(prev_ball[0] - (T)24.5, prev_ball[1], prev_ball[2]);
-  T cur_bgd = norm3v(bp[0] - (T)24.5, bp[1], bp[2]);
-  if (cur_bgd < prev_bgd) r += (T)300 * (prev_bgd - cur_bgd);
+  const double bpd[3] = {(double)bp[0], (double)bp[1], (double)bp[2]};
+  const double txd[3] = {(double)tx[0], (double)tx[1], (double)tx[2]};
+  const double pbd[3] = {(double)prev_ball[0], (double)prev_ball[1], (double)prev_ball[2]};
+  const double prd[3] = {(double)prev_robot[0], (double)prev_robot[1], (double)prev_robot[2]};
+  const double r = soccer_reward_np(goal_now, ball_contact, upright, bpd, txd, pbd, prd,
+                                    np_sumsq_clip_f32(action, m.nu));
+  bool gs = (*goal_scored != 0) || goal_now;
   bool term = gs || (!upright && st > 100) ||
               (fabs(bp[0]) > (T)30 || fabs(bp[1]) > (T)20 || bp[2] < (T)-1 || bp[2] > (T)10) ||
               (fabs(tx[0]) > (T)30 || fabs(tx[1]) > (T)20 || tx[2] < (T)0 || tx[2] > (T)5);
   bool trunc = st >= ids.max_episode_steps;
-  // episode stats (soccer_env.py:718-730), then the prev_* snapshots (:444-446)
-  T bv = norm3v(e.qvel[ids.ball_dofadr], e.qvel[ids.ball_dofadr + 1], e.qvel[ids.ball_dofadr + 2]);
-  T dist = norm3v(tx[0] - prev_robot[0], tx[1] - prev_robot[1], tx[2] - prev_robot[2]);
+  // episode stats (soccer_env.py:640-662 in the reward, :718-730 after the flags), then the
+  // prev_* snapshots (:444-446)
+  double bv = norm3_np((double)e.qvel[ids.ball_dofadr], (double)e.qvel[ids.ball_dofadr + 1],
+                       (double)e.qvel[ids.ball_dofadr + 2]);
+  double dist = norm3_np(txd[0] - prd[0], txd[1] - prd[1], txd[2] - prd[2]);
   wsync();
   if (l == 0) {
     if (goal_now) stats[0] += 1;
     if (ball_contact) stats[1] += 1;
-    stats[2] += dist;
-    if (upright) stats[3] += m.timestep;
-    stats[4] = stats[4] > bv ? stats[4] : bv;
-    *reward = (double)r;
+    if (upright) stats[3] = (T)((double)stats[3] + (double)m.timestep);
+    stats[2] = (T)((double)stats[2] + dist);
+    stats[4] = (double)stats[4] >= bv ? stats[4] : (T)bv;
+    *reward = r;
     *terminated = term;
     *truncated = trunc;
     *goal_scored = gs;

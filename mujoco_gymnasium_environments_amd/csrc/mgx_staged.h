@@ -7,8 +7,8 @@
 //
 //   S1  k_soccer_rows   wave per slot   pre-logic, kinematics .. collision, constraint rows;
 //                                       B rows + row scalars -> HBM, carry -> HBM (27 KB LDS)
-//   S2  k_pgs_groups    16 lanes / slot PGS sweeps with B streamed from L2/MALL, v = B'f in
-//                                       registers (lane j holds dofs j, j+16, ...), 4 slots/wave
+//   S2  k_pgs_groups    8 lanes / slot PGS sweeps with B streamed from L2/MALL, v = B'f in
+//                                       registers (lane j holds dofs j, j+8, ...), 8 slots/wave
 //   S3  k_soccer_finish wave per env    qacc, checkAcc, Euler, post-logic, autoreset (7 KB LDS)
 //   S4  k_soccer_fixup  wave per listed env, monolithic: reset whose bank was not ready
 //
@@ -24,8 +24,10 @@
 
 namespace mgx {
 
-#define MGX_PGS_LPE 16         // lanes per slot in the solver kernel
 #define MGX_SCAL 5             // row scalars: b, f, R, 1/AR, AR/2
+// scalar layout per 4-row block (20 reals, 16-byte aligned): [b x4][f x4][R x4][1/AR x4][AR/2 x4],
+// so the solver reads each quantity of a block with one 16-byte LDS load
+#define MGX_SQ(k, i) (4 * (k) + (i))
 #define MGX_PGS_SPW 8          // solver: slots per wave (8 lanes each)
 enum { FIX_RESET = 2 };
 
@@ -35,7 +37,6 @@ struct Pipe {
   int N, R, S, maxE, dpl, nv;
   int carry_stride;    // reals per slot: carry_reals (64-aligned) + 5 * 64 registers
   int carryi_stride;   // ints per slot: carry_ints + 8
-  int brow;            // unused (dense-row width of earlier layouts)
   int bcap;            // reals per slot of group-compressed B: 32 + (max_nefc / 4) * (8 + 32 * ceil(nv / 8))
   size_t o_carry, o_carryi, o_ne, o_niter, o_k2list, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
   size_t o_bq, o_bv, o_ba, o_btime, o_bobs, o_bprev, o_bwind, o_bk, o_bep, o_bwarn, o_bseed;
@@ -298,7 +299,7 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
   wave_sum4(a31, a32, z0, z1);
   MGX_BSTAMP(10);
   if (l < 4) {
-    T* o = scal + (size_t)(r0 + l) * MGX_SCAL;
+    T* o = scal + (size_t)(r0 >> 2) * (4 * MGX_SCAL) + l;
     const T* rc = e.rowc + 4 * (r0 + l);
     T nn = l == 0 ? n0 : l == 1 ? n1 : l == 2 ? n2 : n3;
     if (rc[3] != 0) {
@@ -306,13 +307,13 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
       T aref = -rc[1] * dv - rc[2];   // mj_referenceConstraint
       T jar = dw - aref;
       T ad = nn + R;
-      o[0] = ds - aref;                 // b = J qacc_smooth - aref
-      o[1] = jar < 0 ? -jar / R : (T)0; // warmstart force (mj_constraintUpdate, pyramidal)
-      o[2] = R;
-      o[3] = (T)1 / ad;
-      o[4] = (T)0.5 * ad;               // the solver's cost change is delta * (delta * AR / 2 + res)
+      o[MGX_SQ(0, 0)] = ds - aref;                 // b = J qacc_smooth - aref
+      o[MGX_SQ(1, 0)] = jar < 0 ? -jar / R : (T)0; // warmstart force (mj_constraintUpdate, pyramidal)
+      o[MGX_SQ(2, 0)] = R;
+      o[MGX_SQ(3, 0)] = (T)1 / ad;
+      o[MGX_SQ(4, 0)] = (T)0.5 * ad;               // the solver's cost change is delta * (delta * AR / 2 + res)
     } else {
-      o[0] = 0; o[1] = 0; o[2] = 1; o[3] = 1; o[4] = (T)0.5;
+      o[MGX_SQ(0, 0)] = 0; o[MGX_SQ(1, 0)] = 0; o[MGX_SQ(2, 0)] = 1; o[MGX_SQ(3, 0)] = 1; o[MGX_SQ(4, 0)] = (T)0.5;
     }
   }
   // the block for the solver: [A10 A20 A21 A30 A31 A32 0 0] then, for each 8-dof group the
@@ -438,7 +439,8 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
 // on which slots share the wave (other slots only add masked no-op blocks / sweeps).
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+  // bound_ctrl: every source lane of these patterns is valid, so the mov folds into its add
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
 }
 // four independent 8-lane sums (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror); every lane of
 // the 8-lane group ends with the identical total
@@ -470,7 +472,7 @@ template <typename T, int EPL>
 struct PgsBlk {
   typename Vec4T<T>::type b[EPL];  // B of the block's 4 rows at this lane's dof j + 8d
   typename Vec4T<T>::type a0, a1;  // A10 A20 A21 A30 | A31 A32 - -
-  T q[4][4];                       // the rows' b, R, 1/AR, AR/2
+  typename Vec4T<T>::type qb, qR, qi, qh;  // the rows' b, R, 1/AR, AR/2
 };
 
 // f32: two values per v_pk_fma_f32
@@ -488,14 +490,11 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.a1 = pa[1];
 #pragma unroll
   for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t[1 + d] + 4 * j);
-  const T* q = sc + 4 * blk * MGX_SCAL;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    k.q[i][0] = q[i * MGX_SCAL + 0];
-    k.q[i][1] = q[i * MGX_SCAL + 2];
-    k.q[i][2] = q[i * MGX_SCAL + 3];
-    k.q[i][3] = q[i * MGX_SCAL + 4];
-  }
+  const V4* q = reinterpret_cast<const V4*>(sc + 4 * MGX_SCAL * blk);
+  k.qb = q[0];
+  k.qR = q[2];
+  k.qi = q[3];
+  k.qh = q[4];
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
 }
 
@@ -522,40 +521,48 @@ __device__ __forceinline__ void pgs_dots(const PgsBlk<float, EPL>& k, const floa
 
 template <typename T, int EPL>
 __device__ __forceinline__ void pgs_update(const PgsBlk<T, EPL>& k, T (&v)[EPL], T dl0, T dl1, T dl2, T dl3) {
+  // v += B' dl as four FMA chains per entry (one v_fmac each)
 #pragma unroll
-  for (int d = 0; d < EPL; d++) v[d] += dl0 * k.b[d].x + dl1 * k.b[d].y + dl2 * k.b[d].z + dl3 * k.b[d].w;
+  for (int d = 0; d < EPL; d++) {
+    T x = fma(dl0, k.b[d].x, v[d]);
+    x = fma(dl1, k.b[d].y, x);
+    x = fma(dl2, k.b[d].z, x);
+    v[d] = fma(dl3, k.b[d].w, x);
+  }
 }
 
 template <typename T, int EPL>
 __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], T* sc, int r0, bool ok0, T& impr) {
-  T* q0 = sc + r0 * MGX_SCAL;
+  typedef typename Vec4T<T>::type V4;
+  V4* qf = reinterpret_cast<V4*>(sc + r0 * MGX_SCAL + MGX_SQ(1, 0));
   // forces read here, not with the prefetch: a row's f must be its latest value
-  const T f0 = q0[1], f1 = q0[MGX_SCAL + 1], f2 = q0[2 * MGX_SCAL + 1], f3 = q0[3 * MGX_SCAL + 1];
+  const V4 f = *qf;
   T d0, d1, d2, d3;
   pgs_dots(k, v, d0, d1, d2, d3);
   // b + R f off the dependent chain
-  const T t0 = k.q[0][0] + k.q[0][1] * f0, t1 = k.q[1][0] + k.q[1][1] * f1;
-  const T t2 = k.q[2][0] + k.q[2][1] * f2, t3 = k.q[3][0] + k.q[3][1] * f3;
+  const T t0 = k.qb.x + k.qR.x * f.x, t1 = k.qb.y + k.qR.y * f.y;
+  const T t2 = k.qb.z + k.qR.z * f.z, t3 = k.qb.w + k.qR.w * f.w;
   oct_sum4(d0, d1, d2, d3);
   T dl0, dl1, dl2, dl3;
-#define MGX_PGS_ROW(I, DOT, DL)                                   \
+  V4 nfv;
+#define MGX_PGS_ROW(C, I, DOT, DL)                                \
   {                                                               \
-    const T fr = f##I, ai = k.q[I][2], hd = k.q[I][3];            \
+    const T fr = f.C, ai = k.qi.C, hd = k.qh.C;                   \
     T res = (DOT) + t##I;                                         \
     T fn = fmax(fr - res * ai, (T)0);                             \
     T delta = fn - fr;                                            \
     T change = delta * (delta * hd + res);                        \
     bool keep = !ok0 || change > (T)1e-10;                        \
-    T nf = keep ? fr : fn;                                        \
-    DL = nf - fr;                                                 \
+    DL = keep ? (T)0 : delta;                                     \
     impr -= keep ? (T)0 : change;                                 \
-    q0[(I) * MGX_SCAL + 1] = nf;                                  \
+    nfv.C = keep ? fr : fn;                                       \
   }
-  MGX_PGS_ROW(0, d0, dl0)
-  MGX_PGS_ROW(1, d1 + k.a0.x * dl0, dl1)
-  MGX_PGS_ROW(2, d2 + k.a0.y * dl0 + k.a0.z * dl1, dl2)
-  MGX_PGS_ROW(3, d3 + k.a0.w * dl0 + k.a1.x * dl1 + k.a1.y * dl2, dl3)
+  MGX_PGS_ROW(x, 0, d0, dl0)
+  MGX_PGS_ROW(y, 1, d1 + k.a0.x * dl0, dl1)
+  MGX_PGS_ROW(z, 2, d2 + k.a0.y * dl0 + k.a0.z * dl1, dl2)
+  MGX_PGS_ROW(w, 3, d3 + k.a0.w * dl0 + k.a1.x * dl1 + k.a1.y * dl2, dl3)
 #undef MGX_PGS_ROW
+  *qf = nfv;
   pgs_update(k, v, dl0, dl1, dl2, dl3);
 }
 
@@ -574,7 +581,7 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   const int nblk = ne >> 2;
   // LDS capacity in whole ring turns: nbcap3 = max_nefc / 4 rounded up to a multiple of 3
   const int nbcap = P.maxE / 4, nbcap3 = (nbcap + 2) / 3 * 3;
-  const int sstride = MGX_SCAL * 4 * nbcap3 + 1;
+  const int sstride = MGX_SCAL * 4 * nbcap3 + 4;  // 16-byte aligned per slot
   T* sc = reinterpret_cast<T*>(smem) + s * sstride;
   uint16_t* bt = reinterpret_cast<uint16_t*>(reinterpret_cast<T*>(smem) + MGX_PGS_SPW * sstride) + s * 8 * nbcap3;
   const size_t sl = (size_t)(slot >= 0 ? slot : 0);
@@ -601,10 +608,9 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
     pgs_load_block<T, EPL>(k, Bsl, sc, bt, b, j);
-    const T* qf = sc + 4 * b * MGX_SCAL + 1;
+    const T* qf = sc + 4 * b * MGX_SCAL + MGX_SQ(1, 0);
     bool ok = b < nblk;
-    T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[MGX_SCAL] : (T)0, f2 = ok ? qf[2 * MGX_SCAL] : (T)0,
-      f3 = ok ? qf[3 * MGX_SCAL] : (T)0;
+    T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[1] : (T)0, f2 = ok ? qf[2] : (T)0, f3 = ok ? qf[3] : (T)0;
     pgs_update(k, v, f0, f1, f2, f3);
   }
   T cpart = 0;
@@ -619,13 +625,13 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
       const T* qq = sc + 4 * b * MGX_SCAL;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const T* qi = qq + i * MGX_SCAL;
-        cpart += qi[1] * (qi[0] + (T)0.5 * (dd[i] + qi[2] * qi[1]));
+        const T fi = qq[MGX_SQ(1, i)];
+        cpart += fi * (qq[MGX_SQ(0, i)] + (T)0.5 * (dd[i] + qq[MGX_SQ(2, i)] * fi));
       }
     }
   }
   if (cpart > 0) {
-    for (int r = j; r < ne; r += 8) sc[r * MGX_SCAL + 1] = 0;
+    for (int r = j; r < ne; r += 8) sc[(r >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, r & 3)] = 0;
 #pragma unroll
     for (int d = 0; d < EPL; d++) v[d] = 0;
   }

@@ -32,6 +32,7 @@ __global__ void __launch_bounds__(64) k_step(DevModel<T> m, mgx_state s, mgx_fra
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   int l = lane_id();
   if (l == 0 && s.warning) s.warning[env] += warn;
+  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
   if (fr.xpos) for (int k = l; k < 3 * m.nbody; k += 64) ((T*)fr.xpos)[(size_t)env * 3 * m.nbody + k] = e.xpos[k];
   if (fr.xquat) for (int k = l; k < 4 * m.nbody; k += 64) ((T*)fr.xquat)[(size_t)env * 4 * m.nbody + k] = e.xquat[k];
   if (fr.subtree_com)

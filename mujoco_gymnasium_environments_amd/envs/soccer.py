@@ -140,7 +140,9 @@ class SoccerVectorEnv:
         self.stats = torch.zeros(N, 5, dtype=dt, device=dev)
         self.episode = torch.zeros(N, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(N, 2, dtype=torch.uint8, device=dev)
-        self.rollout = torch.zeros(N, 4, dtype=dt, device=dev)  # reward, terminated, truncated, steps
+        # running sums: reward, terminated, truncated, steps, nefc, PGS sweeps, nefc^2,
+        # sweeps * nefc^2 (include/mgx.h mgx_soccer_env.rollout)
+        self.rollout = torch.zeros(N, 8, dtype=torch.float64, device=dev)
         self.obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
         self.final_obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
         self.reward = torch.zeros(N, dtype=torch.float64, device=dev)

@@ -15,7 +15,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = ["mgx_api.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip"]
+SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip"]
+# per-translation-unit flags: the staged solver's FMA chains must not be SLP-packed (mgx_pgs.hip)
+SOURCE_FLAGS = {"mgx_pgs.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
            "mgx_bipedal.h", "mgx_dancing.h", "mgx_internal.h"]
 
@@ -45,7 +47,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(build_dir, src.replace(".hip", ".o"))
         objs.append(obj)
-        procs.append((src, subprocess.Popen([hipcc, *flags, "-c", "-o", obj, os.path.join(CSRC, src)],
+        procs.append((src, subprocess.Popen([hipcc, *flags, *SOURCE_FLAGS.get(src, []), "-c", "-o", obj,
+                                             os.path.join(CSRC, src)],
                                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
     for src, p in procs:
         _, err = p.communicate()

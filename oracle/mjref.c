@@ -1254,10 +1254,9 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
   memcpy(a, cw < c0 ? d->qacc_warmstart : d->qacc_smooth, sizeof(double) * nv);
   double cost = newton_cost(m, d, a, M, x, g);
   int iter = 0;
+  /* mj_solNewton's loop order [ext]: every iteration updates, then tests the scaled improvement
+     and the scaled gradient at the new point, so at least one iteration always runs */
   while (iter < m->iterations) {
-    double gn = 0;
-    for (int k = 0; k < nv; k++) gn += g[k] * g[k];
-    if (scale * sqrt(gn) < m->tolerance) break;
     /* H = M + J_A' D_A J_A, Cholesky (lower, in place) */
     memcpy(H, M, sizeof(double) * nv * nv);
     for (int r = 0; r < ne; r++) {
@@ -1327,7 +1326,9 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
     double improvement = scale * (cost - cnew);
     cost = cnew;
     iter++;
-    if (improvement < m->tolerance) break;
+    double gn = 0;
+    for (int k = 0; k < nv; k++) gn += g[k] * g[k];
+    if (improvement < m->tolerance || scale * sqrt(gn) < m->tolerance) break;
   }
   d->solver_niter[0] = iter;
   memcpy(d->qacc, a, sizeof(double) * nv);

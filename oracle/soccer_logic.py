@@ -87,41 +87,54 @@ class SoccerLogic:
         o.extend(np.clip(s["xpos"][t.goalkeeper][:2] / 15.0, -1, 1))
         return np.array(o, dtype=np.float32)
 
-    def post(self, s, action, step):
-        """Returns obs, reward, terminated, truncated; updates s['goal_scored'], prev_*, stats."""
+    def reward(self, s, action, ball_contact, upright):
+        """_calculate_reward (soccer_env.py:633-690) with the reference's own numpy arithmetic:
+        the reward starts as a Python float; the approach / progress terms are np.float64
+        (np.linalg.norm); the energy term is np.float32 (-0.1 * float32 pairwise sum), so a reward
+        that is still a Python float becomes float32 there (NEP 50), and a later np.float64 term
+        promotes it back. Updates goal_scored and the goals / contacts / time_upright stats."""
         t = self.t
-        obs = self.obs(s, step)
         robot, ball = s["xpos"][t.torso], s["xpos"][t.ball]
         r = 0.0
         if ball[0] > 24.0 and abs(ball[1]) < 3.66 and ball[2] < 2.44:
             r += 10000.0
             s["goal_scored"] = True
             s["stats"][0] += 1
-        bc = self.ball_contact(s)
-        if bc:
+        if ball_contact:
             r += 1000.0
             s["stats"][1] += 1
         cur = np.linalg.norm(ball - robot)
         prev = np.linalg.norm(s["prev_ball_pos"] - s["prev_robot_pos"])
         if cur < prev and cur > 2.0:
             r += 500.0 * (prev - cur)
-        up = self.upright(s)
-        if up:
+        if upright:
             r += 200.0
             s["stats"][3] += 0.02
         pg, cg = np.linalg.norm(s["prev_robot_pos"] - GOAL), np.linalg.norm(robot - GOAL)
         if cg < pg:
             r += 100.0 * (pg - cg)
-        r += -0.1 * float(np.sum(np.square(np.asarray(action, np.float32))))
-        if not up:
+        r += -0.1 * np.sum(np.square(np.asarray(action, np.float32)))
+        if not upright:
             r += -1000.0
         pb, cb = np.linalg.norm(s["prev_ball_pos"] - GOAL), np.linalg.norm(ball - GOAL)
         if cb < pb:
             r += 300.0 * (pb - cb)
+        return float(r)
+
+    def post(self, s, action, step):
+        """Returns obs, reward, terminated, truncated; updates s['goal_scored'], prev_*, stats
+        (soccer_env.py:420-446 order: obs, reward, termination, truncation, stats, prev_*)."""
+        t = self.t
+        obs = self.obs(s, step)
+        robot, ball = s["xpos"][t.torso], s["xpos"][t.ball]
+        bc = self.ball_contact(s)
+        up = self.upright(s)
+        r = self.reward(s, action, bc, up)
         term = bool(s["goal_scored"] or (not up and step > 100) or
                     abs(ball[0]) > 30.0 or abs(ball[1]) > 20.0 or ball[2] < -1.0 or ball[2] > 10.0 or
                     abs(robot[0]) > 30.0 or abs(robot[1]) > 20.0 or robot[2] < 0.0 or robot[2] > 5.0)
         trunc = step >= self.max_episode_steps
+        # _update_episode_stats :718-730
         s["stats"][2] += np.linalg.norm(robot - s["prev_robot_pos"])
         s["stats"][4] = max(s["stats"][4], np.linalg.norm(s["qvel"][t.ball_dofadr:t.ball_dofadr + 3]))
         s["prev_ball_pos"] = ball.copy()

@@ -2,7 +2,11 @@
 against the oracle's newton_solve (oracle/mjref.c), on the humanoid_soccer model with its
 solver switched to Newton (tolerance 1e-10, the option martial arts / assembly use:
 humanoid_martial_arts_env/assets/martial_arts_scene.xml:10). Newton converges to the unique
-minimiser, so the bars are tighter than PGS's: fp64 forces and qacc 1e-7 relative.
+minimiser, so the bars are tighter than PGS's: fp64 forces and qacc 1e-7 relative. At MuJoCo's
+default tolerance 1e-8 (construction_site.xml:10 keeps the default) both solvers stop early by
+the same rules (scaled improvement or scaled gradient after each update); the stopping iterate
+then depends on the line search (exact here, MuJoCo's ls_tolerance rule differs), so
+that case is held to 1e-4 relative on forces and qacc.
 The oracle Newton itself is checked against a 5000-sweep PGS solve in tools/newton_check.py
 (agreement 1e-12..1e-16 where PGS has converged)."""
 import copy
@@ -17,12 +21,12 @@ pytestmark = pytest.mark.gpu
 N = 8
 
 
-@pytest.fixture(scope="module")
-def newton_case(soccer_model):
+@pytest.fixture(scope="module", params=[1e-10, 1e-8])
+def newton_case(soccer_model, request):
     from mujoco_gymnasium_environments_amd import cabi
     m = copy.deepcopy(soccer_model)
     m.solver = 2
-    m.tolerance = 1e-10
+    m.tolerance = request.param
     packed = cabi.pack_model(m)
     return m, packed, oracle_states(packed, N, seed=11)
 
@@ -45,11 +49,16 @@ def test_newton_forward(newton_case, prec):
         assert int(dbg["nefc"][i][0]) == ne
         assert int(dbg["niter"][i][0]) >= 1 or ne == 0
         if prec == "f64":
-            assert _rel(dbg["efc_force"][i][:ne], o.efc_force[:ne]) < 1e-7, "efc_force"
-            assert _rel(dbg["qacc"][i], o.qacc) < 1e-7, "qacc"
-            assert _rel(dbg["qfrc_constraint"][i], o.qfrc_constraint) < 1e-7, "qfrc_constraint"
+            bar = 1e-7 if m.tolerance < 1e-9 else 1e-4
+            assert _rel(dbg["efc_force"][i][:ne], o.efc_force[:ne]) < bar, "efc_force"
+            assert _rel(dbg["qacc"][i], o.qacc) < bar, "qacc"
+            assert _rel(dbg["qfrc_constraint"][i], o.qfrc_constraint) < bar, "qfrc_constraint"
+            if m.tolerance < 1e-9:
+                assert abs(int(dbg["niter"][i][0]) - int(o.solver_niter[0])) <= 1, "niter"
         else:
-            assert _rel(dbg["qacc"][i], o.qacc) < 5e-3, "qacc"
+            # fp32 at tolerance 1e-8: the improvement / gradient rules fire a different iteration
+            # than in fp64 on these violent states (|qacc| up to 1e12), so the iterate differs more
+            assert _rel(dbg["qacc"][i], o.qacc) < (5e-3 if m.tolerance < 1e-9 else 1e-1), "qacc"
 
 
 @pytest.mark.parametrize("prec", ["f64", "f32"])
@@ -66,14 +75,17 @@ def test_newton_one_step(newton_case, prec):
     for i, st in enumerate(states):
         o = oracle_at(packed, st)
         o.step()
-        tol = 1e-8 if prec == "f64" else 2e-3
+        loose = m.tolerance > 1e-9
+        tol = (1e-6 if loose else 1e-8) if prec == "f64" else 2e-3
         assert np.max(np.abs(qpos[i] - o.qpos)) < tol * max(1, np.abs(o.qpos).max()), f"qpos env {i}"
         vscale = max(1.0, np.abs(o.qvel).max())
-        assert np.max(np.abs(qvel[i] - o.qvel)) < (1e-6 if prec == "f64" else 5e-2) * vscale, f"qvel env {i}"
+        vtol = (1e-4 if loose else 1e-6) if prec == "f64" else 5e-2
+        assert np.max(np.abs(qvel[i] - o.qvel)) < vtol * vscale, f"qvel env {i}"
 
 
 def test_newton_rollout_f64(newton_case):
-    """Zero-action settle from qpos0 with the Newton solver: 200 steps, drift < 1e-6."""
+    """Zero-action settle from qpos0 with the Newton solver: 200 steps, drift < 1e-6 (1e-4 at
+    tolerance 1e-8)."""
     import torch
     from mujoco_gymnasium_environments_amd.batch import PhysicsBatch
     from oracle.mjref import RefSim
@@ -86,7 +98,7 @@ def test_newton_rollout_f64(newton_case):
         o.step(1)
         worst = max(worst, float(np.max(np.abs(b.qpos[0].cpu().numpy() - o.qpos))))
     torch.cuda.synchronize()
-    assert worst < 1e-6, worst
+    assert worst < (1e-6 if m.tolerance < 1e-9 else 1e-4), worst
 
 
 def test_newton_rk4_rows_in_scratch(bipedal_model):
@@ -110,3 +122,20 @@ def test_newton_rk4_rows_in_scratch(bipedal_model):
         o = oracle_at(packed, st)
         o.step()
         assert np.max(np.abs(qpos[i] - o.qpos)) < 1e-6 * max(1, np.abs(o.qpos).max()), f"qpos env {i}"
+
+
+def test_task_kernels_reject_newton_models(soccer_model):
+    """The task kernels are compiled with the PGS solver: a Newton model handed to a task's
+    configure call is refused (MGX_E_UNSUPPORTED), never silently solved with PGS."""
+    import copy
+    import ctypes as C
+    from mujoco_gymnasium_environments_amd.batch import PhysicsBatch
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerTables
+    from mujoco_gymnasium_environments_amd.native import lib
+    m = copy.deepcopy(soccer_model)
+    m.solver = 2
+    for prec in ("f64", "f32"):
+        b = PhysicsBatch(m, 2, precision=prec)
+        ids = SoccerTables(m).ids_struct()
+        rc = lib().mgx_soccer_configure(b.native.handle, C.byref(ids))
+        assert rc < 0 and b"PGS" in lib().mgx_last_error()

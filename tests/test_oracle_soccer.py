@@ -2,8 +2,9 @@
 
 Golden vectors (tests/golden/*.npz) were produced by calling the reference's methods
 (soccer_env.py:454-716) on synthetic MjData-like state; see tests/golden/make_fixtures.py.
-Tolerances: observation float32 exact-or-1-ulp (atol 1e-6); reward atol 0.05 (the reference
-rounds the energy term through float32, soccer_env.py:674-675); flags and goalkeeper force exact.
+Tolerances: observation float32 exact-or-1-ulp (atol 1e-6); reward, episode stats, flags and the
+goalkeeper force exact (the oracle reproduces numpy's float32 energy term and type promotion,
+soccer_env.py:673-675).
 """
 import numpy as np
 import pytest
@@ -35,7 +36,7 @@ def state_from_golden(g, i, nb, nv):
              ctrl=np.zeros(33), qfrc_applied=np.zeros(nv), xfrc_applied=np.zeros((nb, 6)),
              wind_strength=float(g["wind_strength"][i]), wind_direction=g["wind_direction"][i].copy(),
              goal_scored=bool(g["goal_scored_in"][i]), prev_ball_pos=g["prev_ball_pos"][i].copy(),
-             prev_robot_pos=g["prev_robot_pos"][i].copy(), stats=np.zeros(5))
+             prev_robot_pos=g["prev_robot_pos"][i].copy(), stats=g["stats_in"][i].copy())
     s["qfrc_applied"][0] = g["qfrc_applied_in"][i]
     s["xfrc_applied"][4, :2] = g["xfrc_applied_in"][i]
     return s
@@ -59,7 +60,8 @@ def test_soccer_logic_matches_reference(soccer_model, tables, golden):
         np.testing.assert_array_equal(s["xfrc_applied"][4, :2], g["xfrc_applied_out"][i])
         obs, r, term, trunc, bc, up = L.post(s, a, int(g["current_step"][i]))
         np.testing.assert_allclose(obs, g["obs"][i], atol=1e-6, err_msg=f"obs {i}")
-        assert abs(r - g["reward"][i]) < 0.05, (i, r, g["reward"][i])
+        assert r == g["reward"][i], (i, r, g["reward"][i])
+        np.testing.assert_array_equal(s["stats"], g["stats_out"][i], err_msg=f"stats {i}")
         assert term == bool(g["terminated"][i]) and trunc == bool(g["truncated"][i]), i
         assert bc == bool(g["ball_contact"][i]) and up == bool(g["upright"][i]), i
         assert s["goal_scored"] == bool(g["goal_scored_out"][i]), i

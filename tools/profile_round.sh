@@ -14,9 +14,9 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps "$STEPS" --warmup 10 --no-cpu-baseline $BENCH_ARGS > "$OUT/bench_under_rocprof.json"
+  python3 "$R/bench.py" --steps "$STEPS" --warmup 10 --no-cpu-baseline --no-f64-line $BENCH_ARGS > "$OUT/bench_under_rocprof.json"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS > "$OUT/bench_pmc_fetch.json"
+  python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-f64-line $BENCH_ARGS > "$OUT/bench_pmc_fetch.json"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS > "$OUT/bench_pmc_write.json"
+  python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-f64-line $BENCH_ARGS > "$OUT/bench_pmc_write.json"
 python3 "$R/tools/summarize_profile.py" "$OUT" "$TAG"

@@ -7,7 +7,7 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS \
-  -d "$OUT" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline "${@:2}" > "$OUT/bench.json"
+  -d "$OUT" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-f64-line "${@:2}" > "$OUT/bench.json"
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
