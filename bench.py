@@ -18,7 +18,7 @@ step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obs
 obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
 
 --task mixed benchmarks BASELINE configs[4] over the tasks this build simulates (soccer,
-parkour, bipedal, dancing; the three Newton-solver tasks are not built yet): 1024 envs per task
+parkour, bipedal, dancing, martial arts; construction and assembly are not built yet): 1024 envs per task
 on one GPU, each task's fused step on its own HIP stream so the ragged models overlap on the
 chip; one step = one env step of every task; value = all tasks' env steps / wall time.
 
@@ -66,6 +66,9 @@ BIPEDAL_METRIC = "env steps/sec (whole node), bipedal_rescue 8192 envs/GPU (BASE
 # int32 task scalars + 3 hist, prev_jvel 23 (fp64), read the 20-move sequence (int32 + fp64),
 # obs 94, reward, flags
 DANCING_ALG_BYTES = 4 * (2 * 87 + 2 * 29 + 29 + 2 * 8 + 2 * 3 + 20 + 94) + 8 * (2 * 18 + 2 * 23 + 20 + 1) + 2
+# martial arts: r/w qpos 50 + qvel 47 + qacc_warmstart 47 and ctrl 28 (fp32), action 28, r/w 5 fp64
+# + 4 int32 task scalars, obs 113, reward, flags
+MARTIAL_ALG_BYTES = 4 * (2 * 144 + 2 * 28 + 28 + 2 * 4 + 113) + 8 * (2 * 5 + 1) + 2
 MIXED_METRIC = "env steps/sec (whole node), all tasks mixed, 1024 envs each on 1 MI355X (BASELINE configs[4])"
 
 
@@ -253,6 +256,7 @@ def bench_mixed(args, dev, world, rank, dist):
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout
     from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
     from mujoco_gymnasium_environments_amd.envs.dancing import DancingVectorEnv
+    from mujoco_gymnasium_environments_amd.envs.martial import MartialArtsVectorEnv
     from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv, action_limits
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     N = args.envs
@@ -270,6 +274,9 @@ def bench_mixed(args, dev, world, rank, dist):
                            lambda: (torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0, BIPEDAL_ALG_BYTES),
         "humanoid_dancing": (DancingVectorEnv(N, device=str(dev), precision=args.precision, seed=14, env_offset=off),
                              lambda: (torch.rand(N, 29, device=dev, generator=g) * 2 - 1) * 200.0, DANCING_ALG_BYTES),
+        "humanoid_martial_arts": (MartialArtsVectorEnv(N, device=str(dev), precision=args.precision, seed=15,
+                                                       env_offset=off),
+                                  lambda: torch.rand(N, 28, device=dev, generator=g) * 2 - 1, MARTIAL_ALG_BYTES),
     }
     streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
     pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
@@ -323,8 +330,7 @@ def bench_mixed(args, dev, world, rank, dist):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (uniform actions within each task's action_space, Philox reset draws)",
             "config": {"workload": "all tasks mixed, 1024 envs each on 1 GPU (BASELINE configs[4])",
-                       "tasks": list(tasks), "tasks_missing": ["humanoid_construction", "humanoid_martial_arts",
-                                                               "robotic_arm_assembly"],
+                       "tasks": list(tasks), "tasks_missing": ["humanoid_construction", "robotic_arm_assembly"],
                        "envs_per_task": N, "global_batch": N * len(tasks) * world,
                        "parallelism": f"dp{world} (env shards), one HIP stream per task",
                        "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},

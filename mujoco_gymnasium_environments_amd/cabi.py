@@ -17,7 +17,7 @@ P_F64 = C.POINTER(C.c_double)
 
 # (field, kind) in declaration order of mgx_model_desc
 _INT_SIZES = ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "npair", "nM", "nmaskword",
-              "solver", "integrator", "cone", "iterations", "efc_capacity", "con_capacity", "pad0"]
+              "solver", "integrator", "cone", "iterations", "efc_capacity", "con_capacity", "layout_flags"]
 _REAL_SCALARS = ["timestep", "tolerance", "impratio", "meaninertia"]
 _ARRAYS = [
     ("body_parentid", "i"), ("body_rootid", "i"), ("body_weldid", "i"), ("body_jntnum", "i"),
@@ -43,6 +43,9 @@ _ARRAYS = [
 ]
 _PTR = {"i": P_I32, "u": P_U32, "d": P_F64}
 _NP = {"i": np.int32, "u": np.uint32, "d": np.float64}
+
+
+MGX_KEEP_CVEL = 1  # mgx_model_desc.layout_flags (include/mgx.h)
 
 
 class MgxModelDesc(C.Structure):
@@ -109,6 +112,21 @@ class MgxParkourLogicIO(C.Structure):
                 ("truncated", C.c_void_p)]
 
 
+class MgxMartialIds(C.Structure):
+    _fields_ = [("torso", C.c_int32), ("right_hand", C.c_int32), ("left_hand", C.c_int32), ("right_foot", C.c_int32),
+                ("left_foot", C.c_int32), ("dummy1", C.c_int32), ("dummy2", C.c_int32), ("n_act", C.c_int32),
+                ("max_episode_steps", C.c_int32), ("pad0", C.c_int32), ("ctrl_scale", C.c_double * 32)]
+
+
+class MgxMartialEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["scal", "ints", "episode", "rollout"]]
+
+
+class MgxMartialLogicIO(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["qpos", "qvel", "xpos", "xquat", "cvel", "ctrl", "action", "obs", "reward",
+                                          "terminated", "truncated"]]
+
+
 class MgxBipedalIds(C.Structure):
     _fields_ = [("torso", C.c_int32), ("victims", C.c_int32 * 5), ("obs_qposadr", C.c_int32 * 26),
                 ("obs_dofadr", C.c_int32 * 26), ("root_x", C.c_int32), ("root_y", C.c_int32), ("root_z", C.c_int32),
@@ -173,7 +191,7 @@ class PackedModel:
                      ngeom=model.ngeom, npair=int(A["pair_geom"].shape[0]), nM=model.nM,
                      nmaskword=nmask, solver=model.solver, integrator=model.integrator,
                      cone=model.cone, iterations=model.iterations, efc_capacity=efc_capacity,
-                     con_capacity=con_capacity, pad0=0)
+                     con_capacity=con_capacity, layout_flags=int(getattr(model, "layout_flags", 0)))
         for k, v in sizes.items():
             setattr(d, k, int(v))
         d.timestep, d.tolerance = model.timestep, model.tolerance

@@ -391,11 +391,17 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged ? 1 : max_nefc);
   L.efc_blk = take(staged ? 1 : 2 * max_nefc);
   L.hess = (!staged && d->solver == 2) ? take(nv * nv) : 0;
+  // env logic that reads cvel after the step (martial arts, martial_arts_env.py:536-589) keeps
+  // it out of the union the constraint rows overwrite
+  const bool keep_cvel = !staged && (d->layout_flags & MGX_KEEP_CVEL);
+  if (keep_cvel) L.cvel = take(6 * nb);
   // union: phase A (kinematics .. collision) arrays, then B rows on top (all rows for the
   // monolithic kernel, one chunk of rows for the staged row builder)
   int u0 = p;
   L.xmat = take(9 * nb); L.xipos = take(3 * nb); L.ximat = take(9 * nb); L.cinert = take(10 * nb);
-  L.crb = take(10 * nb); L.cvel = take(6 * nb); L.cfrc = take(6 * nb); L.cdof_dot = take(6 * nv);
+  L.crb = take(10 * nb);
+  if (!keep_cvel) L.cvel = take(6 * nb);
+  L.cfrc = take(6 * nb); L.cdof_dot = take(6 * nv);
   L.xaxis = take(3 * nj); L.xanchor = take(3 * nj); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
   L.act_force = take(d->nu);
   // staged: per-body sums of cdof * (qacc_smooth | qacc_warmstart), built after the velocity

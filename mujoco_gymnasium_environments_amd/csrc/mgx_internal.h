@@ -9,6 +9,7 @@
 #include "../../include/mgx.h"
 #include "mgx_bipedal.h"
 #include "mgx_dancing.h"
+#include "mgx_martial.h"
 #include "mgx_parkour.h"
 #include "mgx_staged.h"
 
@@ -26,6 +27,8 @@ struct mgx_model {
   bool parkour_ok = false;
   mgx::ParkourIds<float> pkf;
   mgx::ParkourIds<double> pkd;
+  bool martial_ok = false;
+  mgx::MartialIds ma;
   bool bipedal_ok = false;
   mgx::BipedalIds bp;
   bool dancing_ok = false;

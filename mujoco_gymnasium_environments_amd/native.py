@@ -15,11 +15,12 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip"]
+SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip",
+           "mgx_martial.hip"]
 # per-translation-unit flags: the staged solver's FMA chains must not be SLP-packed (mgx_pgs.hip)
 SOURCE_FLAGS = {"mgx_pgs.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
-           "mgx_bipedal.h", "mgx_dancing.h", "mgx_internal.h"]
+           "mgx_bipedal.h", "mgx_dancing.h", "mgx_martial.h", "mgx_internal.h"]
 
 MGX_OK = 0
 MGX_F32 = 0
@@ -105,6 +106,13 @@ _SIGS = {
     "mgx_dancing_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxDancingEnv), _VP, _VP, C.c_uint64,
                            C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_dancing_logic_test": ([_VP, C.POINTER(cabi.MgxDancingLogicIO), C.POINTER(cabi.MgxDancingEnv), C.c_int, _VP],
+                               C.c_int),
+    "mgx_martial_configure": ([_VP, C.POINTER(cabi.MgxMartialIds)], C.c_int),
+    "mgx_martial_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxMartialEnv), _VP, _VP, _VP, _VP, _VP,
+                          _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_martial_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxMartialEnv), _VP, _VP, C.c_uint64,
+                           C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_martial_logic_test": ([_VP, C.POINTER(cabi.MgxMartialLogicIO), C.POINTER(cabi.MgxMartialEnv), C.c_int, _VP],
                                C.c_int),
 }
 EXPORTS = tuple(_SIGS)

@@ -65,3 +65,15 @@ def dancing_model():
 def dancing_packed(dancing_model):
     from mujoco_gymnasium_environments_amd import cabi
     return cabi.pack_model(dancing_model)
+
+
+@pytest.fixture(scope="session")
+def martial_model():
+    from mujoco_gymnasium_environments_amd.envs.martial import martial_model as load
+    return load()
+
+
+@pytest.fixture(scope="session")
+def martial_packed(martial_model):
+    from mujoco_gymnasium_environments_amd import cabi
+    return cabi.pack_model(martial_model)
