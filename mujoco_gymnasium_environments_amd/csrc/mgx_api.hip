@@ -595,8 +595,8 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 
 static int pgs_lds_bytes(const mgx_model* m) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
-  int nb3 = (m->Ls.max_nefc / 4 + 2) / 3 * 3;  // whole ring turns of 3 blocks
-  return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 4) * rb + MGX_PGS_SPW * nb3 * 16 + 64;
+  int nb3 = (m->Ls.max_nefc / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
+  return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 4) * rb + MGX_PGS_SPW * nb3 * 32 + 64;
 }
 
 template <typename T>

@@ -29,6 +29,7 @@ namespace mgx {
 // so the solver reads each quantity of a block with one 16-byte LDS load
 #define MGX_SQ(k, i) (4 * (k) + (i))
 #define MGX_PGS_SPW 8          // solver: slots per wave (8 lanes each)
+#define MGX_PGS_RING 3         // solver: register ring of 4-row blocks (RING - 1 in flight; 4 measured no faster)
 enum { FIX_RESET = 2 };
 
 // Workspace layout (byte offsets from base), computed on the host (mgx_soccer_workspace_bytes)
@@ -479,12 +480,12 @@ struct PgsBlk {
 typedef float mgx_f2 __attribute__((ext_vector_type(2)));
 
 template <typename T, int EPL>
-__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint16_t* bt, int blk,
+__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint32_t* bt, int blk,
                                                int j) {
   // the table entry of a block past the slot's end points at the zero group (A included);
   // every load is one 16-byte vector load at a table offset
   typedef typename Vec4T<T>::type V4;
-  const uint16_t* t = bt + 8 * blk;
+  const uint32_t* t = bt + 8 * blk;  // widened in LDS: no 16-bit extracts on the address path
   const V4* pa = reinterpret_cast<const V4*>(Bsl + t[0]);
   k.a0 = pa[0];
   k.a1 = pa[1];
@@ -579,17 +580,17 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   const int slot = (s < spn && idx < cnt) ? P.at<int>(P.o_k2list)[idx] : -1;
   const int ne = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;  // a multiple of 4
   const int nblk = ne >> 2;
-  // LDS capacity in whole ring turns: nbcap3 = max_nefc / 4 rounded up to a multiple of 3
-  const int nbcap = P.maxE / 4, nbcap3 = (nbcap + 2) / 3 * 3;
+  // LDS capacity in whole ring turns: nbcap3 = max_nefc / 4 rounded up to a multiple of the ring
+  const int nbcap = P.maxE / 4, nbcap3 = (nbcap + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;
   const int sstride = MGX_SCAL * 4 * nbcap3 + 4;  // 16-byte aligned per slot
   T* sc = reinterpret_cast<T*>(smem) + s * sstride;
-  uint16_t* bt = reinterpret_cast<uint16_t*>(reinterpret_cast<T*>(smem) + MGX_PGS_SPW * sstride) + s * 8 * nbcap3;
+  uint32_t* bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + MGX_PGS_SPW * sstride) + s * 8 * nbcap3;
   const size_t sl = (size_t)(slot >= 0 ? slot : 0);
   const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
   const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * P.maxE);
   for (int q = j; q < MGX_SCAL * 4 * nbcap3; q += 8) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
   // block table: the slot's blocks, then zero-group entries up to the capacity
-  for (int q = j; q < 8 * nbcap3; q += 8) bt[q] = q < 8 * nblk ? gbt[q] : (uint16_t)0;
+  for (int q = j; q < 8 * nbcap3; q += 8) bt[q] = q < 8 * nblk ? (uint32_t)gbt[q] : 0u;
   int nm = nblk;
   nm = max(nm, __shfl_xor(nm, 8));
   nm = max(nm, __shfl_xor(nm, 16));
@@ -598,7 +599,7 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   if (spw < 0) nbMax = nbcap;  // debug: sweep every block slot
   // whole ring turns (3 blocks): the sweep has no remainder path; the padding blocks are
   // zero-table blocks whose rows are masked (their LDS scalars zero-filled below)
-  const int nbRun = (nbMax + 2) / 3 * 3;
+  const int nbRun = (nbMax + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;
   const T* Bsl = P.at<T>(P.o_B) + sl * P.bcap;
   __syncthreads();
   // warmstart: v = B' f, dual cost, reset to zero if the cost is positive
@@ -649,19 +650,20 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
     nsweep++;
 #endif
     T impr = 0;
-    PgsBlk<T, EPL> R0, R1, R2;
-    pgs_load_block<T, EPL>(R0, Bsl, sc, bt, 0, j);
-    pgs_load_block<T, EPL>(R1, Bsl, sc, bt, 1, j);
+    PgsBlk<T, EPL> R[MGX_PGS_RING];
+#pragma unroll
+    for (int k = 0; k < MGX_PGS_RING - 1; k++) pgs_load_block<T, EPL>(R[k], Bsl, sc, bt, k, j);
     // full groups of 3 blocks (ring of 3, 2 ahead): no early exit inside, so every prefetch is
     // consumed on every path and the compiler cannot sink the loads next to their use. The
     // table has zero entries up to its capacity, so the look-ahead past nbMax reads zeros.
-    for (int b0 = 0; b0 < nbRun; b0 += 3) {
-      pgs_load_block<T, EPL>(R2, Bsl, sc, bt, b0 + 2, j);
-      pgs_block<T, EPL>(R0, v, sc, 4 * b0, act && b0 < nblk, impr);
-      pgs_load_block<T, EPL>(R0, Bsl, sc, bt, min(b0 + 3, nbcap3 - 1), j);
-      pgs_block<T, EPL>(R1, v, sc, 4 * (b0 + 1), act && b0 + 1 < nblk, impr);
-      pgs_load_block<T, EPL>(R1, Bsl, sc, bt, min(b0 + 4, nbcap3 - 1), j);
-      pgs_block<T, EPL>(R2, v, sc, 4 * (b0 + 2), act && b0 + 2 < nblk, impr);
+    for (int b0 = 0; b0 < nbRun; b0 += MGX_PGS_RING) {
+#pragma unroll
+      for (int k = 0; k < MGX_PGS_RING; k++) {
+        // the slot consumed last lands the block RING - 1 ahead, then block b0 + k is solved
+        pgs_load_block<T, EPL>(R[(k + MGX_PGS_RING - 1) % MGX_PGS_RING], Bsl, sc, bt,
+                               min(b0 + k + MGX_PGS_RING - 1, nbcap3 - 1), j);
+        pgs_block<T, EPL>(R[k], v, sc, 4 * (b0 + k), act && b0 + k < nblk, impr);
+      }
     }
     if (act) {
       it++;

@@ -1002,21 +1002,35 @@ static void make_constraint(const mgx_model_desc *m, ref_data *d) {
     jac(m, d, jp2, NULL, d->con_pos + 3 * c, b2);
     for (int k = 0; k < 3 * nv; k++) jd[k] = jp2[k] - jp1[k];
     double tran = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
-    /* contact-frame rows: cj[0] normal, cj[1..2] tangents */
+    double rot = m->body_invweight0[2 * b1 + 1] + m->body_invweight0[2 * b2 + 1];
+    /* contact-frame rows: cj[0] normal, cj[1..2] tangents (translational); cj[3] torsional,
+       cj[4..5] rolling (rotational Jacobian on the normal / tangents) for condim 4 and 6 */
     double *cj = jd + 3 * nv;
     for (int a = 0; a < 3; a++)
       for (int k = 0; k < nv; k++)
         cj[a * nv + k] = fr[3 * a] * jd[k] + fr[3 * a + 1] * jd[nv + k] + fr[3 * a + 2] * jd[2 * nv + k];
+    if (dim > 3) {
+      double *jr1 = cj + 6 * nv, *jr2 = jr1 + 3 * nv;
+      jac(m, d, jp1, jr1, d->con_pos + 3 * c, b1);
+      jac(m, d, jp2, jr2, d->con_pos + 3 * c, b2);
+      for (int k = 0; k < 3 * nv; k++) jr2[k] -= jr1[k];
+      for (int a = 0; a < 3; a++)
+        for (int k = 0; k < nv; k++)
+          cj[(3 + a) * nv + k] = fr[3 * a] * jr2[k] + fr[3 * a + 1] * jr2[nv + k] + fr[3 * a + 2] * jr2[2 * nv + k];
+    }
     if (dim == 1) {
       int r = add_row(d, C_CONTACT_FRICTIONLESS, c, d->con_dist[c], d->con_includemargin[c], tran);
       if (r < 0) return;
       memcpy(d->efc_J + (size_t)r * nv, cj, sizeof(double) * nv);
     } else {
-      for (int k = 1; k < 3; k++)
+      /* pyramid edges J_n +- mu_k J_k, k = 1 .. dim-1, in MuJoCo's order; diagApprox uses the
+         translational weight for the two sliding directions and the rotational one for spin
+         and rolling [ext] */
+      for (int k = 1; k < dim; k++)
         for (int sgn = 0; sgn < 2; sgn++) {
           double f = mu[k - 1];
           int r = add_row(d, C_CONTACT_PYRAMIDAL, c, d->con_dist[c], d->con_includemargin[c],
-                          tran + f * f * tran);
+                          tran + f * f * (k < 3 ? tran : rot));
           if (r < 0) return;
           double s = sgn ? -f : f;
           for (int q = 0; q < nv; q++) d->efc_J[(size_t)r * nv + q] = cj[q] + s * cj[k * nv + q];

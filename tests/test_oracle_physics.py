@@ -221,3 +221,72 @@ def test_box_resting_on_box_newton():
     s.forward()
     p.forward()
     np.testing.assert_allclose(s.qacc, p.qacc, atol=1e-6)
+
+
+def _sphere_on_plane(condim, friction):
+    xml = ('<mujoco><compiler angle="radian"/><option timestep="0.01" iterations="100" solver="Newton" '
+           'tolerance="1e-12" gravity="0 0 -10"/><worldbody><geom type="plane" size="5 5 0.1"/>'
+           f'<body pos="0 0 0.1"><freejoint/><geom type="sphere" size="0.1" mass="1" condim="{condim}" '
+           f'friction="{friction}"/></body></worldbody></mujoco>')
+    return sim_of(xml)
+
+
+@pytest.mark.parametrize("condim", [3, 4, 6])
+def test_torsional_friction_condim(condim):
+    """A sphere resting on a plane under a spin torque tau_z = 0.05: one contact point, so the
+    sliding rows cannot resist the spin; condim >= 4 adds the torsional pyramid edges
+    J_n +- mu_spin J_spin (rotational Jacobian on the normal), whose capacity mu_spin N = 5 N m
+    holds it. condim 3: w_z(0.5 s) = tau / I * t = 0.05 / (0.4 * 1 * 0.01) * 0.5 = 6.25."""
+    m, pk, s = _sphere_on_plane(condim, "1 0.5 0.001")
+    assert int(m.pair_condim[0]) == condim
+    np.testing.assert_allclose(m.pair_friction[0], [1, 1, 0.5, 0.001, 0.001])
+    for _ in range(20):  # settle
+        s.step()
+    s.xfrc_applied[6 + 5] = 0.05
+    for _ in range(50):
+        s.step()
+    wz = s.qvel[5]
+    if condim == 3:
+        assert abs(wz - 6.25) < 0.05, wz
+    else:
+        assert abs(wz) < 0.02, wz
+        assert int(s.nefc[0]) == 2 * (condim - 1)
+
+
+@pytest.mark.parametrize("condim", [3, 6])
+def test_rolling_friction_condim6(condim):
+    """A 1 N push at the sphere's centre: with sliding friction 1 (capacity 10 N) it rolls
+    without slipping at a = F / (m + I / r^2) = 1 / 1.4 (condim 3: v(0.5 s) = 0.357); the rolling
+    edges of condim 6 (mu_roll = 1 m, capacity 10 N m) hold the rotation, so it neither rolls
+    nor slides."""
+    m, pk, s = _sphere_on_plane(condim, "1 0.005 1")
+    for _ in range(20):
+        s.step()
+    s.xfrc_applied[6 + 0] = 1.0
+    for _ in range(50):
+        s.step()
+    vx = s.qvel[0]
+    if condim == 3:
+        assert abs(vx - 0.5 / 1.4) < 0.01, vx
+        assert abs(s.qvel[4] - vx / 0.1) < 0.1  # rolling: w_y = v / r
+    else:
+        assert abs(vx) < 0.01 and abs(s.qvel[4]) < 0.1, (vx, s.qvel[4])
+
+
+def test_position_servo_kp_and_forcerange():
+    """<position kp="200" ctrlrange="0 0.05" forcerange="-50 50">: force = kp (ctrl - q) after the
+    ctrl clamp, then the force clamp (complete_model.xml:271-272 pattern). ctrl 0.5 -> clamped to
+    0.05 -> force 200 * 0.05 = 10 at q = 0; with kp = 2000 the 100 N is clamped to 50."""
+    for kp, f_exp in ((200, 10.0), (2000, 50.0)):
+        xml = ('<mujoco><compiler angle="radian"/><option timestep="0.01" gravity="0 0 0" solver="PGS"/><worldbody>'
+               '<body><joint name="s" type="slide" axis="1 0 0"/><geom type="sphere" size="0.1" mass="2"/></body>'
+               f'</worldbody><actuator><position joint="s" kp="{kp}" ctrlrange="0 0.05" forcerange="-50 50"/>'
+               '</actuator></mujoco>')
+        m, pk, s = sim_of(xml)
+        s.ctrl[0] = 0.5
+        s.forward()
+        assert abs(s.actuator_force[0] - f_exp) < 1e-12
+        assert abs(s.qacc[0] - f_exp / 2.0) < 1e-9
+        s.qpos[0] = 0.02
+        s.forward()
+        assert abs(s.actuator_force[0] - min(50.0, kp * (0.05 - 0.02))) < 1e-12
