@@ -650,8 +650,12 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   if (d->nv > MGX_MAX_NV) return fail(MGX_E_CAPACITY, "nv > 64 not supported by the wave-per-env kernel");
   if (d->nbody > 4096 || (d->solver != 0 && d->solver != 2) || (d->integrator != 0 && d->integrator != 1))
     return fail(MGX_E_UNSUPPORTED, "this build implements PGS or Newton with Euler or RK4");
-  for (int p = 0; p < d->npair; p++)
-    if (d->pair_condim[p] != 1 && d->pair_condim[p] != 3) return fail(MGX_E_UNSUPPORTED, "condim must be 1 or 3");
+  bool condim13 = true;  // the staged row builder packs one contact per 4-row block
+  for (int p = 0; p < d->npair; p++) {
+    const int c = d->pair_condim[p];
+    if (c != 1 && c != 3 && c != 4 && c != 6) return fail(MGX_E_UNSUPPORTED, "condim must be 1, 3, 4 or 6");
+    condim13 = condim13 && (c == 1 || c == 3);
+  }
   mgx_model* m = new mgx_model();
   m->precision = precision;
   m->device = device;
@@ -673,7 +677,7 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024) m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false, true);
   // the staged soccer pipeline (register-ring solver) handles Euler models up to 192 rows
-  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS;
+  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS && condim13;
   m->Ls = make_layout(d, rb, max_ncon, m->staged_ok ? max_nefc : 4, 128, true);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;

@@ -538,11 +538,14 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
     for (int k = 0; k < m.nv; k++) row[k] = 0;
     row[m.jnt_dofadr[e.efc_id[r]]] = e.efc[8 * r + 1];
   }
-  // ---- contacts: 2*(condim-1) pyramid rows (condim 3) or 1 row (condim 1); lane = dof
+  // ---- contacts: 2*(condim-1) pyramid rows (condim 3, 4, 6) or 1 row (condim 1); lane = dof.
+  // Edge k (k = 1 .. condim-1) is J_n +- mu_k J_k with J_1, J_2 the sliding directions
+  // (translational Jacobian on the tangents), J_3 torsion (rotational on the normal), J_4, J_5
+  // rolling (rotational on the tangents), in MuJoCo's order [ext]
   for (int c = 0; c < e.ncon; c++) {
     int p = e.con_pair[c];
     int dim = m.pair_condim[p];
-    int nrow = dim == 1 ? 1 : 4;
+    int nrow = dim == 1 ? 1 : 2 * (dim - 1);
     if (nefc + nrow > L.max_nefc) { e.overflow |= 4; break; }
     int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
     int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
@@ -568,24 +571,35 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
       if (dim == 1) {
         e.Bm[nefc * e.Bs + l] = cj0;
       } else {
-        T cj1 = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
-        T cj2 = fr[6] * jd[0] + fr[7] * jd[1] + fr[8] * jd[2];
-        T mu0 = m.pair_friction[5 * p], mu1 = m.pair_friction[5 * p + 1];
-        e.Bm[(nefc + 0) * e.Bs + l] = cj0 + mu0 * cj1;
-        e.Bm[(nefc + 1) * e.Bs + l] = cj0 - mu0 * cj1;
-        e.Bm[(nefc + 2) * e.Bs + l] = cj0 + mu1 * cj2;
-        e.Bm[(nefc + 3) * e.Bs + l] = cj0 - mu1 * cj2;
+        T cj[6];
+        cj[1] = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
+        cj[2] = fr[6] * jd[0] + fr[7] * jd[1] + fr[8] * jd[2];
+        if (dim > 3) {
+          // relative angular motion: the rotational parts of the dof's motion subspace
+          T jr[3] = {0, 0, 0};
+          if (b2 > 0 && body_has_dof(m, b2, l)) { jr[0] += cd[0]; jr[1] += cd[1]; jr[2] += cd[2]; }
+          if (b1 > 0 && body_has_dof(m, b1, l)) { jr[0] -= cd[0]; jr[1] -= cd[1]; jr[2] -= cd[2]; }
+          cj[3] = fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2];
+          cj[4] = fr[3] * jr[0] + fr[4] * jr[1] + fr[5] * jr[2];
+          cj[5] = fr[6] * jr[0] + fr[7] * jr[1] + fr[8] * jr[2];
+        }
+        for (int k = 1; k < dim; k++) {
+          T mu = m.pair_friction[5 * p + k - 1];
+          e.Bm[(nefc + 2 * (k - 1)) * e.Bs + l] = cj0 + mu * cj[k];
+          e.Bm[(nefc + 2 * (k - 1) + 1) * e.Bs + l] = cj0 - mu * cj[k];
+        }
       }
     }
     if (l < nrow) {
       int r = nefc + l;
       T tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      T rot = m.body_invweight0[2 * b1 + 1] + m.body_invweight0[2 * b2 + 1];
       T f = dim == 1 ? (T)0 : m.pair_friction[5 * p + (l >> 1)];
       e.efc_type[r] = dim == 1 ? C_CONTACT_FRICTIONLESS : C_CONTACT_PYRAMIDAL;
       e.efc_id[r] = c;
       e.efc[8 * r + 7] = e.con_dist[c];
       e.efc_margin[r] = m.pair_margin[p] - m.pair_gap[p];
-      e.efc[8 * r + 2] = tran + f * f * tran;
+      e.efc[8 * r + 2] = tran + f * f * ((l >> 1) < 2 ? tran : rot);  // mj_diagApprox [ext]
     }
     nefc += nrow;
   }

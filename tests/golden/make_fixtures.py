@@ -832,6 +832,65 @@ def main_martial():
     np.savez_compressed(f"{HERE}/martial_envlogic.npz", **martial_envlogic_vectors(env, 600))
 
 
+# ------------------------------------------------------------------------------- construction / assembly
+class _Loaded(Exception):
+    """Raised by the MjData stub once a constructor has handed its model to MuJoCo."""
+
+
+def captured_model_xml(path, module_name, cls_name, **ctor_kw):
+    """Run the reference constructor until it calls MjModel.from_xml_string / from_xml_path and
+    return the MJCF it passes (the model input of the task, as MuJoCo would receive it)."""
+    import contextlib
+    import io
+    import tempfile
+    install_stubs()
+    mj = sys.modules["mujoco"]
+    seen = {}
+
+    class MjModel:
+        @staticmethod
+        def from_xml_string(xml):
+            seen["xml"] = xml
+            return FakeModel(mjcf.compile_xml(xml))
+
+        @staticmethod
+        def from_xml_path(p):
+            with open(p) as f:
+                return MjModel.from_xml_string(f.read())
+
+    def mjdata(m):
+        raise _Loaded()
+    mj.MjModel, mj.MjData = MjModel, mjdata
+    mod = load_module(path, module_name)
+    cls = getattr(mod, cls_name)
+    if hasattr(cls, "_generate_xml_files"):
+        # generators write next to the module; point them at a scratch directory instead
+        d = tempfile.mkdtemp()
+        gen = cls._generate_xml_files
+        cls._load_xml_models = lambda self: (gen(self, d), setattr(
+            self, "xml_string", open(os.path.join(d, "construction_site.xml")).read()))
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            cls(**ctor_kw)
+    except _Loaded:
+        pass
+    return seen["xml"]
+
+
+def main_models():
+    """Composed models of the two tasks not simulated yet (construction: _generate_site_xml,
+    construction_env.py:177-495; assembly: complete_model.xml loaded at assembly_env.py:46-54)."""
+    os.makedirs(f"{HERE}/xml", exist_ok=True)
+    xml = captured_model_xml(f"{REF}/humanoid_construction_env/construction_env.py", "ref_construction_env",
+                             "HumanoidConstructionEnv", render_mode=None)
+    with open(f"{HERE}/xml/humanoid_construction.xml", "w") as f:
+        f.write(xml)
+    xml = captured_model_xml(f"{REF}/robotic_arm_assembly_env/assembly_env.py", "ref_assembly_env",
+                             "RoboticArmAssemblyEnv", render_mode=None)
+    with open(f"{HERE}/xml/robotic_arm_assembly.xml", "w") as f:
+        f.write(xml)
+
+
 def main_dancing():
     install_stubs()
     denv = dancing_env()
@@ -859,6 +918,8 @@ def main():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "dancing":
         main_dancing()
+    elif len(sys.argv) > 1 and sys.argv[1] == "models":
+        main_models()
     elif len(sys.argv) > 1 and sys.argv[1] == "martial":
         main_martial()
     elif len(sys.argv) > 1 and sys.argv[1] == "soccer":

@@ -121,3 +121,36 @@ def test_martial_address_tables_and_free_joints(martial):
     np.testing.assert_array_equal(m.qpos0[7:14], [-2, 0, 0, 1, 0, 0, 0])
     np.testing.assert_array_equal(m.qpos0[15:22], [0, 0, 1.4, 1, 0, 0, 0])
     assert m.jnt_qposadr[_joint(m, "neck_pitch")] == 22
+
+
+def _golden(name):
+    with open("tests/golden/xml/" + name + ".xml") as f:
+        return mjcf.compile_xml(f.read())
+
+
+def test_construction_model_inventory():
+    """humanoid_construction (construction_env.py:177-495): RK4 + MuJoCo's default Newton solver,
+    dt 0.002; 11 free bodies + 32 hinges + 1 slide -> nv = 99, which exceeds the 64-lane
+    dof-per-lane kernels (the next step for this task)."""
+    m = _golden("humanoid_construction")
+    assert (m.nq, m.nv, m.nu, m.nbody, m.ngeom) == (110, 99, 33, 39, 55)
+    assert m.integrator == 1 and m.solver == 2 and m.timestep == 0.002
+    assert sorted(set(int(t) for t in m.jnt_type)) == [0, 2, 3]  # free, slide, hinge
+    assert np.isclose(m.tolerance, 1e-8) and m.iterations == 100
+
+
+def test_assembly_model_inventory():
+    """robotic_arm_assembly complete_model.xml: Euler + Newton, dt 0.002; 7 arm hinges + 2 gripper
+    slides + 9 free components (nv 63); 7 gear motors with force ranges and 2 position servos
+    kp 200 (:261-272); 18 explicit condim-6 gripper-pad pairs with friction (2, 1, 1) (:299-318)."""
+    m = _golden("robotic_arm_assembly")
+    assert (m.nq, m.nv, m.nu) == (72, 63, 9)
+    assert m.integrator == 0 and m.solver == 2 and m.timestep == 0.002
+    np.testing.assert_array_equal(m.actuator_gear[:3], [100, 100, 50])
+    np.testing.assert_array_equal(np.asarray(m.actuator_forcerange)[0], [-100, 100])
+    np.testing.assert_array_equal(m.actuator_gainprm[7], [200, 0, 0])
+    np.testing.assert_array_equal(m.actuator_biasprm[7], [0, -200, 0])
+    np.testing.assert_array_equal(np.asarray(m.actuator_ctrlrange)[7], [0, 0.05])
+    explicit = [k for k in range(len(m.pair_condim)) if m.pair_condim[k] == 6]
+    assert len(explicit) == 18
+    np.testing.assert_allclose(m.pair_friction[explicit[0]][:3], [2, 1, 1])

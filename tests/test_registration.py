@@ -1,0 +1,41 @@
+"""CPU: gymnasium's make / TimeLimit semantics for the registered ids (SURVEY §8f row 4;
+humanoid_soccer_env/__init__.py:18-26 registers 2500 steps while the class truncates at 5000)."""
+from mujoco_gymnasium_environments_amd.registration import REGISTRY, TimeLimit
+
+
+class _Counter:
+    """A fake env whose own truncation is at 5 steps and termination at step 7."""
+    def __init__(self):
+        self.t = 0
+
+    def reset(self, seed=None, options=None):
+        self.t = 0
+        return 0, {}
+
+    def step(self, a):
+        self.t += 1
+        return self.t, 1.0, self.t == 7, self.t >= 5, {}
+
+
+def test_time_limit_truncates_at_registered_steps():
+    env = TimeLimit(_Counter(), 3)
+    env.reset()
+    flags = [env.step(0)[3] for _ in range(4)]
+    assert flags == [False, False, True, True]
+    env.reset()
+    assert env.step(0)[3] is False  # reset zeroes the elapsed count
+
+
+def test_time_limit_keeps_inner_flags():
+    env = TimeLimit(_Counter(), 100)
+    env.reset()
+    out = [env.step(0) for _ in range(7)]
+    assert [o[3] for o in out] == [False, False, False, False, True, True, True]  # inner truncation
+    assert out[-1][2] is True  # termination passes through
+
+
+def test_registry_matches_reference_registrations():
+    assert REGISTRY['HumanoidSoccer-v0'][1] == 2500
+    assert REGISTRY['QuadrupedParkour-v0'][1] == REGISTRY['QuadrupedParkour-v1'][1] == 6000
+    assert REGISTRY['BipedalRescue-v0'][1] == 10000
+    assert REGISTRY['HumanoidDancing-v0'][1] == 3600
