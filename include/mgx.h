@@ -475,6 +475,75 @@ typedef struct mgx_martial_logic_io {
 int mgx_martial_logic_test(const mgx_model *m, const mgx_martial_logic_io *io, const mgx_martial_env *e, int n_env,
                            void *stream);
 
+/* ---- robotic_arm_assembly env logic fused with physics (Newton, Euler, 10 substeps) ------ */
+#define MGX_ASSEMBLY_NCOMP 9
+#define MGX_ASSEMBLY_OBS 110
+#define MGX_ASSEMBLY_MAX_GEOM 128
+/* Name lookups of the reference, resolved once on the host (robotic_arm_assembly_env/
+ * assembly_env.py): component bodies in assembly_sequence order (:47-50, :324-329), per-geom
+ * gripper-pad flag and component tag by substring (:299-322), the ee_site frame (:437-439),
+ * targets (:77-87), placement rewards (:340-353), the 0.95-scaled joint bounds (:410-414), the
+ * float32 action bounds (:150-151). */
+typedef struct mgx_assembly_ids {
+  int32_t comp_body[MGX_ASSEMBLY_NCOMP];
+  int32_t ee_body;                          /* body of 'ee_site' */
+  int32_t n_geom;                           /* <= MGX_ASSEMBLY_MAX_GEOM */
+  int32_t max_episode_steps;                /* 150000 (:36) */
+  int32_t substeps;                         /* mj_steps per env step: 10 (:37-39, :228) */
+  int32_t settle_steps;                     /* mj_steps in reset(): 10 (:186) */
+  int8_t geom_comp[MGX_ASSEMBLY_MAX_GEOM];  /* -1, or the first component whose name is a substring */
+  uint8_t geom_pad[MGX_ASSEMBLY_MAX_GEOM];  /* 1: name holds 'gripper' and 'pad' */
+  double ee_pos[3];                         /* site_pos of 'ee_site' in its body frame */
+  double targets[3 * MGX_ASSEMBLY_NCOMP];
+  double place_reward[MGX_ASSEMBLY_NCOMP];
+  double joint_low[7], joint_high[7];       /* limits x 0.95 as float64 products */
+  float action_low[9], action_high[9];
+} mgx_assembly_ids;
+
+/* Persistent per-env task state (device, env-major). */
+typedef struct mgx_assembly_env {
+  int32_t *ints;             /* [N][16] step_count, held (-1 | component), task phase (0 idle,
+                                1 pickup, 2 transport, 3 align, 4 insert), assembly-progress
+                                bit mask, status[9] (0 in_bin, 1 held, 2 assembled, 3 dropped,
+                                4 damaged), 3 spare */
+  double *cumulative;        /* [N] cumulative_reward */
+  int32_t *episode;          /* [N] episodes started (nullable) */
+  double *rollout;           /* [N][4] fp64 running sums: reward, terminated, truncated, env steps (nullable) */
+  const double *reset_qpos;  /* [nq] qpos0 with the home pose and the bin positions (:167-218) */
+} mgx_assembly_env;
+
+int mgx_assembly_configure(mgx_model *m, const mgx_assembly_ids *ids);
+
+/* One env step for N envs (assembly_env.py:220-250): np.clip to the action bounds, ctrl[0:7] =
+ * a[0:7], ctrl[7] = ctrl[8] = a[7] / 1000 (float32), 10 mj_steps (Newton, Euler), gripper-contact
+ * task state, reward [N] float64, termination / truncation, observation [N][110] float32.
+ * autoreset != 0: ended envs run reset() (10 settle steps) in the same launch. */
+int mgx_assembly_step(const mgx_model *m, const mgx_state *s, const mgx_assembly_env *e, const float *action,
+                      float *obs, double *reward, uint8_t *terminated, uint8_t *truncated, float *final_obs,
+                      int autoreset, int n_env, const uint8_t *env_mask, void *stream);
+
+/* reset() for masked envs (:162-218, deterministic): mj_resetData, reset_qpos, tracking state
+ * cleared, 10 mj_steps, observation. */
+int mgx_assembly_reset(const mgx_model *m, const mgx_state *s, const mgx_assembly_env *e, float *obs, int n_env,
+                       const uint8_t *env_mask, void *stream);
+
+/* Test hook: assembly env logic only (clip/ctrl, task state, reward, termination, obs) on
+ * caller-supplied frames and contact lists (no physics). */
+typedef struct mgx_assembly_logic_io {
+  const void *qpos, *qvel, *xpos, *xquat;  /* [N][nq] [N][nv] [N][nbody][3] [N][nbody][4] real */
+  const int32_t *ncon;                     /* [N] */
+  const int32_t *con_geom;                 /* [N][max_contacts][2] */
+  const void *con_dist;                    /* [N][max_contacts] real */
+  int32_t max_contacts, pad0;
+  void *ctrl;                              /* out [N][nu] real */
+  const float *action;                     /* [N][9] */
+  float *obs;                              /* [N][110] */
+  double *reward;
+  uint8_t *terminated, *truncated;
+} mgx_assembly_logic_io;
+int mgx_assembly_logic_test(const mgx_model *m, const mgx_assembly_logic_io *io, const mgx_assembly_env *e,
+                            int n_env, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

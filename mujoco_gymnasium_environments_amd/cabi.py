@@ -127,6 +127,30 @@ class MgxMartialLogicIO(C.Structure):
                                           "terminated", "truncated"]]
 
 
+ASSEMBLY_NCOMP = 9
+ASSEMBLY_MAX_GEOM = 128
+
+
+class MgxAssemblyIds(C.Structure):
+    _fields_ = [("comp_body", C.c_int32 * ASSEMBLY_NCOMP), ("ee_body", C.c_int32), ("n_geom", C.c_int32),
+                ("max_episode_steps", C.c_int32), ("substeps", C.c_int32), ("settle_steps", C.c_int32),
+                ("geom_comp", C.c_int8 * ASSEMBLY_MAX_GEOM), ("geom_pad", C.c_uint8 * ASSEMBLY_MAX_GEOM),
+                ("ee_pos", C.c_double * 3), ("targets", C.c_double * (3 * ASSEMBLY_NCOMP)),
+                ("place_reward", C.c_double * ASSEMBLY_NCOMP), ("joint_low", C.c_double * 7),
+                ("joint_high", C.c_double * 7), ("action_low", C.c_float * 9), ("action_high", C.c_float * 9)]
+
+
+class MgxAssemblyEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["ints", "cumulative", "episode", "rollout", "reset_qpos"]]
+
+
+class MgxAssemblyLogicIO(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("xpos", C.c_void_p), ("xquat", C.c_void_p),
+                ("ncon", C.c_void_p), ("con_geom", C.c_void_p), ("con_dist", C.c_void_p),
+                ("max_contacts", C.c_int32), ("pad0", C.c_int32), ("ctrl", C.c_void_p), ("action", C.c_void_p),
+                ("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p), ("truncated", C.c_void_p)]
+
+
 class MgxBipedalIds(C.Structure):
     _fields_ = [("torso", C.c_int32), ("victims", C.c_int32 * 5), ("obs_qposadr", C.c_int32 * 26),
                 ("obs_dofadr", C.c_int32 * 26), ("root_x", C.c_int32), ("root_y", C.c_int32), ("root_z", C.c_int32),

@@ -397,6 +397,57 @@ __device__ __forceinline__ int plane_box(const T* pp, const T* pm, const T* bp, 
   return cnt;
 }
 
+// cylinder support point in world direction d (oracle/mjref.c cyl_support)
+template <typename T>
+__device__ __forceinline__ void cyl_support(const T* yp, const T* ym, const T* ys, const T* d, T* q) {
+  T dl[3];
+  mulmatTvec3(dl, ym, d);
+  T rxy = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+  T sl[3] = {0, 0, dl[2] >= 0 ? ys[1] : -ys[1]};
+  if (rxy > minval<T>()) { sl[0] = ys[0] * dl[0] / rxy; sl[1] = ys[0] * dl[1] / rxy; }
+  mulmatvec3(q, ym, sl);
+  for (int k = 0; k < 3; k++) q[k] += yp[k];
+}
+
+template <typename T>
+__device__ __forceinline__ T cyl_sd_world(const T* yp, const T* ym, const T* ys, const T* w, T* ew) {
+  T tmp[3] = {w[0] - yp[0], w[1] - yp[1], w[2] - yp[2]}, pl[3], e[3];
+  mulmatTvec3(pl, ym, tmp);
+  T sd = cyl_sd(pl, ys[0], ys[1], e);
+  mulmatvec3(ew, ym, e);
+  return sd;
+}
+
+// cylinder (geom1) vs cylinder (geom2): fixed-point support search both ways, one contact
+// (oracle/mjref.c cyl_cyl)
+template <typename T>
+__device__ __forceinline__ int cyl_cyl(const T* ap, const T* am, const T* as, const T* bp, const T* bm, const T* bs,
+                                       T margin, Con<T>* out) {
+  T best = (T)1e30, bn[3] = {0, 0, 1}, bpos[3] = {0, 0, 0};
+  for (int side = 0; side < 2; side++) {
+    const T *fp = side ? bp : ap, *fm = side ? bm : am, *fs = side ? bs : as;
+    const T *sp = side ? ap : bp, *sm = side ? am : bm, *ss = side ? as : bs;
+    T q[3] = {sp[0], sp[1], sp[2]}, ew[3], d[3];
+    for (int it = 0; it < 4; it++) {
+      cyl_sd_world(fp, fm, fs, q, ew);
+      for (int k = 0; k < 3; k++) d[k] = -ew[k];
+      cyl_support(sp, sm, ss, d, q);
+      T sd = cyl_sd_world(fp, fm, fs, q, ew);
+      if (sd < best) {
+        best = sd;
+        for (int k = 0; k < 3; k++) {
+          bn[k] = side ? -ew[k] : ew[k];
+          bpos[k] = q[k] - (T)0.5 * sd * ew[k];
+        }
+      }
+    }
+  }
+  if (best > margin) return 0;
+  out->dist = best;
+  for (int k = 0; k < 3; k++) { out->n[k] = bn[k]; out->pos[k] = bpos[k]; }
+  return 1;
+}
+
 // Dispatch one candidate pair. Geom frames come from LDS.
 template <typename T>
 __device__ __forceinline__ int collide_pair(int t1, int t2, const T* p1, const T* m1, const T* s1, const T* p2, const T* m2,
@@ -433,6 +484,7 @@ __device__ __forceinline__ int collide_pair(int t1, int t2, const T* p1, const T
   if (t1 == GSPHERE && t2 == GCYLINDER) return sphere_cyl_core(p1, s1[0], p2, m2, s2, margin, out);
   if (t1 == GCAPSULE && t2 == GCYLINDER) return capsule_cyl(p1, m1, s1, p2, m2, s2, margin, out);
   if (t1 == GCYLINDER && t2 == GBOX) return cyl_box(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GCYLINDER && t2 == GCYLINDER) return cyl_cyl(p1, m1, s1, p2, m2, s2, margin, out);
   return 0;
 }
 

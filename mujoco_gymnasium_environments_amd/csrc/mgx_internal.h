@@ -33,6 +33,8 @@ struct mgx_model {
   mgx::BipedalIds bp;
   bool dancing_ok = false;
   mgx::DancingIds dn;
+  bool assembly_ok = false;
+  mgx_assembly_ids as;
   int npair;
   bool staged_ok = false;  // the staged soccer pipeline supports this model's capacities
 };

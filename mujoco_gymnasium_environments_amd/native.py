@@ -16,11 +16,13 @@ ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
 SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip",
-           "mgx_martial.hip"]
+           "mgx_martial.hip", "mgx_assembly.hip"]
 # per-translation-unit flags: the staged solver's FMA chains must not be SLP-packed (mgx_pgs.hip)
 SOURCE_FLAGS = {"mgx_pgs.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
            "mgx_bipedal.h", "mgx_dancing.h", "mgx_martial.h", "mgx_internal.h"]
+# task headers included by one translation unit only (so editing one rebuilds one object)
+TU_HEADERS = {"mgx_assembly.hip": ["mgx_assembly.h"]}
 
 MGX_OK = 0
 MGX_F32 = 0
@@ -33,10 +35,14 @@ class NativeError(RuntimeError):
 
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile libmgx.so for gfx950 in-tree (hipcc). Returns the library path."""
-    srcs = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "mgx.h")]
+    common = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "mgx.h")]
+
+    def deps(src):
+        return [os.path.join(CSRC, src)] + common + [os.path.join(CSRC, h) for h in TU_HEADERS.get(src, [])]
+
     if not force and os.path.exists(LIB_PATH):
         lib_t = os.path.getmtime(LIB_PATH)
-        if all(os.path.getmtime(s) <= lib_t for s in srcs):
+        if all(os.path.getmtime(d) <= lib_t for src in SOURCES for d in deps(src)):
             return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
@@ -48,6 +54,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(build_dir, src.replace(".hip", ".o"))
         objs.append(obj)
+        if not force and os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in deps(src)):
+            continue  # object newer than its source and headers
         procs.append((src, subprocess.Popen([hipcc, *flags, *SOURCE_FLAGS.get(src, []), "-c", "-o", obj,
                                              os.path.join(CSRC, src)],
                                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
@@ -114,6 +122,13 @@ _SIGS = {
                            C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_martial_logic_test": ([_VP, C.POINTER(cabi.MgxMartialLogicIO), C.POINTER(cabi.MgxMartialEnv), C.c_int, _VP],
                                C.c_int),
+    "mgx_assembly_configure": ([_VP, C.POINTER(cabi.MgxAssemblyIds)], C.c_int),
+    "mgx_assembly_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxAssemblyEnv), _VP, _VP, _VP, _VP, _VP,
+                           _VP, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_assembly_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxAssemblyEnv), _VP, C.c_int, _VP, _VP],
+                           C.c_int),
+    "mgx_assembly_logic_test": ([_VP, C.POINTER(cabi.MgxAssemblyLogicIO), C.POINTER(cabi.MgxAssemblyEnv), C.c_int,
+                                 _VP], C.c_int),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -711,6 +711,61 @@ static int cyl_box(const double *yp, const double *ym, const double *ys, const d
   return 1;
 }
 
+/* cylinder support point (world) in world direction d: the rim point on the side d leans to,
+ * the face centre when d is along the axis */
+static void cyl_support(const double *yp, const double *ym, const double *ys, const double *d, double *q) {
+  double dl[3];
+  mulmatTvec3(dl, ym, d);
+  double rxy = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+  double sl[3] = {0, 0, dl[2] >= 0 ? ys[1] : -ys[1]};
+  if (rxy > MINVAL) { sl[0] = ys[0] * dl[0] / rxy; sl[1] = ys[0] * dl[1] / rxy; }
+  mulmatvec3(q, ym, sl);
+  for (int k = 0; k < 3; k++) q[k] += yp[k];
+}
+
+/* signed distance of world point w to a cylinder geom; e = outward normal (world) */
+static double cyl_sd_world(const double *yp, const double *ym, const double *ys, const double *w, double *ew) {
+  double tmp[3] = {w[0] - yp[0], w[1] - yp[1], w[2] - yp[2]}, pl[3], e[3];
+  mulmatTvec3(pl, ym, tmp);
+  double sd = cyl_sd(pl, ys[0], ys[1], e);
+  mulmatvec3(ew, ym, e);
+  return sd;
+}
+
+/* cylinder (geom1) vs cylinder (geom2) [ext]: MuJoCo routes this pair through its general
+ * convex collider (one contact). Own restatement with the same one-contact semantics, built
+ * like cyl_box's support search: (a) the point of cylinder 2 deepest in cylinder 1, found by 4
+ * fixed-point steps q <- support_2(-n_1(q)) from cylinder 2's centre, normal = n_1 (out of 1);
+ * (b) the same with the roles swapped, normal = -n_2; the deeper candidate wins. The contact
+ * point sits half the depth back along the normal. */
+static int cyl_cyl(const double *ap, const double *am, const double *as, const double *bp, const double *bm,
+                   const double *bs, double margin, rcon *out) {
+  double best = 1e300, bn[3] = {0, 0, 1}, bpos[3] = {0, 0, 0};
+  for (int side = 0; side < 2; side++) {
+    /* side 0: points of B in A; side 1: points of A in B */
+    const double *fp = side ? bp : ap, *fm = side ? bm : am, *fs = side ? bs : as;  /* the SDF body */
+    const double *sp = side ? ap : bp, *sm = side ? am : bm, *ss = side ? as : bs;  /* the support body */
+    double q[3] = {sp[0], sp[1], sp[2]}, ew[3], d[3];
+    for (int it = 0; it < 4; it++) {
+      cyl_sd_world(fp, fm, fs, q, ew);
+      for (int k = 0; k < 3; k++) d[k] = -ew[k];
+      cyl_support(sp, sm, ss, d, q);
+      double sd = cyl_sd_world(fp, fm, fs, q, ew);
+      if (sd < best) {
+        best = sd;
+        for (int k = 0; k < 3; k++) {
+          bn[k] = side ? -ew[k] : ew[k];
+          bpos[k] = q[k] - 0.5 * sd * ew[k];
+        }
+      }
+    }
+  }
+  if (best > margin) return 0;
+  out->dist = best;
+  for (int k = 0; k < 3; k++) { out->n[k] = bn[k]; out->pos[k] = bpos[k]; }
+  return 1;
+}
+
 /* box (geom1) vs box (geom2): separating-axis test over 15 axes, then face clipping
  * (reference face vs incident face, up to 8 points) or one edge-edge contact. */
 static int clip_poly(double (*in)[2], int n, int axis, double lim, double sgn, double (*out)[2]) {
@@ -910,8 +965,8 @@ static int collide_geoms(const mgx_model_desc *m, ref_data *d, int g1, int g2, d
   if (t1 == GSPHERE && t2 == GCYLINDER) return sphere_cyl_core(p1, s1[0], p2, m2, s2, margin, out);
   if (t1 == GCAPSULE && t2 == GCYLINDER) return capsule_cyl(p1, m1, s1, p2, m2, s2, margin, out);
   if (t1 == GCYLINDER && t2 == GBOX) return cyl_box(p1, m1, s1, p2, m2, s2, margin, out);
-  return 0; /* unsupported pair types (plane-cylinder, cylinder-cylinder, ellipsoid): no task of
-               configs 1-4 has them */
+  if (t1 == GCYLINDER && t2 == GCYLINDER) return cyl_cyl(p1, m1, s1, p2, m2, s2, margin, out);
+  return 0; /* unsupported pair types (plane-cylinder, ellipsoid): no task has them */
 }
 
 static int add_contacts(const mgx_model_desc *m, ref_data *d, int pi, rcon *rc, int n) {

@@ -129,6 +129,7 @@ class FakeModel:
         self._c = c
         self.nu, self.nq, self.nv, self.nbody, self.ngeom = c.nu, c.nq, c.nv, c.nbody, c.ngeom
         self.jnt_qposadr = c.jnt_qposadr.copy()
+        self.body_jntadr = c.body_jntadr.copy()
         self.jnt_dofadr = c.jnt_dofadr.copy()
         self.jnt_range = c.jnt_range.copy()
         self.qpos0 = c.qpos0.copy()
@@ -162,6 +163,7 @@ class FakeData:
         self.xmat = np.tile(np.eye(3).reshape(-1), (c.nbody, 1))
         self.subtree_com = np.zeros((c.nbody, 3))
         self.cvel = np.zeros((c.nbody, 6))
+        self.site_xpos = np.zeros((len(c.site_names), 3))
         self.contact = []
         self.ncon = 0
         self.time = 0.0
@@ -891,6 +893,167 @@ def main_models():
         f.write(xml)
 
 
+def assembly_env():
+    """RoboticArmAssemblyEnv built by the reference constructor on the stubs (its reset() runs the
+    10 settle mj_steps as stub no-ops), complete_model.xml read from the reference's assets."""
+    import contextlib
+    import io
+    install_stubs()
+    mj = sys.modules["mujoco"]
+
+    class MjModel:
+        @staticmethod
+        def from_xml_path(p):
+            with open(p) as f:
+                return FakeModel(mjcf.compile_xml(f.read()))
+    mj.MjModel = MjModel
+    mod = load_module(f"{REF}/robotic_arm_assembly_env/assembly_env.py", "ref_assembly_env")
+    with contextlib.redirect_stdout(io.StringIO()):
+        env = mod.RoboticArmAssemblyEnv(render_mode=None)
+    return env
+
+
+def _assembly_site(c, xpos, xquat):
+    """site_xpos of every site from body frames (xmat = quat2mat(xquat)); the logic only reads
+    ee_site (assembly_env.py:437-439)."""
+    out = np.zeros((len(c.site_names), 3))
+    for s in range(len(c.site_names)):
+        b = int(c.site_bodyid[s])
+        R = mjcf.quat2mat(np.asarray(xquat[b], np.float64))
+        out[s] = xpos[b] + R @ c.site_pos[s]
+    return out
+
+
+def assembly_reset_vectors(env):
+    """reset() (assembly_env.py:162-218): mj_resetData, the home pose into qpos[0:7], every
+    component at its bin position with an identity quaternion; tracking state cleared. The 10
+    settle steps are stub no-ops here, so qpos is the state those steps start from."""
+    env.data.qpos[:] = 7.0  # garbage that mj_resetData must clear
+    obs, info = env.reset(seed=5)
+    return dict(qpos=env.data.qpos.copy(), nstep=np.int64(getattr(env.data, "nstep", 0)),
+                obs=obs, phase=np.int64(('idle', 'pickup', 'transport', 'align', 'insert').index(info['task_phase'])))
+
+
+def assembly_envlogic_vectors(env, n, seed=8642, max_contacts=12):
+    """Random synthetic states -> the reference's step() with mj_step stubbed out: clip, ctrl,
+    gripper-contact task state, reward, termination, truncation, observation, tracking state."""
+    c = env.model._c
+    rng = np.random.default_rng(seed)
+    seq = env.assembly_sequence
+    status_names = ['in_bin', 'held', 'assembled', 'dropped']
+    gnames = [c.id2name("geom", g) for g in range(c.ngeom)]
+    pads = [g for g, nme in enumerate(gnames) if nme and 'gripper' in nme and 'pad' in nme]
+    comp_geoms = [g for g, nme in enumerate(gnames) if nme and any(s in nme for s in seq)]
+    other = [g for g in range(c.ngeom) if g not in pads and g not in comp_geoms]
+    bodies = [c.name2id("body", s) for s in seq]
+    targets = env.component_targets
+    lo = np.array([-3.14, -2.36, -2.97, -3.14, -2.09, -3.14, -3.14])
+    hi = np.array([3.14, 0.78, 2.97, 3.14, 2.09, 3.14, 3.14])
+    cols = {k: [] for k in ("qpos", "qvel", "xpos", "xquat", "site_xpos", "ncon", "con_geom", "con_dist", "action",
+                            "step_in", "held_in", "phase_in", "status_in", "progress_in", "cum_in", "ctrl", "obs",
+                            "reward", "terminated", "truncated", "step_out", "held_out", "phase_out", "status_out",
+                            "progress_out", "cum_out")}
+    for i in range(n):
+        d = env.data
+        d.reset()
+        scen = i % 8
+        q = c.qpos0 + rng.normal(scale=0.3, size=c.nq)
+        q[0:7] = rng.uniform(lo * 0.9, hi * 0.9)
+        if scen == 0:  # one arm joint just past (or just inside) its 0.95 termination bound
+            j = int(rng.integers(0, 7))
+            q[j] = (hi[j] if rng.random() < 0.5 else lo[j]) * 0.95 * (1 + rng.choice([-1e-3, 1e-3]) * np.sign(hi[j]))
+        d.qpos[:] = q
+        d.qvel[:] = rng.normal(scale=rng.choice([0.01, 0.3, 3.0]), size=c.nv)
+        xpos = rng.uniform(-1, 1, (c.nbody, 3))
+        held_in = None if rng.random() < 0.4 else seq[int(rng.integers(0, 9))]
+        if held_in is not None and scen in (1, 2, 3):
+            # the held component near its target: inside the 2 mm assembly tolerance, inside
+            # the 5 cm precision band, or just outside it
+            r = {1: 0.0015, 2: 0.03, 3: 0.051}[scen] * rng.uniform(0.2, 1.0)
+            v = rng.normal(size=3)
+            xpos[bodies[seq.index(held_in)]] = np.asarray(targets[held_in]) + r * v / np.linalg.norm(v)
+        d.xpos[:] = xpos
+        qq = rng.normal(size=(c.nbody, 4))
+        d.xquat[:] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+        d.site_xpos = _assembly_site(c, d.xpos, d.xquat)
+        nc = int(rng.integers(0, max_contacts + 1)) if scen != 4 else 0
+        cons = []
+        for k in range(nc):
+            u = rng.random()
+            if u < 0.35:
+                g1, g2 = int(rng.choice(pads)), int(rng.choice(comp_geoms))
+            elif u < 0.5:
+                g1, g2 = int(rng.choice(pads)), int(rng.choice(other))
+            else:
+                g1, g2 = int(rng.integers(0, c.ngeom)), int(rng.integers(0, c.ngeom))
+            if rng.random() < 0.5:
+                g1, g2 = g2, g1
+            dist = float(rng.choice([rng.uniform(-0.002, 0.001), rng.uniform(-0.02, 0), rng.uniform(-0.2, 0)]))
+            cons.append(FakeContact(g1, g2, dist, [1, 0.5, 0.5]))
+        if scen == 5 and cons:
+            # one component only: the deterministic case of list(set(...))[0]
+            cg = int(rng.choice(comp_geoms))
+            for cn in cons:
+                if cn.geom1 in comp_geoms and cn.geom2 in pads:
+                    cn.geom1 = cg
+                elif cn.geom2 in comp_geoms and cn.geom1 in pads:
+                    cn.geom2 = cg
+        # keep only states whose touched-component set has at most one member (quirk A3: with
+        # two or more the reference's pick depends on PYTHONHASHSEED)
+        touched = set()
+        for cn in cons:
+            for ga, gb in ((cn.geom1, cn.geom2), (cn.geom2, cn.geom1)):
+                if ga in pads:
+                    for s in seq:
+                        if gnames[gb] and s in gnames[gb]:
+                            touched.add(s)
+                            break
+                    break
+        if len(touched) > 1:
+            cons = [cn for cn in cons if not (cn.geom1 in pads or cn.geom2 in pads)]
+        d.contact = cons
+        d.ncon = len(cons)
+        env.step_count = int(rng.choice([0, 1, 7, 149998, 149999, int(rng.integers(0, 200000))]))
+        env.held_component = held_in
+        env.task_phase = ('idle', 'pickup', 'transport', 'align', 'insert')[int(rng.integers(0, 5))]
+        prog = [bool(rng.random() < (0.97 if scen == 6 else 0.3)) for _ in seq]
+        env.assembly_progress = dict(zip(seq, prog))
+        st = [status_names[int(rng.integers(0, 4))] for _ in seq]
+        if held_in is not None:
+            st[seq.index(held_in)] = 'held'
+        env.component_status = dict(zip(seq, st))
+        env.cumulative_reward = float(rng.choice([0.0, rng.normal(scale=1e4)]))
+        action = (rng.uniform(-3, 3, 9) * np.array([1] * 7 + [50, 30])).astype(np.float32)
+        snap = dict(qpos=d.qpos.copy(), qvel=d.qvel.copy(), xpos=d.xpos.copy(), xquat=d.xquat.copy(),
+                    site_xpos=d.site_xpos.copy(), ncon=len(cons),
+                    con_geom=_pad(np.array([[cn.geom1, cn.geom2] for cn in cons], np.int64).reshape(-1, 2),
+                                  max_contacts, 2, -1),
+                    con_dist=_pad(np.array([cn.dist for cn in cons]), max_contacts),
+                    action=action, step_in=env.step_count,
+                    held_in=-1 if held_in is None else seq.index(held_in),
+                    phase_in=('idle', 'pickup', 'transport', 'align', 'insert').index(env.task_phase),
+                    status_in=np.array([status_names.index(s) for s in st]), progress_in=np.array(prog),
+                    cum_in=env.cumulative_reward)
+        obs, reward, term, trunc, info = env.step(action)
+        assert isinstance(reward, np.float64), type(reward)
+        out = dict(ctrl=d.ctrl.copy(), obs=obs, reward=float(reward), terminated=bool(term), truncated=bool(trunc),
+                   step_out=env.step_count,
+                   held_out=-1 if env.held_component is None else seq.index(env.held_component),
+                   phase_out=('idle', 'pickup', 'transport', 'align', 'insert').index(env.task_phase),
+                   status_out=np.array([status_names.index(env.component_status[s]) for s in seq]),
+                   progress_out=np.array([env.assembly_progress[s] for s in seq]),
+                   cum_out=float(env.cumulative_reward))
+        for k, v in {**snap, **out}.items():
+            cols[k].append(v)
+    return {k: np.asarray(v) for k, v in cols.items()}
+
+
+def main_assembly():
+    env = assembly_env()
+    np.savez_compressed(f"{HERE}/assembly_reset.npz", **assembly_reset_vectors(env))
+    np.savez_compressed(f"{HERE}/assembly_envlogic.npz", **assembly_envlogic_vectors(env, 600))
+
+
 def main_dancing():
     install_stubs()
     denv = dancing_env()
@@ -912,6 +1075,7 @@ def main():
     np.savez_compressed(f"{HERE}/bipedal_envlogic.npz", **bipedal_envlogic_vectors(benv, 600))
     main_dancing()
     main_martial()
+    main_assembly()
     print("fixtures written to", HERE)
 
 
@@ -922,6 +1086,8 @@ if __name__ == "__main__":
         main_models()
     elif len(sys.argv) > 1 and sys.argv[1] == "martial":
         main_martial()
+    elif len(sys.argv) > 1 and sys.argv[1] == "assembly":
+        main_assembly()
     elif len(sys.argv) > 1 and sys.argv[1] == "soccer":
         install_stubs()
         np.savez_compressed(f"{HERE}/soccer_envlogic.npz", **soccer_envlogic_vectors(soccer_env(), 400))

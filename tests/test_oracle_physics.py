@@ -196,6 +196,28 @@ def test_cylinder_box_cap_and_side():
     np.testing.assert_allclose(c["frame"][0][:3], [0, 0, 1], atol=1e-9)
 
 
+@pytest.mark.parametrize("psize,pos,rot,dist,normal", [
+    # short cylinder standing on the top cap (cap 0.6, probe bottom 0.695 - 0.1)
+    ("0.2 0.1", "1.1 2.1 0.695", "", 0.595 - 0.6, [0, 0, 1]),
+    # parallel axes side by side: axis distance 0.69 - radii 0.5 + 0.2
+    ("0.2 0.1", "1.69 2 0.3", "", 0.69 - 0.7, [1, 0, 0]),
+    # probe lying across the cap (axis along x): its lowest side line at 0.695 - 0.1
+    ("0.1 0.4", "1 2 0.695", 'euler="0 1.5707963267948966 0"', 0.595 - 0.6, [0, 0, 1]),
+    # separated beyond the margin: no contact
+    ("0.2 0.1", "1 2 0.8", "", None, None),
+])
+def test_cylinder_cylinder_known_answers(psize, pos, rot, dist, normal):
+    """cylinder (world geom, geom1) vs cylinder probe (geom2): one contact, normal from geom1 to
+    geom2 (oracle/mjref.c cyl_cyl; the pair assembly's screws and arm links form)."""
+    m, c = _cyl_contacts("cylinder", psize, pos, rot)
+    if dist is None:
+        assert len(c["dist"]) == 0
+        return
+    assert len(c["dist"]) == 1
+    assert abs(c["dist"][0] - dist) < 1e-9
+    np.testing.assert_allclose(c["frame"][0][:3], normal, atol=1e-9)
+
+
 def test_box_resting_on_box_newton():
     """Same rest state with the Newton solver (oracle/mjref.c newton_solve): the box settles,
     the contacts carry m g, and the converged qacc agrees with a long PGS solve of the same

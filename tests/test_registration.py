@@ -39,3 +39,4 @@ def test_registry_matches_reference_registrations():
     assert REGISTRY['QuadrupedParkour-v0'][1] == REGISTRY['QuadrupedParkour-v1'][1] == 6000
     assert REGISTRY['BipedalRescue-v0'][1] == 10000
     assert REGISTRY['HumanoidDancing-v0'][1] == 3600
+    assert REGISTRY['RoboticArmAssembly-v0'][1] == 150000
