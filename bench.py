@@ -18,7 +18,7 @@ step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obs
 obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
 
 --task mixed benchmarks BASELINE configs[4] over the tasks this build simulates (soccer,
-parkour, bipedal, dancing, martial arts; construction and assembly are not built yet): 1024 envs per task
+parkour, bipedal, dancing, martial arts, assembly; construction is not built yet): 1024 envs per task
 on one GPU, each task's fused step on its own HIP stream so the ragged models overlap on the
 chip; one step = one env step of every task; value = all tasks' env steps / wall time.
 
@@ -69,6 +69,9 @@ DANCING_ALG_BYTES = 4 * (2 * 87 + 2 * 29 + 29 + 2 * 8 + 2 * 3 + 20 + 94) + 8 * (
 # martial arts: r/w qpos 50 + qvel 47 + qacc_warmstart 47 and ctrl 28 (fp32), action 28, r/w 5 fp64
 # + 4 int32 task scalars, obs 113, reward, flags
 MARTIAL_ALG_BYTES = 4 * (2 * 144 + 2 * 28 + 28 + 2 * 4 + 113) + 8 * (2 * 5 + 1) + 2
+# assembly: r/w qpos 72 + qvel 63 + qacc_warmstart 63 and ctrl 9 (fp32), action 9, r/w 16 int32
+# task words + cumulative reward (fp64), obs 110, reward, flags
+ASSEMBLY_ALG_BYTES = 4 * (2 * 198 + 2 * 9 + 9 + 2 * 16 + 110) + 8 * (2 + 1) + 2
 MIXED_METRIC = "env steps/sec (whole node), all tasks mixed, 1024 envs each on 1 MI355X (BASELINE configs[4])"
 
 
@@ -254,6 +257,7 @@ def cpu_baseline_bipedal(n_envs: int, n_steps: int, seed: int = 0) -> dict:
 def bench_mixed(args, dev, world, rank, dist):
     """BASELINE configs[4]: every built task, N envs each, one HIP stream per task."""
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout
+    from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
     from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
     from mujoco_gymnasium_environments_amd.envs.dancing import DancingVectorEnv
     from mujoco_gymnasium_environments_amd.envs.martial import MartialArtsVectorEnv
@@ -264,6 +268,9 @@ def bench_mixed(args, dev, world, rank, dist):
     g = torch.Generator(device=dev)
     g.manual_seed(2000 + rank)
     plim = torch.as_tensor(action_limits(), dtype=torch.float32, device=dev)
+    # assembly action_space: [-2, 2]^7 joint commands, [0, 100] opening, [0, 50] force (:150-151)
+    alo = torch.tensor([-2.0] * 7 + [0.0, 0.0], device=dev)
+    alim = torch.tensor([4.0] * 7 + [100.0, 50.0], device=dev)
     tasks = {
         "humanoid_soccer": (SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=11, env_offset=off,
                                             banks=args.banks), lambda: torch.rand(N, 33, device=dev, generator=g) * 300 - 150,
@@ -277,6 +284,9 @@ def bench_mixed(args, dev, world, rank, dist):
         "humanoid_martial_arts": (MartialArtsVectorEnv(N, device=str(dev), precision=args.precision, seed=15,
                                                        env_offset=off),
                                   lambda: torch.rand(N, 28, device=dev, generator=g) * 2 - 1, MARTIAL_ALG_BYTES),
+        # assembly's reset is deterministic (assembly_env.py:162-218): no seed
+        "robotic_arm_assembly": (AssemblyVectorEnv(N, device=str(dev), precision=args.precision),
+                                 lambda: torch.rand(N, 9, device=dev, generator=g) * alim + alo, ASSEMBLY_ALG_BYTES),
     }
     streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
     pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
@@ -330,7 +340,7 @@ def bench_mixed(args, dev, world, rank, dist):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (uniform actions within each task's action_space, Philox reset draws)",
             "config": {"workload": "all tasks mixed, 1024 envs each on 1 GPU (BASELINE configs[4])",
-                       "tasks": list(tasks), "tasks_missing": ["humanoid_construction", "robotic_arm_assembly"],
+                       "tasks": list(tasks), "tasks_missing": ["humanoid_construction"],
                        "envs_per_task": N, "global_batch": N * len(tasks) * world,
                        "parallelism": f"dp{world} (env shards), one HIP stream per task",
                        "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},

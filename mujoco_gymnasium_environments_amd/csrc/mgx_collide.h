@@ -245,14 +245,14 @@ __device__ __forceinline__ int cyl_box(const T* yp, const T* ym, const T* ys, co
 }
 
 template <typename T>
-__device__ __forceinline__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T (*out)[2]) {
+__device__ __forceinline__ int clip_poly(T (*in)[2], int n, int axis, T lim, T sgn, T tol, T (*out)[2]) {
   int m = 0;
   for (int i = 0; i < n; i++) {
     T* P = in[i];
     T* Q = in[(i + 1) % n];
     T dp = sgn * P[axis] - lim, dq = sgn * Q[axis] - lim;
-    if (dp <= 0) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
-    if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+    if (dp <= tol) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
+    if ((dp < -tol && dq > tol) || (dp > tol && dq < -tol)) {
       T t = dp / (dp - dq);
       out[m][0] = P[0] + t * (Q[0] - P[0]);
       out[m][1] = P[1] + t * (Q[1] - P[1]);
@@ -271,6 +271,10 @@ __device__ __forceinline__ int box_box(const T* pa, const T* Ra, const T* ha, co
     for (int k = 0; k < 3; k++) { A[i][k] = Ra[3 * k + i]; B[i][k] = Rb[3 * k + i]; }
   T best_face = (T)-1e30, best_edge = (T)-1e30;
   int face_axis = -1, edge_i = -1, edge_j = -1;
+  // face-axis ties within ftol keep the earlier axis (oracle/mjref.c box_box)
+  T hmax = 0;
+  for (int k = 0; k < 3; k++) { hmax = ha[k] > hmax ? ha[k] : hmax; hmax = hb[k] > hmax ? hb[k] : hmax; }
+  const T ftol = (T)1e-6 * hmax;
   T edge_n[3] = {0, 0, 0};
   for (int ax = 0; ax < 6; ax++) {
     const T* n = ax < 3 ? A[ax] : B[ax - 3];
@@ -278,7 +282,7 @@ __device__ __forceinline__ int box_box(const T* pa, const T* Ra, const T* ha, co
     for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(A[k], n)); rb += hb[k] * fabs(dot3(B[k], n)); }
     T s = fabs(dot3(d, n)) - ra - rb;
     if (s > margin) return 0;
-    if (s > best_face) { best_face = s; face_axis = ax; }
+    if (s > best_face + ftol) { best_face = s; face_axis = ax; }
   }
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) {
@@ -343,11 +347,13 @@ __device__ __forceinline__ int box_box(const T* pa, const T* Ra, const T* ha, co
     poly[c][0] = dot3(rel, R[ru]);
     poly[c][1] = dot3(rel, R[rv]);
   }
+  // vertices within tol of a clip line count as on it (oracle/mjref.c box_box)
+  const T tol = (T)1e-5 * (hr[ru] > hr[rv] ? hr[ru] : hr[rv]);
   int np = 4;
-  np = clip_poly(poly, np, 0, hr[ru], (T)1, tmp);
-  np = clip_poly(tmp, np, 0, hr[ru], (T)-1, poly);
-  np = clip_poly(poly, np, 1, hr[rv], (T)1, tmp);
-  np = clip_poly(tmp, np, 1, hr[rv], (T)-1, poly);
+  np = clip_poly(poly, np, 0, hr[ru], (T)1, tol, tmp);
+  np = clip_poly(tmp, np, 0, hr[ru], (T)-1, tol, poly);
+  np = clip_poly(poly, np, 1, hr[rv], (T)1, tol, tmp);
+  np = clip_poly(tmp, np, 1, hr[rv], (T)-1, tol, poly);
   T fn[3];
   for (int k = 0; k < 3; k++) fn[k] = si * I[ii][k];
   T fndn = dot3(fn, nr);

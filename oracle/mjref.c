@@ -768,13 +768,13 @@ static int cyl_cyl(const double *ap, const double *am, const double *as, const d
 
 /* box (geom1) vs box (geom2): separating-axis test over 15 axes, then face clipping
  * (reference face vs incident face, up to 8 points) or one edge-edge contact. */
-static int clip_poly(double (*in)[2], int n, int axis, double lim, double sgn, double (*out)[2]) {
+static int clip_poly(double (*in)[2], int n, int axis, double lim, double sgn, double tol, double (*out)[2]) {
   int m = 0;
   for (int i = 0; i < n; i++) {
     double *P = in[i], *Q = in[(i + 1) % n];
     double dp = sgn * P[axis] - lim, dq = sgn * Q[axis] - lim;
-    if (dp <= 0) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
-    if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+    if (dp <= tol) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
+    if ((dp < -tol && dq > tol) || (dp > tol && dq < -tol)) {
       double t = dp / (dp - dq);
       out[m][0] = P[0] + t * (Q[0] - P[0]);
       out[m][1] = P[1] + t * (Q[1] - P[1]);
@@ -792,6 +792,11 @@ static int box_box(const double *pa, const double *Ra, const double *ha, const d
     for (int k = 0; k < 3; k++) { A[i][k] = Ra[3 * k + i]; B[i][k] = Rb[3 * k + i]; }
   double best_face = -1e30, best_edge = -1e30;
   int face_axis = -1, edge_i = -1, edge_j = -1;
+  /* face axes within ftol of the best keep the earlier one (box a before box b): equal
+   * separations of aligned boxes then pick the same reference face whatever the rounding */
+  double hmax = 0;
+  for (int k = 0; k < 3; k++) { hmax = ha[k] > hmax ? ha[k] : hmax; hmax = hb[k] > hmax ? hb[k] : hmax; }
+  const double ftol = 1e-6 * hmax;
   double edge_n[3] = {0, 0, 0};
   for (int ax = 0; ax < 6; ax++) {
     const double *n = ax < 3 ? A[ax] : B[ax - 3];
@@ -799,7 +804,7 @@ static int box_box(const double *pa, const double *Ra, const double *ha, const d
     for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(A[k], n)); rb += hb[k] * fabs(dot3(B[k], n)); }
     double s = fabs(dot3(d, n)) - ra - rb;
     if (s > margin) return 0;
-    if (s > best_face) { best_face = s; face_axis = ax; }
+    if (s > best_face + ftol) { best_face = s; face_axis = ax; }
   }
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) {
@@ -866,11 +871,15 @@ static int box_box(const double *pa, const double *Ra, const double *ha, const d
     poly[c][0] = dot3(rel, R[ru]);
     poly[c][1] = dot3(rel, R[rv]);
   }
+  /* vertices within tol of a clip line count as on it (inside, no intersection point): aligned
+   * faces of equal extent (the gripper fingers) then clip to the same polygon whatever the
+   * rounding of the coordinates */
+  const double tol = 1e-5 * (hr[ru] > hr[rv] ? hr[ru] : hr[rv]);
   int np = 4;
-  np = clip_poly(poly, np, 0, hr[ru], 1, tmp);
-  np = clip_poly(tmp, np, 0, hr[ru], -1, poly);
-  np = clip_poly(poly, np, 1, hr[rv], 1, tmp);
-  np = clip_poly(tmp, np, 1, hr[rv], -1, poly);
+  np = clip_poly(poly, np, 0, hr[ru], 1, tol, tmp);
+  np = clip_poly(tmp, np, 0, hr[ru], -1, tol, poly);
+  np = clip_poly(poly, np, 1, hr[rv], 1, tol, tmp);
+  np = clip_poly(tmp, np, 1, hr[rv], -1, tol, poly);
   /* depth of each clipped point: intersect the incident face plane along nr */
   double fn[3];
   for (int k = 0; k < 3; k++) fn[k] = si * I[ii][k];
