@@ -72,6 +72,7 @@ MARTIAL_ALG_BYTES = 4 * (2 * 144 + 2 * 28 + 28 + 2 * 4 + 113) + 8 * (2 * 5 + 1) 
 # assembly: r/w qpos 72 + qvel 63 + qacc_warmstart 63 and ctrl 9 (fp32), action 9, r/w 16 int32
 # task words + cumulative reward (fp64), obs 110, reward, flags
 ASSEMBLY_ALG_BYTES = 4 * (2 * 198 + 2 * 9 + 9 + 2 * 16 + 110) + 8 * (2 + 1) + 2
+ASSEMBLY_METRIC = "env steps/sec (whole node), robotic_arm_assembly 1024 envs/GPU (10 Newton substeps per env step)"
 MIXED_METRIC = "env steps/sec (whole node), all tasks mixed, 1024 envs each on 1 MI355X (BASELINE configs[4])"
 
 
@@ -254,6 +255,50 @@ def cpu_baseline_bipedal(n_envs: int, n_steps: int, seed: int = 0) -> dict:
             "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
 
 
+def cpu_baseline_assembly(n_envs: int, n_steps: int, seed: int = 0) -> dict:
+    """Oracle port on one host core: mjref (C, fp64, Newton) physics + numpy assembly logic."""
+    from mujoco_gymnasium_environments_amd import cabi
+    from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyTables, assembly_model
+    from oracle.assembly_logic import AssemblyLogic, AssemblyTables as OTables
+    from oracle.mjref import RefSim
+    m = assembly_model()
+    pk = cabi.pack_model(m)
+    tb = AssemblyTables(m)
+    L = AssemblyLogic(OTables(m))
+    rng = np.random.default_rng(seed)
+    lo = np.array([-2.0] * 7 + [0, 0])
+    hi = np.array([2.0] * 7 + [100, 50])
+    total = 0
+    t0 = time.perf_counter()
+    for e in range(n_envs):
+        sim = RefSim(pk)
+
+        def reset():
+            sim.reset()
+            sim.qpos[:] = tb.reset_qpos
+            sim.step(10)
+            return L.new_state()
+        s = reset()
+        for _ in range(n_steps):
+            a = rng.uniform(lo, hi).astype(np.float32)
+            _, ctrl = L.pre(a)
+            sim.ctrl[:] = ctrl
+            sim.step(10)
+            c = sim.contacts()
+            nc = int(sim.ncon[0])
+            _, _, term, trunc = L.post(s, sim.qpos, sim.qvel, sim.xpos.reshape(-1, 3), sim.xmat.reshape(-1, 9),
+                                       c["geom"][:nc], c["dist"][:nc])
+            total += 1
+            if term or trunc:
+                s = reset()
+    dt = time.perf_counter() - t0
+    return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of robotic_arm_assembly, uniform actions, "
+                      f"oracle/mjref.c fp64 Newton physics (10 substeps) + oracle/assembly_logic.py; CPU MuJoCo "
+                      f"unavailable (not installed)",
+            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+
+
 def bench_mixed(args, dev, world, rank, dist):
     """BASELINE configs[4]: every built task, N envs each, one HIP stream per task."""
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout
@@ -284,8 +329,9 @@ def bench_mixed(args, dev, world, rank, dist):
         "humanoid_martial_arts": (MartialArtsVectorEnv(N, device=str(dev), precision=args.precision, seed=15,
                                                        env_offset=off),
                                   lambda: torch.rand(N, 28, device=dev, generator=g) * 2 - 1, MARTIAL_ALG_BYTES),
-        # assembly's reset is deterministic (assembly_env.py:162-218): no seed
-        "robotic_arm_assembly": (AssemblyVectorEnv(N, device=str(dev), precision=args.precision),
+        # assembly's reset is deterministic (assembly_env.py:162-218): no seed; fp64 only (its
+        # degenerate base contact breaks the fp32 Newton factorisation, envs/assembly.py)
+        "robotic_arm_assembly": (AssemblyVectorEnv(N, device=str(dev), precision="f64"),
                                  lambda: torch.rand(N, 9, device=dev, generator=g) * alim + alo, ASSEMBLY_ALG_BYTES),
     }
     streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
@@ -344,6 +390,7 @@ def bench_mixed(args, dev, world, rank, dist):
                        "envs_per_task": N, "global_batch": N * len(tasks) * world,
                        "parallelism": f"dp{world} (env shards), one HIP stream per task",
                        "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},
+                       "task_dtype": {k: ("f64" if k == "robotic_arm_assembly" else args.precision) for k in tasks},
                        "bad_state_resets": int(acc[5].item())},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": f"{dom} step (dominant stream)",
@@ -403,12 +450,12 @@ def main():
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
     ap.add_argument("--no-f64-line", action="store_true", help="skip the fp64 parity-precision line (soccer)")
-    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed"])
+    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly"])
     args = ap.parse_args()
     if args.task != "soccer":
         args.mono = True  # one fused wave-per-env launch per step
     if args.envs <= 0:
-        args.envs = {"bipedal": 8192, "mixed": 1024}.get(args.task, 4096)
+        args.envs = {"bipedal": 8192, "mixed": 1024, "assembly": 1024}.get(args.task, 4096)
 
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     world, rank, local = world_from_env()
@@ -435,6 +482,13 @@ def main():
         from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
         env = BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
         pool = [((torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0).contiguous() for _ in range(16)]
+    elif args.task == "assembly":
+        from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
+        args.precision = "f64"  # fp64 only (envs/assembly.py)
+        env = AssemblyVectorEnv(N, device=str(dev), precision="f64")
+        alo = torch.tensor([-2.0] * 7 + [0.0, 0.0], device=dev)
+        alim = torch.tensor([4.0] * 7 + [100.0, 50.0], device=dev)
+        pool = [(torch.rand(N, 9, device=dev, generator=g) * alim + alo).contiguous() for _ in range(16)]
     else:
         from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
         env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
@@ -493,6 +547,28 @@ def main():
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_bipedal(max(1, args.cpu_envs // 8), args.cpu_steps // 10)
+        print(json.dumps(out))
+    elif rank == 0 and args.task == "assembly":
+        bytes_per_launch = ASSEMBLY_ALG_BYTES * N
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        out = {
+            "metric": ASSEMBLY_METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (uniform actions over action_space; deterministic reset)",
+            "config": {"workload": "robotic_arm_assembly_env, 1024 envs/GPU (BASELINE configs[4] task)",
+                       "envs_per_gpu": N, "global_batch": N * world, "parallelism": f"dp{world} (env shards)",
+                       "autoreset": "same-step (10 settle steps)", "substeps_per_step": 10, "solver": "Newton",
+                       "episodes_started": int(acc[1].item()), "terminated_total": int(acc[3].item()),
+                       "bad_state_resets": int(acc[5].item()), "capacity_overflow_steps": overflow_steps,
+                       "mean_reward": _finite(acc[2].item() / total_steps)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "mgx_assembly_step = k_assembly<T,0,GB>", "alg_bytes_per_step": bytes_per_launch,
+                         "launch_ms": round(launch_ms, 4)},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_assembly(2, max(5, args.cpu_steps // 2))
         print(json.dumps(out))
     elif rank == 0 and args.task == "parkour":
         bytes_per_launch = PARKOUR_ALG_BYTES * N

@@ -14,6 +14,12 @@ The model is the reference's complete_model.xml (assembly_env.py:53), compiled b
 nq 72, nv 63, nu 9, 28 bodies, 53 geoms (boxes and cylinders), 785 filtered candidate pairs +
 18 explicit condim-6 pad pairs. Under random actions it holds up to ~70 contacts / ~310
 constraint rows (oracle rollouts), hence the capacities below.
+
+Precision: the scene runs in fp64 only. Its arm base is degenerate in the reference model
+(base_plate and shoulder_pan_link interpenetrate coaxially: the contact's normal Jacobian is
+zero, diagApprox is zero, so R sits at mjMINVAL = 1e-15 and the rows carry ~1e17 forces,
+DESIGN.md §2). In fp32 the Newton Hessian I + D B B' with D = 1e15 overflows the factorisation
+and every substep ends in a bad-state reset, so ``precision="f32"`` is refused.
 """
 from __future__ import annotations
 
@@ -139,8 +145,11 @@ class AssemblyVectorEnv:
 
     metadata = {'render_modes': [], 'render_fps': 50}
 
-    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32",
+    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64",
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True):
+        if precision != "f64":
+            raise ValueError("robotic_arm_assembly runs in fp64 only: its degenerate base contact (R = 1e-15, "
+                             "~1e17 forces) breaks the fp32 Newton factorisation (module docstring)")
         self.num_envs = num_envs
         self.device = torch.device(device)
         self.model = assembly_model()
@@ -218,7 +227,7 @@ class RoboticArmAssemblyEnv(EnvBase):
     metadata = {'render_modes': ['human', 'rgb_array'], 'render_fps': 50}
 
     def __init__(self, render_mode: Optional[str] = None, config: Optional[Dict] = None, device: str = "cuda:0",
-                 precision: str = "f32"):
+                 precision: str = "f64"):
         super().__init__()
         self.render_mode = render_mode
         self.config = config or {}

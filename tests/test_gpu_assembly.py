@@ -296,9 +296,15 @@ def test_autoreset_and_final_obs():
     assert int(v.ints[0, 0]) == 0 and int(v.episode[0]) == 2
 
 
+def test_f32_refused():
+    from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
+    with pytest.raises(ValueError, match="fp64 only"):
+        AssemblyVectorEnv(2, precision="f32")
+
+
 def test_single_env_api():
     from mujoco_gymnasium_environments_amd.envs.assembly import RoboticArmAssemblyEnv
-    env = RoboticArmAssemblyEnv(render_mode="rgb_array", precision="f32")
+    env = RoboticArmAssemblyEnv(render_mode="rgb_array")
     obs, info = env.reset(seed=3)
     assert obs.shape == (110,) and obs.dtype == np.float32
     assert set(info) == {'step_count', 'assembly_progress', 'component_status', 'task_phase', 'held_component',
