@@ -212,11 +212,11 @@ __device__ __forceinline__ bool assembly_post(const DevModel<T>& m, Env<T>& e, c
   return done;
 }
 
-// reset() (:162-218): mj_resetData, qpos = reset_qpos (home pose + bins), tracking state
-// cleared, 10 mj_steps (ctrl 0), observation. Returns the bad-state resets of the settle steps.
+// reset() (:162-218), split around its 10 mj_steps so the task kernel keeps one physics call
+// site: the prologue runs mj_resetData, qpos = reset_qpos (home pose + bins) and clears the
+// tracking state; the epilogue writes the observation of the settled state.
 template <typename T>
-__device__ __forceinline__ int assembly_reset_body(const DevModel<T>& m, Env<T>& e, const mgx_assembly_ids& ids,
-                                                   mgx_assembly_env ae, int env, float* obs) {
+__device__ __forceinline__ void assembly_reset_prologue(const DevModel<T>& m, Env<T>& e, mgx_assembly_env ae, int env) {
   const int l = lane_id();
   reset_env(m, e);
   for (int k = l; k < m.nq; k += 64) e.qpos[k] = (T)ae.reset_qpos[k];
@@ -224,12 +224,14 @@ __device__ __forceinline__ int assembly_reset_body(const DevModel<T>& m, Env<T>&
   if (l < AI_N) st[l] = l == AI_HELD ? -1 : 0;
   if (l == 0) ae.cumulative[env] = 0.0;
   wsync();
-  int warn = 0;
-  for (int k = 0; k < ids.settle_steps; k++) warn += mj_step_env<T, false, true>(m, e);
+}
+
+template <typename T>
+__device__ __forceinline__ void assembly_reset_epilogue(const DevModel<T>& m, Env<T>& e, const mgx_assembly_ids& ids,
+                                                        int env, float* obs) {
   const int ncon = __builtin_amdgcn_readfirstlane(e.ncon);
   assembly_obs(m, e, ids, -1, AP_IDLE, 0, assembly_max_force(e, ncon), obs + (size_t)env * MGX_ASSEMBLY_OBS);
   wsync();
-  return warn;
 }
 
 }  // namespace mgx

@@ -20,20 +20,9 @@ __device__ __forceinline__ void bind(const DevModel<T>& m, Env<T>& e, char* smem
   env_bind<T, GB>(m, e, smem, GB ? (T*)s.scratch + (size_t)env * m.L.gB_stride : nullptr);
 }
 
-template <typename T>
-__device__ __forceinline__ void reset_and_store(const DevModel<T>& m, Env<T>& e, const mgx_assembly_ids& ids,
-                                                const mgx_state& s, mgx_assembly_env ae, float* obs, int env) {
-  const int warn = assembly_reset_body(m, e, ids, ae, env, obs);
-  store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
-              (T*)s.time, env);
-  if (lane_id() == 0) {
-    if (s.warning) s.warning[env] += warn;
-    if (s.overflow && e.overflow) s.overflow[env] += 1;
-    if (ae.episode) ae.episode[env] += 1;
-  }
-}
-
-// MODE 0: one env step (+ same-step autoreset); MODE 1: reset
+// MODE 0: one env step (10 substeps; ended envs then reset in the same launch when autoreset);
+// MODE 1: reset. ONE physics call site: the step's substeps and a reset's settle steps share
+// the loop below, so the Newton forward pass is inlined once.
 template <typename T, int MODE, bool GB>
 __global__ void __launch_bounds__(64) k_assembly(DevModel<T> m, mgx_assembly_ids ids, mgx_state s, mgx_assembly_env ae,
                                                  const float* action, float* obs, double* reward, uint8_t* terminated,
@@ -49,31 +38,40 @@ __global__ void __launch_bounds__(64) k_assembly(DevModel<T> m, mgx_assembly_ids
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  if (MODE == 1) {
-    reset_and_store(m, e, ids, s, ae, obs, env);
-    return;
-  }
-  assembly_pre(m, e, ids, action + (size_t)env * 9);
+  bool resetting = MODE == 1;
+  if (MODE == 1) assembly_reset_prologue(m, e, ae, env);
+  else assembly_pre(m, e, ids, action + (size_t)env * 9);
   int warn = 0;
-  for (int k = 0; k < ids.substeps; k++) warn += mj_step_env<T, false, true>(m, e);  // assembly_env.py:228-229
-  const bool done = assembly_post(m, e, ids, ae, env, obs, reward, terminated, truncated);
-  if (ae.rollout && l == 0) {
-    double* ro = ae.rollout + 4 * (size_t)env;
-    ro[0] += reward[env];
-    ro[1] += terminated[env];
-    ro[2] += truncated[env];
-    ro[3] += 1.0;
-  }
-  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  if (l == 0 && s.warning) s.warning[env] += warn;
-  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
-  if (done && autoreset) {
+  for (;;) {
+    const int nsteps = resetting ? ids.settle_steps : ids.substeps;  // assembly_env.py:186 / :228-229
+#pragma clang loop unroll(disable)
+    for (int k = 0; k < nsteps; k++) warn += mj_step_env<T, false, true>(m, e);
+    if (resetting) {
+      assembly_reset_epilogue(m, e, ids, env, obs);
+      if (l == 0 && ae.episode) ae.episode[env] += 1;
+      break;
+    }
+    const bool done = assembly_post(m, e, ids, ae, env, obs, reward, terminated, truncated);
+    if (ae.rollout && l == 0) {
+      double* ro = ae.rollout + 4 * (size_t)env;
+      ro[0] += reward[env];
+      ro[1] += terminated[env];
+      ro[2] += truncated[env];
+      ro[3] += 1.0;
+    }
+    if (!(done && autoreset)) break;
     if (final_obs)
       for (int i = l; i < MGX_ASSEMBLY_OBS; i += 64)
         final_obs[(size_t)env * MGX_ASSEMBLY_OBS + i] = obs[(size_t)env * MGX_ASSEMBLY_OBS + i];
     __threadfence();
     wsync();
-    reset_and_store(m, e, ids, s, ae, obs, env);
+    assembly_reset_prologue(m, e, ae, env);
+    resetting = true;
+  }
+  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  if (l == 0) {
+    if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
   }
 }
 

@@ -244,20 +244,25 @@ __device__ __forceinline__ void bipedal_philox_draws(uint64_t seed, uint32_t gen
   }
 }
 
-// reset(): mj_resetData, tracking reset, _randomize_initial_state, 10 settle mj_step's, obs,
-// prev_robot_pos. The _prev_* / _fall_timer attributes are left alone (quirk B3).
-template <typename T, bool RK>
-__device__ __forceinline__ int bipedal_reset_body(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, const T* draws,
-                                                  mgx_bipedal_env be, int env, float* obs) {
-  reset_env(m, e);
+// reset() (rescue_env.py:373-414), split around its 10 settle mj_step's (:390-391) so the task
+// kernel keeps one physics call site: the prologue runs mj_resetData, the tracking reset and
+// _randomize_initial_state from the 12 draws (read before the physics reuses the LDS); the
+// epilogue writes the observation and prev_robot_pos. The _prev_* / _fall_timer attributes are
+// left alone (quirk B3).
+template <typename T>
+__device__ __forceinline__ void bipedal_reset_prologue(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids,
+                                                       const T* draws, mgx_bipedal_env be, int env) {
   int l = lane_id();
+  T d[12];
+  for (int j = 0; j < 12; j++) d[j] = draws[j];  // uniform reads: every lane holds all 12 in registers
+  reset_env(m, e);
   if (l == 0) {
-    e.qpos[ids.root_x] = draws[0];
-    e.qpos[ids.root_y] = draws[1];
+    e.qpos[ids.root_x] = d[0];
+    e.qpos[ids.root_y] = d[1];
     e.qpos[ids.root_z] = (T)1.2;
     for (int i = 0; i < 5; i++) {
-      e.qpos[ids.victim_x[i]] = e.qpos[ids.victim_x[i]] + draws[2 + 2 * i];
-      e.qpos[ids.victim_y[i]] = e.qpos[ids.victim_y[i]] + draws[3 + 2 * i];
+      e.qpos[ids.victim_x[i]] = e.qpos[ids.victim_x[i]] + d[2 + 2 * i];
+      e.qpos[ids.victim_y[i]] = e.qpos[ids.victim_y[i]] + d[3 + 2 * i];
     }
     be.step[env] = 0;
     be.energy[env] = 1000.0f;
@@ -273,12 +278,15 @@ __device__ __forceinline__ int bipedal_reset_body(const DevModel<T>& m, Env<T>& 
     be.collisions[env] = 0;
   }
   wsync();
-  int warn = 0;
-  for (int k = 0; k < 10; k++) warn += mj_step_env<T, RK>(m, e);  // rescue_env.py:390-391
+}
+
+template <typename T>
+__device__ __forceinline__ void bipedal_reset_epilogue(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids,
+                                                       mgx_bipedal_env be, int env, float* obs) {
+  int l = lane_id();
   bipedal_obs(m, e, ids, 0, 0, 0, 1000.0f, obs + (size_t)env * 102);
   if (l < 3) be.prev_robot_pos[3 * (size_t)env + l] = (double)e.xpos[3 * ids.torso + l];
   wsync();
-  return warn;
 }
 
 }  // namespace mgx

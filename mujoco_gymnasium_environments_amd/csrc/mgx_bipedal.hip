@@ -18,30 +18,10 @@ __device__ __forceinline__ void bind(const DevModel<T>& m, Env<T>& e, char* smem
   env_bind<T, GB>(m, e, smem, GB ? (T*)s.scratch + (size_t)env * m.L.gB_stride : nullptr);
 }
 
-// Philox-drawn reset of `env` for its current episode counter (the counter then advances);
-// writes the state back to HBM.
-template <typename T, bool GB>
-__device__ __forceinline__ void bipedal_reset_philox(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, mgx_state s,
-                                                     mgx_bipedal_env be, float* obs, uint64_t seed, int env_offset,
-                                                     int env) {
-  int l = lane_id();
-  int E = be.episode[env];
-  bipedal_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)E, e.vec3);
-  wsync();
-  T d[12];
-  for (int j = 0; j < 12; j++) d[j] = e.vec3[j];
-  wsync();
-  int warn = bipedal_reset_body<T, true>(m, e, ids, d, be, env, obs);
-  store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
-              (T*)s.time, env);
-  if (l == 0) {
-    if (s.warning) s.warning[env] += warn;
-    if (s.overflow && e.overflow) s.overflow[env] += 1;
-    be.episode[env] = E + 1;
-  }
-}
-
-// MODE 0: one env step (+ same-step autoreset); MODE 1: reset (host draws or Philox)
+// One launch = one env step (MODE 0; ended envs then reset in the same launch when autoreset)
+// or one reset (MODE 1; host draws, or Philox keyed by (seed, env_offset + env, episode)). ONE
+// physics call site: the step's RK4 mj_step and a reset's 10 settle steps share the loop below,
+// so the forward pass (four stages per RK4 step) is inlined once.
 template <typename T, int MODE, bool GB>
 __global__ void __launch_bounds__(64) k_bipedal(DevModel<T> m, BipedalIds ids, mgx_state s, mgx_bipedal_env be,
                                                 const float* action, const T* draws, float* obs, double* reward,
@@ -56,44 +36,51 @@ __global__ void __launch_bounds__(64) k_bipedal(DevModel<T> m, BipedalIds ids, m
   int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
-  if (MODE == 1) {
-    if (!draws) {
-      bipedal_reset_philox<T, GB>(m, e, ids, s, be, obs, seed, env_offset, env);
-      return;
-    }
-    load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    T d[12];
-    for (int j = 0; j < 12; j++) d[j] = draws[12 * (size_t)env + j];
-    int warn = bipedal_reset_body<T, true>(m, e, ids, d, be, env, obs);
-    store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    if (l == 0) {
-      if (s.warning) s.warning[env] += warn;
-      if (s.overflow && e.overflow) s.overflow[env] += 1;
-      if (be.episode) be.episode[env] += 1;
-    }
-    return;
-  }
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  const float* a = action + (size_t)env * ids.n_act;
-  bipedal_pre(m, e, ids, a, be, env);
-  int warn = mj_step_env<T, true>(m, e);
-  bool done = bipedal_post(m, e, ids, action, be, env, obs, reward, terminated, truncated);
-  if (be.rollout && l == 0) {
-    T* ro = (T*)be.rollout + 4 * (size_t)env;
-    ro[0] += (T)reward[env];
-    ro[1] += (T)terminated[env];
-    ro[2] += (T)truncated[env];
-    ro[3] += (T)1;
+  bool resetting = MODE == 1;
+  if (MODE == 1) {
+    const T* dr = draws ? draws + 12 * (size_t)env : nullptr;
+    if (!draws) {
+      bipedal_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)be.episode[env], e.vec3);
+      wsync();
+      dr = e.vec3;
+    }
+    bipedal_reset_prologue(m, e, ids, dr, be, env);
+  } else {
+    bipedal_pre(m, e, ids, action + (size_t)env * ids.n_act, be, env);
   }
-  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  if (l == 0 && s.warning) s.warning[env] += warn;
-  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
-  if (done && autoreset) {
+  int warn = 0;
+  for (;;) {
+    const int nsteps = resetting ? 10 : 1;  // rescue_env.py:390-391 settle steps / one mj_step
+#pragma clang loop unroll(disable)
+    for (int k = 0; k < nsteps; k++) warn += mj_step_env<T, true>(m, e);
+    if (resetting) {
+      bipedal_reset_epilogue(m, e, ids, be, env, obs);
+      if (l == 0 && be.episode) be.episode[env] += 1;
+      break;
+    }
+    const bool done = bipedal_post(m, e, ids, action, be, env, obs, reward, terminated, truncated);
+    if (be.rollout && l == 0) {
+      T* ro = (T*)be.rollout + 4 * (size_t)env;
+      ro[0] += (T)reward[env];
+      ro[1] += (T)terminated[env];
+      ro[2] += (T)truncated[env];
+      ro[3] += (T)1;
+    }
+    if (!(done && autoreset)) break;
     if (final_obs)
       for (int i = l; i < 102; i += 64) final_obs[(size_t)env * 102 + i] = obs[(size_t)env * 102 + i];
     __threadfence();
     wsync();
-    bipedal_reset_philox<T, GB>(m, e, ids, s, be, obs, seed, env_offset, env);
+    bipedal_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)be.episode[env], e.vec3);
+    wsync();
+    bipedal_reset_prologue(m, e, ids, e.vec3, be, env);
+    resetting = true;
+  }
+  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  if (l == 0) {
+    if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
   }
 }
 

@@ -17,24 +17,6 @@
 #include "../../include/mgx.h"
 #include "mgx_soccer.h"
 
-// diagnostic progress trace for the dancing translation unit only (host-pinned memory set by
-// mgx_debug_dancing_trace; NULL = off): lane 0 of env e writes stage codes into
-// trace[16 e + k] so a faulting launch can be located from the host after the fault
-#ifdef MGX_DANCE_TRACE_TU
-__device__ int* g_dance_trace = nullptr;
-#define DTRACE(k, v)                                \
-  do {                                              \
-    if (g_dance_trace && lane_id() == 0) {          \
-      g_dance_trace[16 * blockIdx.x + (k)] = (v);   \
-      __threadfence_system();                       \
-    }                                               \
-  } while (0)
-#else
-#define DTRACE(k, v) \
-  do {               \
-  } while (0)
-#endif
-
 namespace mgx {
 
 // scal[] slots of mgx_dancing_env (include/mgx.h)
@@ -303,22 +285,22 @@ __device__ __forceinline__ void dancing_philox_draws(uint64_t seed, uint32_t gen
   }
 }
 
-// reset(): mj_resetData, counters, sequence, initial pose, 10 settle RK4 steps, obs, prev
-// snapshots. Spotlight, disco rotation and the fall_start_step attribute are left alone.
-template <typename T, bool RK>
-__device__ __forceinline__ int dancing_reset_body(const DevModel<T>& m, Env<T>& e, const DancingIds& ids, const T* draws,
-                                                  mgx_dancing_env de, int env, float* obs) {
+// reset() (dancing_env.py:763-830), split around its 10 settle RK4 steps so the task kernel
+// keeps one physics call site: the prologue stores the move sequence (draws read in place,
+// global for host draws or LDS for Philox, before the physics reuses the LDS), runs
+// mj_resetData, counters and the initial pose; the epilogue writes the observation and the
+// prev snapshots. Spotlight, disco rotation and fall_start_step are left alone.
+template <typename T>
+__device__ __forceinline__ void dancing_reset_prologue(const DevModel<T>& m, Env<T>& e, const T* draws,
+                                                       mgx_dancing_env de, int env) {
   int l = lane_id();
   double* S = de.scal + (size_t)env * DS_N;
   int* I = de.ints + (size_t)env * DI_N;
-  // draws: global (host draws) or LDS (Philox), read before the physics below reuses the LDS
   if (l < MGX_DANCE_SEQ) {
     de.moves[(size_t)env * MGX_DANCE_SEQ + l] = (int)draws[2 * l];
     de.durations[(size_t)env * MGX_DANCE_SEQ + l] = (double)draws[2 * l + 1];
   }
-  DTRACE(1, 1);
   reset_env(m, e);
-  DTRACE(1, 2);
   if (l == 0) {
     e.qpos[0] = 0; e.qpos[1] = 0; e.qpos[2] = (T)1.8;
     e.qpos[3] = 1; e.qpos[4] = 0; e.qpos[5] = 0; e.qpos[6] = 0;
@@ -330,21 +312,20 @@ __device__ __forceinline__ int dancing_reset_body(const DevModel<T>& m, Env<T>& 
     H[0] = H[1] = H[2] = -1;
   }
   wsync();
-  DTRACE(1, 3);
   for (int k = 7 + l; k < m.nq && k - 7 < m.njnt; k += 64) e.qpos[k] = 0;
   wsync();
-  int warn = 0;
-  for (int k = 0; k < 10; k++) {  // dancing_env.py:809-810
-    warn += mj_step_env<T, RK>(m, e);
-    DTRACE(2, k + 1);
-  }
+}
+
+template <typename T>
+__device__ __forceinline__ void dancing_reset_epilogue(const DevModel<T>& m, Env<T>& e, const DancingIds& ids,
+                                                       mgx_dancing_env de, int env, float* obs) {
+  int l = lane_id();
+  double* S = de.scal + (size_t)env * DS_N;
+  int* I = de.ints + (size_t)env * DI_N;
   dancing_obs(m, e, ids, S, I, de.moves + (size_t)env * MGX_DANCE_SEQ, obs + (size_t)env * MGX_DANCE_OBS);
-  DTRACE(1, 4);
   if (l >= 6 && l < m.nv) de.prev_jvel[(size_t)env * (m.nv - 6) + (l - 6)] = (double)e.qvel[l];
   if (l < 3) S[DS_TORSO + l] = (double)e.xpos[3 * ids.torso + l];
   wsync();
-  DTRACE(1, 5);
-  return warn;
 }
 
 }  // namespace mgx

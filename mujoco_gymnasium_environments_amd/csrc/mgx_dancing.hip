@@ -4,7 +4,6 @@
 // (mgx_step.hip): a dancing env step is clip + rhythm + spotlight -> one RK4 mj_step (four
 // forward passes, rows in LDS) -> observation / reward / termination / stats / crowd / move
 // transition, with same-step autoreset (10 settle steps), all in one launch.
-#define MGX_DANCE_TRACE_TU 1
 #include "mgx_internal.h"
 
 using namespace mgx;
@@ -18,28 +17,11 @@ __device__ __forceinline__ void bind(const DevModel<T>& m, Env<T>& e, char* smem
   env_bind<T, GB>(m, e, smem, GB ? (T*)s.scratch + (size_t)env * m.L.gB_stride : nullptr);
 }
 
-// Philox-drawn reset of `env` for its current episode counter (the counter then advances);
-// writes the state back to HBM.
-template <typename T, bool GB>
-__device__ __forceinline__ void dancing_reset_philox(const DevModel<T>& m, Env<T>& e, const DancingIds& ids, mgx_state s,
-                                                     mgx_dancing_env de, float* obs, uint64_t seed, int env_offset,
-                                                     int env) {
-  int l = lane_id();
-  int E = de.episode[env];
-  dancing_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)E, e.vec3);
-  wsync();
-  // the reset body consumes the draws (LDS) before its physics overwrites the vec regions
-  int warn = dancing_reset_body<T, true>(m, e, ids, e.vec3, de, env, obs);
-  store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
-              (T*)s.time, env);
-  if (l == 0) {
-    if (s.warning) s.warning[env] += warn;
-    if (s.overflow && e.overflow) s.overflow[env] += 1;
-    de.episode[env] = E + 1;
-  }
-}
-
-// MODE 0: one env step (+ same-step autoreset); MODE 1: reset (host draws or Philox)
+// One launch = one env step (MODE 0; ended envs then reset in the same launch when autoreset)
+// or one reset (MODE 1; host draws, or Philox keyed by (seed, env_offset + env, episode)).
+// The kernel has ONE physics call site: the step's single RK4 mj_step and a reset's 10 settle
+// steps run through the same loop, so the ~1.6k-instruction forward pass is inlined once (the
+// earlier three-site form carried ~1.5k SGPR spills per kernel).
 template <typename T, int MODE, bool GB>
 __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, mgx_state s, mgx_dancing_env de,
                                                 const float* action, const T* draws, float* obs, double* reward,
@@ -54,46 +36,51 @@ __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, m
   int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
-  if (MODE == 1) {
-    if (!draws) {
-      dancing_reset_philox<T, GB>(m, e, ids, s, de, obs, seed, env_offset, env);
-      return;
-    }
-    DTRACE(0, 1);
-    load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    DTRACE(0, 2);
-    int warn = dancing_reset_body<T, true>(m, e, ids, draws + 2 * MGX_DANCE_SEQ * (size_t)env, de, env, obs);
-    DTRACE(0, 3);
-    store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-    DTRACE(0, 4);
-    if (l == 0) {
-      if (s.warning) s.warning[env] += warn;
-      if (s.overflow && e.overflow) s.overflow[env] += 1;
-      if (de.episode) de.episode[env] += 1;
-    }
-    return;
-  }
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  const float* a = action + (size_t)env * ids.n_act;
-  dancing_pre(m, e, ids, a, de, env);
-  int warn = mj_step_env<T, true>(m, e);
-  bool done = dancing_post(m, e, ids, action, de, env, obs, reward, terminated, truncated);
-  if (de.rollout && l == 0) {
-    T* ro = (T*)de.rollout + 4 * (size_t)env;
-    ro[0] += (T)reward[env];
-    ro[1] += (T)terminated[env];
-    ro[2] += (T)truncated[env];
-    ro[3] += (T)1;
+  bool resetting = MODE == 1;
+  if (MODE == 1) {
+    const T* dr = draws ? draws + 2 * MGX_DANCE_SEQ * (size_t)env : nullptr;
+    if (!draws) {
+      dancing_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)de.episode[env], e.vec3);
+      wsync();
+      dr = e.vec3;
+    }
+    dancing_reset_prologue(m, e, dr, de, env);
+  } else {
+    dancing_pre(m, e, ids, action + (size_t)env * ids.n_act, de, env);
   }
-  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  if (l == 0 && s.warning) s.warning[env] += warn;
-  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
-  if (done && autoreset) {
+  int warn = 0;
+  for (;;) {
+    const int nsteps = resetting ? 10 : 1;  // dancing_env.py:809-810 settle steps / one mj_step
+#pragma clang loop unroll(disable)
+    for (int k = 0; k < nsteps; k++) warn += mj_step_env<T, true>(m, e);
+    if (resetting) {
+      dancing_reset_epilogue(m, e, ids, de, env, obs);
+      if (l == 0 && de.episode) de.episode[env] += 1;
+      break;
+    }
+    const bool done = dancing_post(m, e, ids, action, de, env, obs, reward, terminated, truncated);
+    if (de.rollout && l == 0) {
+      T* ro = (T*)de.rollout + 4 * (size_t)env;
+      ro[0] += (T)reward[env];
+      ro[1] += (T)terminated[env];
+      ro[2] += (T)truncated[env];
+      ro[3] += (T)1;
+    }
+    if (!(done && autoreset)) break;
     if (final_obs)
       for (int i = l; i < MGX_DANCE_OBS; i += 64) final_obs[(size_t)env * MGX_DANCE_OBS + i] = obs[(size_t)env * MGX_DANCE_OBS + i];
     __threadfence();
     wsync();
-    dancing_reset_philox<T, GB>(m, e, ids, s, de, obs, seed, env_offset, env);
+    dancing_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)de.episode[env], e.vec3);
+    wsync();
+    dancing_reset_prologue(m, e, e.vec3, de, env);
+    resetting = true;
+  }
+  store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
+  if (l == 0) {
+    if (s.warning) s.warning[env] += warn;
+    if (s.overflow && e.overflow) s.overflow[env] += 1;
   }
 }
 
@@ -154,12 +141,6 @@ void launch(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const 
 }  // namespace
 
 extern "C" {
-
-int mgx_debug_dancing_trace(void* host_pinned) {
-  int* p = (int*)host_pinned;
-  MGX_HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dance_trace), &p, sizeof(p)));
-  return MGX_OK;
-}
 
 int mgx_dancing_configure(mgx_model* m, const mgx_dancing_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");

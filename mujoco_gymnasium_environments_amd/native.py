@@ -107,7 +107,6 @@ _SIGS = {
                            C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_bipedal_logic_test": ([_VP, C.POINTER(cabi.MgxBipedalLogicIO), C.POINTER(cabi.MgxBipedalEnv), C.c_int, _VP],
                                C.c_int),
-    "mgx_debug_dancing_trace": ([_VP], C.c_int),
     "mgx_dancing_configure": ([_VP, C.POINTER(cabi.MgxDancingIds)], C.c_int),
     "mgx_dancing_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxDancingEnv), _VP, _VP, _VP, _VP, _VP,
                           _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
