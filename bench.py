@@ -45,7 +45,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
-PMC_PROFILE = "r01_v4_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
+PMC_PROFILE = "r02_v3_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
 PMC_PROFILE_BIPEDAL = "r01_bipedal_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task

@@ -14,15 +14,7 @@
 
 using namespace mgx;
 
-#ifdef MGX_PROFILE
-namespace mgx {
-__device__ unsigned long long* g_mgx_prof = nullptr;
-}
-extern "C" int mgx_prof_set_buffer(void* p) {
-  unsigned long long* q = (unsigned long long*)p;
-  return hipMemcpyToSymbol(HIP_SYMBOL(mgx::g_mgx_prof), &q, sizeof(q)) == hipSuccess ? 0 : -3;
-}
-#endif
+MGX_PROF_SETTER(mgx_prof_set_buffer)
 
 namespace {
 thread_local std::string g_err;

@@ -83,7 +83,14 @@ struct DevModel {
 // Built only with -DMGX_PROFILE (libmgx_prof.so, never the shipped library): per-env cycle
 // sums per stage, read back by tools/stage_profile.py. Stamps never feed any output.
 #ifdef MGX_PROFILE
-extern __device__ unsigned long long* g_mgx_prof;
+// one buffer pointer per translation unit (no relocatable device code); each TU exports its
+// setter with MGX_PROF_SETTER(name)
+static __device__ unsigned long long* g_mgx_prof = nullptr;
+#define MGX_PROF_SETTER(name)                                                                     \
+  extern "C" int name(void* p) {                                                                 \
+    unsigned long long* q = (unsigned long long*)p;                                               \
+    return hipMemcpyToSymbol(HIP_SYMBOL(mgx::g_mgx_prof), &q, sizeof(q)) == hipSuccess ? 0 : -3; \
+  }
 #define MGX_STAMP_DECL unsigned long long _mgx_t0 = __builtin_amdgcn_s_memtime();
 #define MGX_STAMP(slot)                                                                 \
   do {                                                                                  \
@@ -94,6 +101,7 @@ extern __device__ unsigned long long* g_mgx_prof;
     __builtin_amdgcn_sched_barrier(0);                                                  \
   } while (0)
 #else
+#define MGX_PROF_SETTER(name)
 #define MGX_STAMP_DECL
 #define MGX_STAMP(slot) do {} while (0)
 #endif

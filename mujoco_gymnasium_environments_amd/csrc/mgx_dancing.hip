@@ -8,6 +8,8 @@
 
 using namespace mgx;
 
+MGX_PROF_SETTER(mgx_prof_set_buffer_dancing)
+
 namespace {
 
 int fail(int code, const std::string& msg) { return host_fail(code, msg); }

@@ -35,3 +35,5 @@ int pgs_configure_lds(int precision, int pl) {
 }
 
 }  // namespace mgx
+
+MGX_PROF_SETTER(mgx_prof_set_buffer_pgs)

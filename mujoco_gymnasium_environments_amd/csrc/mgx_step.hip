@@ -9,6 +9,8 @@
 
 using namespace mgx;
 
+MGX_PROF_SETTER(mgx_prof_set_buffer_step)
+
 namespace {
 int fail(int code, const std::string& msg) { return host_fail(code, msg); }
 #define HIPCHK(x) MGX_HIPCHK(x)

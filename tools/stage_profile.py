@@ -1,8 +1,12 @@
-"""Per-stage cycle breakdown of the soccer step kernel (diagnostic build, -DMGX_PROFILE).
+"""Per-stage cycle breakdown of the step kernels (diagnostic build, -DMGX_PROFILE).
 
-Builds libmgx_prof.so next to libmgx.so, loads it instead, runs K steps of the soccer
-VectorEnv and prints the mean cycles per env step for each stage. Shares only: the
-instrumented build's absolute times are not the shipped kernel's (stamps serialise).
+    python tools/stage_profile.py --build            # CPU: all translation units -> libmgx_prof.so
+    TASK=soccer|assembly|bipedal|martial N=... K=... python tools/stage_profile.py   # GPU
+
+Loads libmgx_prof.so instead of libmgx.so, runs K steps of the task's VectorEnv and prints the
+mean cycles per env step for each stage of the forward pass (each translation unit has its own
+stamp buffer, set through its MGX_PROF_SETTER export). Shares only: the instrumented build's
+absolute times are not the shipped kernel's (stamps serialise).
 """
 import ctypes as C
 import os
@@ -24,9 +28,78 @@ SUBSTAGES = 4  # the block sub-stamps are inside 'rows (all blocks)'; excluded f
 
 
 def build():
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMGX_PROFILE",
-           "-o", PROF_LIB, os.path.join(native.CSRC, "mgx_api.hip")]
-    subprocess.run(cmd, check=True)
+    """Every translation unit of libmgx.so with -DMGX_PROFILE, objects in _build_prof/."""
+    bdir = os.path.join(native.PKG, "_build_prof")
+    os.makedirs(bdir, exist_ok=True)
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DMGX_PROFILE"]
+    procs, objs = [], []
+    for src in native.SOURCES:
+        obj = os.path.join(bdir, src.replace(".hip", ".o"))
+        objs.append(obj)
+        procs.append(subprocess.Popen(base + native.SOURCE_FLAGS.get(src, []) + ["-c", "-o", obj,
+                                                                                 os.path.join(native.CSRC, src)]))
+    for p in procs:
+        if p.wait() != 0:
+            raise SystemExit("profile build failed")
+    subprocess.run(base + ["-shared", "-o", PROF_LIB] + objs, check=True)
+
+
+TASK_TU = {"assembly": "mgx_prof_set_buffer_assembly", "bipedal": "mgx_prof_set_buffer_bipedal",
+           "martial": "mgx_prof_set_buffer_martial"}
+
+
+def make_task(task, n):
+    import torch
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0)
+    if task == "assembly":
+        from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
+        env = AssemblyVectorEnv(n)
+        lo = torch.tensor([-2.0] * 7 + [0, 0], device="cuda:0")
+        span = torch.tensor([4.0] * 7 + [100, 50], device="cuda:0")
+        acts = [torch.rand(n, 9, device="cuda:0", generator=g) * span + lo for _ in range(4)]
+    elif task == "bipedal":
+        from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+        env = BipedalVectorEnv(n, seed=3)
+        acts = [(torch.rand(n, 26, device="cuda:0", generator=g) * 2 - 1) * 100 for _ in range(4)]
+    else:
+        from mujoco_gymnasium_environments_amd.envs.martial import MartialArtsVectorEnv
+        env = MartialArtsVectorEnv(n, seed=3)
+        acts = [torch.rand(n, 28, device="cuda:0", generator=g) * 2 - 1 for _ in range(4)]
+    return env, acts
+
+
+def main_task(task):
+    import numpy as np
+    import torch
+    native.LIB_PATH = PROF_LIB
+    L = native.lib()
+    setter = getattr(L, TASK_TU[task])
+    setter.argtypes = [C.c_void_p]
+    n = int(os.environ.get("N", "1024"))
+    steps = int(os.environ.get("K", "5"))
+    env, acts = make_task(task, n)
+    env.reset()
+    for k in range(2):
+        env.step(acts[k % 4])
+    torch.cuda.synchronize()
+    buf = torch.zeros(n * 32, dtype=torch.int64, device="cuda:0")
+    assert setter(C.c_void_p(buf.data_ptr())) == 0
+    for k in range(steps):
+        env.step(acts[k % 4])
+    torch.cuda.synchronize()
+    raw = buf.view(n, 32).double().cpu().numpy()
+    v = raw / steps
+    tot = v[:, :len(STAGES)].sum(1).mean()
+    calls = raw[:, 23].sum()
+    print(f"{task}: envs={n} steps={steps} mean cycles per env-step (s_memtime units), total {tot:.0f}; "
+          f"forwards per env-step {calls / (n * steps):.2f}")
+    for i, st in enumerate(STAGES):
+        print(f"  {st:16s} {v[:, i].mean():14.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {np.percentile(v[:, i], 99):.0f}")
+    print(f"  per forward: nefc mean {raw[:, 20].sum() / calls:.1f}  solver iterations mean {raw[:, 21].sum() / calls:.2f}"
+          f"  ncon mean {raw[:, 22].sum() / calls:.1f}")
+    print(f"  lds bytes per env {env.native.info.lds_bytes_per_env}, scratch bytes per env "
+          f"{env.native.info.scratch_bytes_per_env}")
 
 
 def main():
@@ -34,6 +107,9 @@ def main():
     if "--build" in sys.argv:
         build()
         return
+    task = os.environ.get("TASK", "soccer")
+    if task != "soccer":
+        return main_task(task)
     import torch
     native.LIB_PATH = PROF_LIB
     L = native.lib()
