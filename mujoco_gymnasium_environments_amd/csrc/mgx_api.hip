@@ -412,6 +412,8 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
     L.gB_stride = align_up(max_nefc * L.Bstride, al);
     L.chunk_rows = 0;
   }
+  // gB: the row transform stages up to 64 rows at a time in the phase-A union (dead by then)
+  L.tchunk = L.gB ? std::min(64, (endA - u0) / L.Bstride) : 0;
   int endB = align_up(u0 + L.chunk_rows * L.Bstride, al);
   L.reals = endA > endB ? endA : endB;
   int q = 0;

@@ -43,6 +43,8 @@ struct Layout {
   // 1: the monolithic kernel keeps B rows in per-env global scratch (gB_stride reals per env)
   // instead of LDS, for models whose rows do not fit the LDS budget
   int gB, gB_stride;
+  // gB only: rows per chunk staged into the (dead) phase-A union region for the row transform
+  int tchunk;
   // Newton solver (solver == mjSOL_NEWTON, monolithic kernels only): nv x nv Hessian
   int hess;
 };

@@ -636,11 +636,33 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
   wsync();
 }
 
-// B_r = D^-1/2 L'^-1 J_r' in place (lane per row), sqrtdi in vec0
+// B_r = D^-1/2 L'^-1 J_r' in place (lane per row), sqrtdi in vec0. Rows in global scratch
+// (Layout.gB) are staged through LDS in chunks of L.tchunk rows (the phase-A union is dead once
+// the rows exist): coalesced row copies in and out (lane = dof), the lane-per-row transform on
+// LDS, instead of lane-strided global read-modify-writes along every row.
 template <typename T>
 __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
-  for (int r = l; r < e.nefc; r += 64) transform_row(m, e, e.Bm + r * e.Bs, e.vec0);
+  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+  const int C = m.L.tchunk;
+  if (m.L.gB && C > 0) {
+    T* S = e.xmat;  // start of the union region
+    const int Bs = e.Bs, nv = m.nv;
+    for (int r0 = 0; r0 < ne; r0 += C) {
+      const int nr = ne - r0 < C ? ne - r0 : C;
+      T* G = e.Bm + (size_t)r0 * Bs;
+      if (l < nv)
+        for (int r = 0; r < nr; r++) S[r * Bs + l] = G[r * Bs + l];
+      wsync();
+      if (l < nr) transform_row(m, e, S + l * Bs, e.vec0);
+      wsync();
+      if (l < nv)
+        for (int r = 0; r < nr; r++) G[r * Bs + l] = S[r * Bs + l];
+      wsync();
+    }
+    return;
+  }
+  for (int r = l; r < ne; r += 64) transform_row(m, e, e.Bm + r * e.Bs, e.vec0);
   wsync();
 }
 
@@ -937,34 +959,31 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     return;
   }
   T qv = dl ? e.qvel[l] : (T)0;
-  T wv = sqrtD * mul_L(m, e, e.qLD, qv);
-  T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
-  T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
-  wsync();
-  if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww - ws; }
-  wsync();
+  const T wv = sqrtD * mul_L(m, e, e.qLD, qv);
+  const T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
+  const T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
+  const T wd = dl ? ww - ws : (T)0;
   T* efc = e.efc;
   const T* Bm = e.Bm;
   const int Bs = e.Bs;
-  // per row: aref, b = J qacc_smooth - aref, D; x at u = 0 (q[1]) and at the warmstart (q[3])
-  T c0p = 0, cwp = 0;
-  for (int r = l; r < ne; r += 64) {
-    const T* row = Bm + r * Bs;
-    T dv = 0, ds = 0, dw = 0;
-    for (int k = 0; k < nv; k++) {
-      T x = row[k];
-      dv += x * e.vec0[k]; ds += x * e.vec1[k]; dw += x * e.vec2[k];
-    }
+  // per row: aref, b = J qacc_smooth - aref, D; x at u = 0 (q[1]) and at the warmstart (q[3]).
+  // Rows are read row-major (lane = dof, one coalesced load per row, wave reductions), which is
+  // what keeps the global-scratch rows (Layout.gB) off the latency path; the row scalars are
+  // uniform and lane 0 stores them.
+  T c0 = 0, cw = 0;
+  for (int r = 0; r < ne; r++) {
+    const T x = dl ? Bm[r * Bs + lc] : (T)0;
+    const T dv = usum(x * wv), ds = usum(x * ws), dw = usum(x * wd);
     T* q = efc + 8 * r;
-    T aref = -q[6] * dv - q[5];
-    q[5] = aref;
-    T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
-    q[0] = b; q[1] = b; q[3] = xw; q[4] = D;
-    if (b < 0) c0p += (T)0.5 * D * b * b;
-    if (xw < 0) cwp += (T)0.5 * D * xw * xw;
+    const T aref = -q[6] * dv - q[5];
+    const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
+    if (b < 0) c0 += (T)0.5 * D * b * b;
+    if (xw < 0) cw += (T)0.5 * D * xw * xw;
+    if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
   }
-  const T uw = dl ? e.vec2[l] : (T)0;
-  const T c0 = usum(c0p), cw = usum(cwp + (T)0.5 * uw * uw);
+  wsync();
+  const T uw = wd;
+  cw += usum((T)0.5 * uw * uw);
   const bool warm = cw < c0;
   T u = warm ? uw : (T)0;
   T cost = warm ? cw : c0;
@@ -979,9 +998,12 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // whitened gradient g = u + sum_{x<0} D x B_r (lane = dof)
   auto gradient = [&]() {
     T gg = u;
+    T bn = dl ? Bm[lc] : (T)0;  // the next row's load is issued ahead of the branch
     for (int r = 0; r < ne; r++) {
-      T xr = efc[8 * r + 1];
-      if (xr < 0) gg += efc[8 * r + 4] * xr * Bm[r * Bs + lc];
+      const T b = bn;
+      bn = r + 1 < ne && dl ? Bm[(r + 1) * Bs + lc] : (T)0;
+      const T xr = efc[8 * r + 1];
+      if (xr < 0) gg += efc[8 * r + 4] * xr * b;
     }
     return dl ? gg : (T)0;
   };
@@ -989,23 +1011,27 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // mj_solNewton's loop order [ext]: update first, then test the scaled improvement and the
   // scaled gradient at the new point, so at least one iteration runs
   while (iter < maxit) {
-    // H = I + sum D B_r B_r', lower triangle, lane = column j, rows i in blocks of 8 held in
-    // registers: per active row one lane-indexed read B_rj and 8 broadcast reads B_ri
-    for (int i0 = 0; i0 < nv; i0 += 8) {
-      T acc[8];
+    // H = I + sum_{x<0} D B_r B_r', lower triangle, lane = column j: per active row one
+    // coalesced load of B_r (lane value b_j), then H[i][j] += (D b_j) b_i for the rows i of a
+    // 32-row half, b_i broadcast by readlane from registers; the next row's load is issued
+    // before the current row's FMAs so the global-scratch rows stream
+    for (int i0 = 0; i0 < nv; i0 += 32) {
+      T acc[32];
 #pragma unroll
-      for (int k = 0; k < 8; k++) acc[k] = l == i0 + k ? (T)1 : (T)0;
+      for (int k = 0; k < 32; k++) acc[k] = l == i0 + k ? (T)1 : (T)0;
+      T bn = dl ? Bm[lc] : (T)0;
       for (int r = 0; r < ne; r++) {
-        T xr = efc[8 * r + 1];
+        const T b = bn;
+        bn = r + 1 < ne && dl ? Bm[(r + 1) * Bs + lc] : (T)0;
+        const T xr = efc[8 * r + 1];
         if (xr < 0) {
-          const T* row = Bm + r * Bs;
-          T c = efc[8 * r + 4] * row[lc];
+          const T c = efc[8 * r + 4] * b;
 #pragma unroll
-          for (int k = 0; k < 8; k++) acc[k] += c * row[i0 + k < nv ? i0 + k : nv - 1];
+          for (int k = 0; k < 32; k++) acc[k] += c * readlane(b, (i0 + k) & 63);
         }
       }
 #pragma unroll
-      for (int k = 0; k < 8; k++)
+      for (int k = 0; k < 32; k++)
         if (i0 + k < nv && l <= i0 + k) H[(i0 + k) * nv + l] = acc[k];
     }
     wsync();
@@ -1041,15 +1067,13 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       else if (l < k) p -= H[k * nv + l] * pk;
     }
     p = dl ? p : (T)0;
-    wsync();
-    if (dl) e.vec3[l] = p;
-    wsync();
-    for (int r = l; r < ne; r += 64) {
-      const T* row = Bm + r * Bs;
-      T s = 0;
-      for (int k = 0; k < nv; k++) s += row[k] * e.vec3[k];
-      efc[8 * r + 3] = s;
+    // J p per row, row-major (coalesced) with a wave reduction; lane 0 stores
+    for (int r = 0; r < ne; r++) {
+      const T x = dl ? Bm[r * Bs + lc] : (T)0;
+      const T jp = usum(x * p);
+      if (l == 0) efc[8 * r + 3] = jp;
     }
+    wsync();
     // exact line search: f'(al) = u.p + al p.p + sum_{x + al jp < 0} D (x + al jp) jp
     const T g0 = usum(u * p), pp = usum(p * p);
     T al = 1, lo = 0, hi = (T)1e30;
