@@ -320,6 +320,20 @@ __device__ __forceinline__ T factor_ld(const DevModel<T>& m, const Env<T>& e, T*
   return l < m.nv ? (T)1 / LD[e.madr] : (T)0;
 }
 
+// ---------------------------------------------------------------- row streaming helpers
+// Row-major passes over B (lane = dof) load 8 rows at a time into registers before using any:
+// with B in global scratch (Layout.gB) the loads would otherwise serialise behind the LDS row-
+// scalar stores of the previous row (generic pointers may alias), one full memory latency each.
+#define MGX_RB 8
+template <typename T>
+__device__ __forceinline__ void load_rows(T* x, const T* Bm, int Bs, int r0, int ne, int lc, bool dl) {
+#pragma unroll
+  for (int j = 0; j < MGX_RB; j++) x[j] = (r0 + j < ne && dl) ? Bm[(r0 + j) * Bs + lc] : (T)0;
+}
+
+template <typename T>
+__device__ __forceinline__ T usum(T x) { return readlane(wave_sum(x), 0); }
+
 // B_r = D^-1/2 L'^-1 J_r' for one row x (LDS, lane-private): for k = nv-1 .. 0 the ancestors
 // of k get x[anc] -= L[k][anc] x[k]. The ancestors of one k are distinct, so all their loads
 // are issued before any store (one LDS latency per k instead of one per ancestor).
@@ -651,8 +665,13 @@ __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) 
     for (int r0 = 0; r0 < ne; r0 += C) {
       const int nr = ne - r0 < C ? ne - r0 : C;
       T* G = e.Bm + (size_t)r0 * Bs;
-      if (l < nv)
-        for (int r = 0; r < nr; r++) S[r * Bs + l] = G[r * Bs + l];
+      for (int q0 = 0; q0 < nr; q0 += MGX_RB) {
+        T xb[MGX_RB];
+        load_rows(xb, G, Bs, q0, nr, l < nv ? l : 0, l < nv);
+#pragma unroll
+        for (int j = 0; j < MGX_RB; j++)
+          if (q0 + j < nr && l < nv) S[(q0 + j) * Bs + l] = xb[j];
+      }
       wsync();
       if (l < nr) transform_row(m, e, S + l * Bs, e.vec0);
       wsync();
@@ -797,57 +816,65 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
     e.niter = 0;
     return;
   }
-  // w vectors: D^1/2 L x for qvel, qacc_smooth, qacc_warmstart -> vec0 / vec1 / vec2
+  // w vectors: D^1/2 L x for qvel, qacc_smooth, qacc_warmstart (lane = dof)
   T qv = dl ? e.qvel[l] : (T)0;
-  T wv = sqrtD * mul_L(m, e, e.qLD, qv);
-  T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
-  T ww = sqrtD * mul_L(m, e, e.qLD, e.qacc_ws);
-  wsync();
-  if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = ww; }
-  wsync();
+  const T wv = sqrtD * mul_L(m, e, e.qLD, qv);
+  const T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
+  const T ww = dl ? sqrtD * mul_L(m, e, e.qLD, e.qacc_ws) : (T)0;
   T* efc = e.efc;
   const T* Bm = e.Bm;
   const int Bs = e.Bs;
-  // per row (lane per row): efc_vel -> aref (mj_referenceConstraint), b = J qacc_smooth - aref,
-  // warmstart force from qacc_warmstart (mj_constraintUpdate), 1/AR_rr and AR_rr
-  for (int r = l; r < ne; r += 64) {
-    const T* row = Bm + r * Bs;
-    T dv = 0, ds = 0, dw = 0, nn = 0;
-    for (int k = 0; k < nv; k++) {
-      T x = row[k];
-      dv += x * e.vec0[k]; ds += x * e.vec1[k]; dw += x * e.vec2[k]; nn += x * x;
+  const int lc = dl ? l : 0;  // clamped column: every lane reads a valid address
+  // per row (row-major, 8 rows per batch, wave reductions; lane 0 stores the scalars):
+  // efc_vel -> aref (mj_referenceConstraint), b = J qacc_smooth - aref, warmstart force from
+  // qacc_warmstart (mj_constraintUpdate), 1/AR_rr and AR_rr
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T x[MGX_RB];
+    load_rows(x, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      if (r < ne) {
+        T dv = x[j] * wv, ds = x[j] * ws, dw = x[j] * ww, nn = x[j] * x[j];
+        wave_sum4(dv, ds, dw, nn);
+        T* q = efc + 8 * r;
+        const T aref = -q[6] * dv - q[5];
+        const T Rr = q[2];
+        const T jar = dw - aref;
+        const T ad = nn + Rr;
+        if (l == 0) {
+          q[5] = aref;
+          q[0] = ds - aref;
+          q[1] = jar < 0 ? -jar / Rr : (T)0;
+          q[4] = ad;
+          q[3] = (T)1 / ad;
+        }
+      }
     }
-    T* q = efc + 8 * r;
-    T aref = -q[6] * dv - q[5];
-    q[5] = aref;
-    q[0] = ds - aref;
-    T Rr = q[2];
-    T jar = dw - aref;
-    q[1] = jar < 0 ? -jar / Rr : (T)0;
-    T ad = nn + Rr;
-    q[4] = ad;
-    q[3] = (T)1 / ad;
   }
   wsync();
   // v = B' f (lane = dof), then the warmstart dual cost
-  const int lc = dl ? l : 0;  // clamped column: every lane reads a valid address
   T v = 0;
-  for (int r = 0; r < ne; r++) {
-    T b = Bm[r * Bs + lc];
-    v += efc[8 * r + 1] * (dl ? b : (T)0);
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T x[MGX_RB];
+    load_rows(x, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++)
+      if (r0 + j < ne) v += efc[8 * (r0 + j) + 1] * x[j];
   }
-  wsync();
-  if (dl) e.vec0[l] = v;
-  wsync();
-  T cpart = 0;
-  for (int r = l; r < ne; r += 64) {
-    const T* row = Bm + r * Bs;
-    T bv = 0;
-    for (int k = 0; k < nv; k++) bv += row[k] * e.vec0[k];
-    const T* q = efc + 8 * r;
-    cpart += q[1] * (q[0] + (T)0.5 * (bv + q[2] * q[1]));
+  T cost = 0;
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T x[MGX_RB];
+    load_rows(x, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      if (r0 + j < ne) {
+        const T bv = usum(x[j] * v);
+        const T* q = efc + 8 * (r0 + j);
+        cost += q[1] * (q[0] + (T)0.5 * (bv + q[2] * q[1]));
+      }
+    }
   }
-  T cost = wave_sum(cpart);
   if (cost > 0) {
     for (int r = l; r < ne; r += 64) efc[8 * r + 1] = 0;
     v = 0;
@@ -867,18 +894,17 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
     if (dl) e.Bm[r * Bs + l] = 0;
   wsync();
   T* blk = e.efc_blk;  // [ne4/4][8]: A_10, A_20, A_21, A_30, A_31, A_32
-  for (int b0 = 4 * l; b0 < ne4; b0 += 256) {
-    const T* r0 = Bm + b0 * Bs;
-    const T* r1 = r0 + Bs;
-    const T* r2 = r1 + Bs;
-    const T* r3 = r2 + Bs;
-    T a10 = 0, a20 = 0, a21 = 0, a30 = 0, a31 = 0, a32 = 0;
-    for (int k = 0; k < nv; k++) {
-      T x0 = r0[k], x1 = r1[k], x2 = r2[k], x3 = r3[k];
-      a10 += x1 * x0; a20 += x2 * x0; a21 += x2 * x1; a30 += x3 * x0; a31 += x3 * x1; a32 += x3 * x2;
+  for (int b0 = 0; b0 < ne4; b0 += 4) {  // row-major: 4 coalesced row loads, 6 wave reductions
+    const T x0 = dl ? Bm[b0 * Bs + lc] : (T)0, x1 = dl ? Bm[(b0 + 1) * Bs + lc] : (T)0;
+    const T x2 = dl ? Bm[(b0 + 2) * Bs + lc] : (T)0, x3 = dl ? Bm[(b0 + 3) * Bs + lc] : (T)0;
+    T a10 = x1 * x0, a20 = x2 * x0, a21 = x2 * x1, a30 = x3 * x0;
+    T a31 = x3 * x1, a32 = x3 * x2, z0 = 0, z1 = 0;
+    wave_sum4(a10, a20, a21, a30);
+    wave_sum4(a31, a32, z0, z1);
+    if (l == 0) {
+      T* o = blk + 2 * b0;
+      o[0] = a10; o[1] = a20; o[2] = a21; o[3] = a30; o[4] = a31; o[5] = a32;
     }
-    T* o = blk + 2 * b0;
-    o[0] = a10; o[1] = a20; o[2] = a21; o[3] = a30; o[4] = a31; o[5] = a32;
   }
   wsync();
   const T scale = (T)1 / (m.meaninertia * (T)(nv > 1 ? nv : 1));
@@ -942,9 +968,6 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
 // (scaled dof-space gradient, scaled improvement). Row scalars: q[0] b, q[1] x (efc_force at
 // exit), q[2] R, q[3] B_r.p, q[4] D.
 template <typename T>
-__device__ __forceinline__ T usum(T x) { return readlane(wave_sum(x), 0); }
-
-template <typename T>
 __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   const int l = lane_id();
   const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
@@ -971,15 +994,23 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // what keeps the global-scratch rows (Layout.gB) off the latency path; the row scalars are
   // uniform and lane 0 stores them.
   T c0 = 0, cw = 0;
-  for (int r = 0; r < ne; r++) {
-    const T x = dl ? Bm[r * Bs + lc] : (T)0;
-    const T dv = usum(x * wv), ds = usum(x * ws), dw = usum(x * wd);
-    T* q = efc + 8 * r;
-    const T aref = -q[6] * dv - q[5];
-    const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
-    if (b < 0) c0 += (T)0.5 * D * b * b;
-    if (xw < 0) cw += (T)0.5 * D * xw * xw;
-    if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T xb[MGX_RB];
+    load_rows(xb, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      if (r < ne) {
+        T dv = xb[j] * wv, ds = xb[j] * ws, dw = xb[j] * wd, z = 0;
+        wave_sum4(dv, ds, dw, z);
+        T* q = efc + 8 * r;
+        const T aref = -q[6] * dv - q[5];
+        const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
+        if (b < 0) c0 += (T)0.5 * D * b * b;
+        if (xw < 0) cw += (T)0.5 * D * xw * xw;
+        if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
+      }
+    }
   }
   wsync();
   const T uw = wd;
@@ -998,12 +1029,17 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // whitened gradient g = u + sum_{x<0} D x B_r (lane = dof)
   auto gradient = [&]() {
     T gg = u;
-    T bn = dl ? Bm[lc] : (T)0;  // the next row's load is issued ahead of the branch
-    for (int r = 0; r < ne; r++) {
-      const T b = bn;
-      bn = r + 1 < ne && dl ? Bm[(r + 1) * Bs + lc] : (T)0;
-      const T xr = efc[8 * r + 1];
-      if (xr < 0) gg += efc[8 * r + 4] * xr * b;
+    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+      T xb[MGX_RB];
+      load_rows(xb, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+      for (int j = 0; j < MGX_RB; j++) {
+        const int r = r0 + j;
+        if (r < ne) {
+          const T xr = efc[8 * r + 1];
+          if (xr < 0) gg += efc[8 * r + 4] * xr * xb[j];
+        }
+      }
     }
     return dl ? gg : (T)0;
   };
@@ -1019,15 +1055,17 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       T acc[32];
 #pragma unroll
       for (int k = 0; k < 32; k++) acc[k] = l == i0 + k ? (T)1 : (T)0;
-      T bn = dl ? Bm[lc] : (T)0;
-      for (int r = 0; r < ne; r++) {
-        const T b = bn;
-        bn = r + 1 < ne && dl ? Bm[(r + 1) * Bs + lc] : (T)0;
-        const T xr = efc[8 * r + 1];
-        if (xr < 0) {
-          const T c = efc[8 * r + 4] * b;
+      for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+        T xb[MGX_RB];
+        load_rows(xb, Bm, Bs, r0, ne, lc, dl);
 #pragma unroll
-          for (int k = 0; k < 32; k++) acc[k] += c * readlane(b, (i0 + k) & 63);
+        for (int j = 0; j < MGX_RB; j++) {
+          const int r = r0 + j;
+          if (r < ne && efc[8 * r + 1] < 0) {
+            const T c = efc[8 * r + 4] * xb[j];
+#pragma unroll
+            for (int k = 0; k < 32; k++) acc[k] += c * readlane(xb[j], (i0 + k) & 63);
+          }
         }
       }
 #pragma unroll
@@ -1067,11 +1105,21 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       else if (l < k) p -= H[k * nv + l] * pk;
     }
     p = dl ? p : (T)0;
-    // J p per row, row-major (coalesced) with a wave reduction; lane 0 stores
-    for (int r = 0; r < ne; r++) {
-      const T x = dl ? Bm[r * Bs + lc] : (T)0;
-      const T jp = usum(x * p);
-      if (l == 0) efc[8 * r + 3] = jp;
+    // J p per row, row-major (coalesced, 8 rows per batch) with wave reductions; lane 0 stores
+    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+      T xb[MGX_RB];
+      load_rows(xb, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+      for (int j = 0; j < MGX_RB; j += 4) {
+        T s0 = xb[j] * p, s1 = xb[j + 1] * p, s2 = xb[j + 2] * p, s3 = xb[j + 3] * p;
+        wave_sum4(s0, s1, s2, s3);
+        if (l == 0) {
+          if (r0 + j < ne) efc[8 * (r0 + j) + 3] = s0;
+          if (r0 + j + 1 < ne) efc[8 * (r0 + j + 1) + 3] = s1;
+          if (r0 + j + 2 < ne) efc[8 * (r0 + j + 2) + 3] = s2;
+          if (r0 + j + 3 < ne) efc[8 * (r0 + j + 3) + 3] = s3;
+        }
+      }
     }
     wsync();
     // exact line search: f'(al) = u.p + al p.p + sum_{x + al jp < 0} D (x + al jp) jp
@@ -1118,7 +1166,13 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   wsync();
   // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = J'f = L' D^1/2 (sum f_r B_r)
   T v = 0;
-  for (int r = 0; r < ne; r++) v += efc[8 * r + 1] * Bm[r * Bs + lc];
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T xb[MGX_RB];
+    load_rows(xb, Bm, Bs, r0, ne, lc, dl);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++)
+      if (r0 + j < ne) v += efc[8 * (r0 + j) + 1] * xb[j];
+  }
   v = dl ? v : (T)0;
   T z = dl ? u * e.diaginv * sqrtD : (T)0;
   z = solve_L(m, e, e.qLD, z);
