@@ -11,16 +11,31 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(env, steps, rng, scale=1.0):
+    """Random actions within the action space. A non-finite observation is accepted only where
+    MuJoCo would produce one: the integrated state itself blew up (RK4 checks accelerations at
+    the first stage only), and then the next step must reset it (mj_checkPos / mj_checkVel:
+    the env's bad-state counter advances) and observe a finite state again."""
     obs, info = env.reset(seed=0)
     n_ep = 1
+    blown = None
     for _ in range(steps):
         a = (rng.uniform(env.action_space.low, env.action_space.high) * scale).astype(np.float32)
         obs, r, term, trunc, info = env.step(a)
-        assert obs.dtype == np.float32 and np.isfinite(obs).all()
+        warn = int(env._vec.batch.warning.sum())
+        assert obs.dtype == np.float32
+        if blown is not None:
+            assert warn > blown and np.isfinite(obs).all(), "bad state not reset on the next step"
+            blown = None
+        if not np.isfinite(obs).all():
+            state = np.concatenate([env._vec.batch.qpos[0].double().cpu().numpy(),
+                                    env._vec.batch.qvel[0].double().cpu().numpy()])
+            assert not np.isfinite(state).all(), "non-finite observation of a finite state"
+            blown = warn
         assert isinstance(r, float) and isinstance(term, bool) and isinstance(trunc, bool) and isinstance(info, dict)
         if term or trunc:
             obs, info = env.reset()
             n_ep += 1
+            blown = None
     return n_ep
 
 
