@@ -956,6 +956,68 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
   wsync();
 }
 
+// ---------------------------------------------------------------- Newton Hessian on MFMA
+// H = I + sum_{x_r<0} D_r B_r B_r' (nv x nv, lower triangle into row-major LDS) as a sum of
+// 16x16x4 MFMA products over chunks of 4 rows: tile (t, u) += A_t B_u with A_t[i][k] = s_k B[r0+k]
+// [16t+i] (s_k = D of an active row, else 0) and B_u[k][j] = B[r0+k][16u+j]; 10 lower tiles for
+// nv <= 64. Lane l holds A[l&15][l>>4] / B[l>>4][l&15] (one element each, 4 loads per chunk, 16
+// consecutive columns of one row per 16 lanes); C/D: col = l&15, row = 4(l>>4)+v (f32) or
+// (l>>4)+4v (f64) (cdna_hip_programming.md, fragment layout).
+template <typename T>
+__device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
+  typedef T V4 __attribute__((ext_vector_type(4)));
+  const int l = lane_id(), i = l & 15, kq = l >> 4;
+  const int nt = (nv + 15) >> 4;
+  auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
+  V4 acc[10];
+#pragma unroll
+  for (int t = 0, q = 0; t < 4; t++)
+#pragma unroll
+    for (int u = 0; u <= t; u++, q++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) acc[q][v] = (t == u && row_of(v) == i) ? (T)1 : (T)0;
+  auto load = [&](int r0, T* b, T& sc) {
+    const int r = r0 + kq;
+    sc = 0;
+    if (r < ne) {
+      const T x = efc[8 * r + 1];
+      sc = x < 0 ? efc[8 * r + 4] : (T)0;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int c = 16 * t + i;
+      b[t] = (r < ne && c < nv) ? Bm[r * Bs + c] : (T)0;
+    }
+  };
+  T bn[4], sn;
+  load(0, bn, sn);
+  for (int r0 = 0; r0 < ne; r0 += 4) {
+    T b[4] = {bn[0], bn[1], bn[2], bn[3]};
+    const T sc = sn;
+    load(r0 + 4, bn, sn);  // the next chunk is in flight during this chunk's MFMAs
+#pragma unroll
+    for (int t = 0, q = 0; t < 4; t++)
+#pragma unroll
+      for (int u = 0; u <= t; u++, q++) {
+        if (t < nt) {
+          if constexpr (sizeof(T) == 8)
+            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sc * b[t], b[u], acc[q], 0, 0, 0);
+          else
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(sc * b[t], b[u], acc[q], 0, 0, 0);
+        }
+      }
+  }
+#pragma unroll
+  for (int t = 0, q = 0; t < 4; t++)
+#pragma unroll
+    for (int u = 0; u <= t; u++, q++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        const int row = 16 * t + row_of(v), col = 16 * u + i;
+        if (t < nt && row < nv && col <= row) H[row * nv + col] = acc[q][v];
+      }
+}
+
 // ---------------------------------------------------------------- constraint solver (Newton)
 // mj_solNewton [ext] (restated in oracle/mjref.c newton_solve), in the whitened coordinates of
 // the PGS path: u = D^1/2 L (qacc - qacc_smooth), so 0.5 (a-a0)'M(a-a0) = 0.5 |u|^2 and
@@ -981,6 +1043,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     e.niter = 0;
     return;
   }
+  MGX_STAMP_DECL
   T qv = dl ? e.qvel[l] : (T)0;
   const T wv = sqrtD * mul_L(m, e, e.qLD, qv);
   const T ws = sqrtD * mul_L(m, e, e.qLD, e.qacc_smooth);
@@ -1044,35 +1107,14 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     return dl ? gg : (T)0;
   };
   T g = gradient();
+  MGX_STAMP(10);  // newton sub-stages (diagnostic build only): setup
   // mj_solNewton's loop order [ext]: update first, then test the scaled improvement and the
   // scaled gradient at the new point, so at least one iteration runs
   while (iter < maxit) {
-    // H = I + sum_{x<0} D B_r B_r', lower triangle, lane = column j: per active row one
-    // coalesced load of B_r (lane value b_j), then H[i][j] += (D b_j) b_i for the rows i of a
-    // 32-row half, b_i broadcast by readlane from registers; the next row's load is issued
-    // before the current row's FMAs so the global-scratch rows stream
-    for (int i0 = 0; i0 < nv; i0 += 32) {
-      T acc[32];
-#pragma unroll
-      for (int k = 0; k < 32; k++) acc[k] = l == i0 + k ? (T)1 : (T)0;
-      for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-        T xb[MGX_RB];
-        load_rows(xb, Bm, Bs, r0, ne, lc, dl);
-#pragma unroll
-        for (int j = 0; j < MGX_RB; j++) {
-          const int r = r0 + j;
-          if (r < ne && efc[8 * r + 1] < 0) {
-            const T c = efc[8 * r + 4] * xb[j];
-#pragma unroll
-            for (int k = 0; k < 32; k++) acc[k] += c * readlane(xb[j], (i0 + k) & 63);
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 32; k++)
-        if (i0 + k < nv && l <= i0 + k) H[(i0 + k) * nv + l] = acc[k];
-    }
+    // H = I + sum_{x<0} D B_r B_r' on MFMA (hessian_mfma), lower triangle
+    hessian_mfma(Bm, Bs, efc, ne, nv, H);
     wsync();
+    MGX_STAMP(11);  // Hessian
     // Cholesky H = L L' in place, left-looking, lane = row i: column k is
     // L[i][k] = (H[i][k] - sum_{j<k} L[i][j] L[k][j]) / L[k][k]; a lane's own row is written only
     // by itself, row k (broadcast reads) was finished by lane k before the barrier
@@ -1091,6 +1133,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       if (act) H[l * nv + k] = l == k ? d : s / d;
       wsync();
     }
+    MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y
     T y = -g;
     for (int k = 0; k < nv; k++) {
@@ -1105,6 +1148,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       else if (l < k) p -= H[k * nv + l] * pk;
     }
     p = dl ? p : (T)0;
+    MGX_STAMP(13);  // triangular solves
     // J p per row, row-major (coalesced, 8 rows per batch) with wave reductions; lane 0 stores
     for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
       T xb[MGX_RB];
@@ -1122,6 +1166,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       }
     }
     wsync();
+    MGX_STAMP(14);  // J p
     // exact line search: f'(al) = u.p + al p.p + sum_{x + al jp < 0} D (x + al jp) jp
     const T g0 = usum(u * p), pp = usum(p * p);
     T al = 1, lo = 0, hi = (T)1e30;
@@ -1140,6 +1185,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
       al = nxt;
       if (done) break;
     }
+    MGX_STAMP(15);  // line search
     u += al * p;
     T cp = 0;
     for (int r = l; r < ne; r += 64) {
@@ -1156,7 +1202,9 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     g = gradient();
     // the gradient rule is on the dof-space gradient M(a - a0) - J'f = L' D^1/2 g
     T ga = mul_LT(m, e, e.qLD, sqrtD * g);
-    if (improvement < tol || scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol) break;
+    const bool stop = improvement < tol || scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol;
+    MGX_STAMP(16);  // update, gradient, stop tests
+    if (stop) break;
   }
   e.niter = iter;
   for (int r = l; r < ne; r += 64) {

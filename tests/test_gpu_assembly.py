@@ -211,7 +211,7 @@ def test_env_steps_match_oracle():
     within 4 env steps at tolerance 1e-10 / 1e-12 / 3 iterations. The ensemble therefore spans
     solver paths: the unperturbed oracle, tolerance 1e-12 and 1e-14, 3 iterations, and a 1e-12
     qpos perturbation, all under the same commands. Each obs entry and the reward must lie in
-    the ensemble's range widened by its width (+1e-5); task state and termination must equal
+    the ensemble's range widened by twice its width (+1e-5); task state and termination must equal
     the unperturbed oracle's wherever the ensemble agrees. From the second step on the device is
     a further member of this family (its own rounding of the degenerate rows' Jacobian moves the
     arm by O(0.1) rad), so the ensemble bar applies to the first env step; the later steps
@@ -262,10 +262,11 @@ def test_env_steps_match_oracle():
             O = np.stack([x[0] for x in outs]).astype(np.float64)
             R = np.array([x[1] for x in outs])
             lo, hi = O.min(0), O.max(0)
-            w = hi - lo + 1e-5 * np.maximum(1.0, np.abs(O[0]))
+            # five solver paths sample the family sparsely: the bar is twice the ensemble width
+            w = 2 * (hi - lo) + 1e-5 * np.maximum(1.0, np.abs(O[0]))
             bad = np.flatnonzero((got_o[i] < lo - w) | (got_o[i] > hi + w))
             assert bad.size == 0, (i, t, bad, got_o[i][bad], O[:, bad])
-            wr = R.max() - R.min() + 1e-5 * max(1.0, abs(R[0]))
+            wr = 2 * (R.max() - R.min()) + 1e-5 * max(1.0, abs(R[0]))
             assert R.min() - wr <= got_r[i] <= R.max() + wr, (i, t, got_r[i], R)
             terms = [x[2] for x in outs]
             disc = lambda st: (st["held"], st["phase"], tuple(st["progress"]), tuple(st["status"]))  # noqa: E731

@@ -98,6 +98,11 @@ def main_task(task):
         print(f"  {st:16s} {v[:, i].mean():14.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {np.percentile(v[:, i], 99):.0f}")
     print(f"  per forward: nefc mean {raw[:, 20].sum() / calls:.1f}  solver iterations mean {raw[:, 21].sum() / calls:.2f}"
           f"  ncon mean {raw[:, 22].sum() / calls:.1f}")
+    sub = ["setup", "Hessian", "Cholesky", "triangular solves", "J p", "line search", "update+gradient+stop"]
+    if v[:, 10:17].sum() > 0:
+        print("  Newton sub-stages (inside the solver slot):")
+        for i, st in enumerate(sub):
+            print(f"    {st:22s} {v[:, 10 + i].mean():14.0f}")
     print(f"  lds bytes per env {env.native.info.lds_bytes_per_env}, scratch bytes per env "
           f"{env.native.info.scratch_bytes_per_env}")
 
