@@ -913,10 +913,13 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
   int iter = 0;
   while (iter < maxit) {
     T improvement = 0;
+    // one block ahead: the next block's 4 rows load while this block is solved
+    T nx0 = Bm[lc], nx1 = Bm[Bs + lc], nx2 = Bm[2 * Bs + lc], nx3 = Bm[3 * Bs + lc];
     for (int r0 = 0; r0 < ne4; r0 += 4) {
-      T bv0 = Bm[(r0 + 0) * Bs + lc], bv1 = Bm[(r0 + 1) * Bs + lc];
-      T bv2 = Bm[(r0 + 2) * Bs + lc], bv3 = Bm[(r0 + 3) * Bs + lc];
-      bv0 = dl ? bv0 : (T)0; bv1 = dl ? bv1 : (T)0; bv2 = dl ? bv2 : (T)0; bv3 = dl ? bv3 : (T)0;
+      const T bv0 = dl ? nx0 : (T)0, bv1 = dl ? nx1 : (T)0, bv2 = dl ? nx2 : (T)0, bv3 = dl ? nx3 : (T)0;
+      const int rn = r0 + 4 < ne4 ? r0 + 4 : r0;  // the last block re-reads itself (in bounds)
+      nx0 = Bm[rn * Bs + lc]; nx1 = Bm[(rn + 1) * Bs + lc];
+      nx2 = Bm[(rn + 2) * Bs + lc]; nx3 = Bm[(rn + 3) * Bs + lc];
       T d0 = bv0 * v, d1 = bv1 * v, d2 = bv2 * v, d3 = bv3 * v;
       wave_sum4(d0, d1, d2, d3);
       const T* a = blk + 2 * r0;
