@@ -46,7 +46,9 @@ METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 M
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
 PMC_PROFILE = "r02_v3_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
-PMC_PROFILE_BIPEDAL = "r01_bipedal_pmc.json"
+PMC_PROFILE_BIPEDAL = "r02_bipedal_pmc.json"
+PMC_PROFILE_ASSEMBLY = "r02_assembly_pmc.json"
+PMC_PROFILE_PARKOUR = "r02_parkour_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
@@ -559,11 +561,13 @@ def main():
             "config": {"workload": "robotic_arm_assembly_env, 1024 envs/GPU (BASELINE configs[4] task)",
                        "envs_per_gpu": N, "global_batch": N * world, "parallelism": f"dp{world} (env shards)",
                        "autoreset": "same-step (10 settle steps)", "substeps_per_step": 10, "solver": "Newton",
+                       "step_kernels": "mono",
                        "episodes_started": int(acc[1].item()), "terminated_total": int(acc[3].item()),
                        "bad_state_resets": int(acc[5].item()), "capacity_overflow_steps": overflow_steps,
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": _pmc_traffic(PMC_PROFILE_ASSEMBLY, N, args.precision, "mono"),
                          "kernel": "mgx_assembly_step = k_assembly<T,0,GB>", "alg_bytes_per_step": bytes_per_launch,
                          "launch_ms": round(launch_ms, 4)},
         }
@@ -580,11 +584,12 @@ def main():
             "data": "synthetic (U(-lim,lim) actions per joint, Philox reset draws)",
             "config": {"workload": "quadruped_parkour_env, 4096 envs/GPU (BASELINE configs[1])", "envs_per_gpu": N,
                        "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
-                       "substeps_per_step": 10, "episodes_started": int(acc[1].item()),
+                       "substeps_per_step": 10, "step_kernels": "mono", "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": _pmc_traffic(PMC_PROFILE_PARKOUR, N, args.precision, "mono"),
                          "kernel": "mgx_parkour_step = k_parkour<float,0>", "alg_bytes_per_step": bytes_per_launch,
                          "launch_ms": round(launch_ms, 4)},
         }
