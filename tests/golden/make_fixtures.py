@@ -128,6 +128,7 @@ class FakeModel:
     def __init__(self, c: mjcf.Model):
         self._c = c
         self.nu, self.nq, self.nv, self.nbody, self.ngeom = c.nu, c.nq, c.nv, c.nbody, c.ngeom
+        self.njnt = c.njnt
         self.jnt_qposadr = c.jnt_qposadr.copy()
         self.body_jntadr = c.body_jntadr.copy()
         self.jnt_dofadr = c.jnt_dofadr.copy()
@@ -1054,6 +1055,105 @@ def main_assembly():
     np.savez_compressed(f"{HERE}/assembly_envlogic.npz", **assembly_envlogic_vectors(env, 600))
 
 
+# ------------------------------------------------------------------------------- construction
+def construction_env():
+    """HumanoidConstructionEnv built by the reference constructor on the stubs, its scene being
+    the composed construction_site.xml captured in tests/golden/xml (construction_env.py:135-175).
+    gymnasium's Env.np_random is a property over _np_random (gymnasium/core.py); the stub gets
+    the same property here so seed() and reset(seed=...) drive one generator, as in gymnasium."""
+    import contextlib
+    import io
+    install_stubs()
+    mod = load_module(f"{REF}/humanoid_construction_env/construction_env.py", "ref_construction_env")
+    cls = mod.HumanoidConstructionEnv
+    with open(f"{HERE}/xml/humanoid_construction.xml") as f:
+        xml = f.read()
+    cls._load_xml_models = lambda self: setattr(self, "xml_string", xml)
+    cls.np_random = property(lambda self: self._np_random, lambda self, v: setattr(self, "_np_random", v))
+    with contextlib.redirect_stdout(io.StringIO()):
+        env = cls(render_mode=None)
+    return env
+
+
+CONSTRUCTION_TASKS = ('stack_blocks', 'operate_crane', 'transport_material', 'build_structure')
+
+
+def construction_reset_vectors(env, seeds):
+    """reset(seed) then an unseeded reset (construction_env.py:547-584): mj_resetData, the task
+    choice and three weather draws from the env generator, the initial observation."""
+    cols = {k: [] for k in ("seeds", "task", "weather", "obs", "task2", "weather2", "obs2")}
+    for s in seeds:
+        env.data.qpos[:] = 3.0  # garbage that mj_resetData must clear
+        obs, info = env.reset(seed=int(s))
+        w = [env.wind_strength, env.rain_intensity, env.temperature]
+        obs2, info2 = env.reset()
+        cols["seeds"].append(int(s))
+        cols["task"].append(CONSTRUCTION_TASKS.index(info["task"]))
+        cols["weather"].append(w)
+        cols["obs"].append(obs)
+        cols["task2"].append(CONSTRUCTION_TASKS.index(info2["task"]))
+        cols["weather2"].append([env.wind_strength, env.rain_intensity, env.temperature])
+        cols["obs2"].append(obs2)
+    return {k: np.asarray(v) for k, v in cols.items()}
+
+
+def construction_envlogic_vectors(env, n, seed=1357):
+    """Random synthetic states -> the reference's step() with mj_step stubbed out: clip, ctrl,
+    task progress, reward (numpy promotion: the float32 energy term makes it np.float32),
+    termination (fall / task complete / safety), truncation at 3000, observation, stats."""
+    c = env.model._c
+    rng = np.random.default_rng(seed)
+    hid = env.humanoid_id
+    cols = {k: [] for k in ("qpos", "qvel", "torso_z", "task", "blocks", "violations", "weather", "step_in",
+                            "progress_in", "completed_in", "total_in", "action", "ctrl", "obs", "reward",
+                            "reward_kind", "terminated", "truncated", "step_out", "progress_out", "completed_out",
+                            "total_out")}
+    for i in range(n):
+        d = env.data
+        d.reset()
+        d.qpos[:] = c.qpos0 + rng.normal(scale=0.5, size=c.nq)
+        d.qvel[:] = rng.normal(scale=rng.choice([0.1, 2.0, 10.0]), size=c.nv)
+        xpos = rng.uniform(-3, 3, (c.nbody, 3))
+        z = float(rng.choice([rng.uniform(0.0, 0.5), 0.5, rng.uniform(0.5, 1.0), 1.0, rng.uniform(1.0, 2.0)]))
+        xpos[hid, 2] = z
+        d.xpos[:] = xpos
+        task = int(rng.integers(0, 4))
+        env.current_task = CONSTRUCTION_TASKS[task]
+        env.blocks_placed = int(rng.choice([0, 1, 4, 5, 9, 10, 12, int(rng.integers(0, 20))]))
+        env.safety_violations = int(rng.choice([0, 0, 1, 3, 4, 7]))
+        env.wind_strength, env.rain_intensity, env.temperature = (float(rng.uniform(0, 5)), float(rng.uniform(0, 0.5)),
+                                                                  float(rng.uniform(15, 35)))
+        env.current_step = int(rng.choice([0, 1, 299, 300, 499, 500, 2998, 2999, 3000, int(rng.integers(0, 3500))]))
+        env.task_progress = float(rng.uniform(0, 1))
+        st = dict(env.episode_stats)
+        st['tasks_completed'] = int(rng.integers(0, 3))
+        st['total_reward'] = float(rng.choice([0.0, rng.normal(scale=1e4)]))
+        env.episode_stats = st
+        scale = rng.choice([1.0, 150.0, 400.0])
+        action = rng.uniform(-scale, scale, c.nu).astype(np.float32)
+        snap = dict(qpos=d.qpos.copy(), qvel=d.qvel.copy(), torso_z=z, task=task, blocks=env.blocks_placed,
+                    violations=env.safety_violations,
+                    weather=[env.wind_strength, env.rain_intensity, env.temperature], step_in=env.current_step,
+                    progress_in=env.task_progress, completed_in=st['tasks_completed'], total_in=st['total_reward'],
+                    action=action)
+        obs, reward, term, trunc, info = env.step(action)
+        out = dict(ctrl=d.ctrl.copy(), obs=obs, reward=float(reward),
+                   reward_kind={float: 0, np.float64: 1, np.float32: 2}[type(reward)],
+                   terminated=bool(term), truncated=bool(trunc), step_out=env.current_step,
+                   progress_out=float(env.task_progress), completed_out=env.episode_stats['tasks_completed'],
+                   total_out=float(env.episode_stats['total_reward']))
+        for k, v in {**snap, **out}.items():
+            cols[k].append(v)
+    return {k: np.asarray(v) for k, v in cols.items()}
+
+
+def main_construction():
+    env = construction_env()
+    np.savez_compressed(f"{HERE}/construction_reset.npz",
+                        **construction_reset_vectors(env, list(range(0, 40)) + [2024]))
+    np.savez_compressed(f"{HERE}/construction_envlogic.npz", **construction_envlogic_vectors(env, 800))
+
+
 def main_dancing():
     install_stubs()
     denv = dancing_env()
@@ -1076,6 +1176,7 @@ def main():
     main_dancing()
     main_martial()
     main_assembly()
+    main_construction()
     print("fixtures written to", HERE)
 
 
@@ -1088,6 +1189,8 @@ if __name__ == "__main__":
         main_martial()
     elif len(sys.argv) > 1 and sys.argv[1] == "assembly":
         main_assembly()
+    elif len(sys.argv) > 1 and sys.argv[1] == "construction":
+        main_construction()
     elif len(sys.argv) > 1 and sys.argv[1] == "soccer":
         install_stubs()
         np.savez_compressed(f"{HERE}/soccer_envlogic.npz", **soccer_envlogic_vectors(soccer_env(), 400))
