@@ -451,6 +451,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="soccer: split the rank's envs into this many stream shards (overlapping pipelines)")
     ap.add_argument("--no-f64-line", action="store_true", help="skip the fp64 parity-precision line (soccer)")
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly"])
     args = ap.parse_args()
@@ -493,8 +495,13 @@ def main():
         pool = [(torch.rand(N, 9, device=dev, generator=g) * alim + alo).contiguous() for _ in range(16)]
     else:
         from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
-        env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
-                              staged=not args.mono, banks=args.banks)
+        if args.streams > 1:
+            from mujoco_gymnasium_environments_amd.envs.soccer import StreamShardedSoccerEnv
+            env = StreamShardedSoccerEnv(N, args.streams, device=str(dev), precision=args.precision, seed=1234,
+                                         env_offset=env_offset(rank, N), staged=not args.mono, banks=args.banks)
+        else:
+            env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234,
+                                  env_offset=env_offset(rank, N), staged=not args.mono, banks=args.banks)
         pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]
     env.reset()
     for k in range(args.warmup):
@@ -502,9 +509,11 @@ def main():
     torch.cuda.synchronize(dev)
     # rollout metrics accumulate inside the kernel (env.rollout); read once after the timed region
     acc = torch.zeros(6, dtype=torch.float64, device=dev)  # env_steps, episodes, reward, term, trunc, bad
-    env.rollout.zero_()
-    env.batch.overflow.zero_()
-    ep0 = int(env.episode.sum().item())
+    shards = getattr(env, "shards", [env])  # StreamShardedSoccerEnv: per-shard metric buffers
+    for e in shards:
+        e.rollout.zero_()
+        e.batch.overflow.zero_()
+    ep0 = sum(int(e.episode.sum().item()) for e in shards)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
         dist.barrier()
@@ -519,12 +528,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    ro = env.rollout.double().sum(0)
+    ro = torch.cat([e.rollout for e in shards]).double().sum(0)
     acc[0] = ro[3]
-    acc[1] = float(env.episode.sum().item() - ep0)
+    acc[1] = float(sum(int(e.episode.sum().item()) for e in shards) - ep0)
     acc[2], acc[3], acc[4] = ro[0], ro[1], ro[2]
-    acc[5] = float(env.batch.warning.sum().item())
-    overflow_steps = int(env.batch.overflow.sum().item())
+    acc[5] = float(sum(float(e.batch.warning.sum().item()) for e in shards))
+    overflow_steps = sum(int(e.batch.overflow.sum().item()) for e in shards)
     acc, elapsed = reduce_rollout(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
     value = total_steps / elapsed
@@ -618,6 +627,7 @@ def main():
             "config": {"workload": "humanoid_soccer_env, 4096 envs/GPU (BASELINE configs[2])",
                        "envs_per_gpu": N, "global_batch": N * world, "parallelism": f"dp{world} (env shards)",
                        "autoreset": "same-step", "step_kernels": mode, "reset_banks": 0 if args.mono else args.banks,
+                       "stream_shards": args.streams,
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "capacity_overflow_steps": overflow_steps,
