@@ -111,6 +111,15 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   for (int k = l; k < 6 * m.nbody; k += 64) D[o.cvel + k] = e.cvel[k];
   for (int k = l; k < 3 * m.ngeom; k += 64) D[o.geom_xpos + k] = e.geom_xpos[k];
   for (int k = l; k < 9 * m.ngeom; k += 64) D[o.geom_xmat + k] = e.geom_xmat[k];
+  // contacts before the solve: with a Newton model in gB mode their frames share LDS with the
+  // Hessian (make_layout)
+  for (int c = l; c < e.ncon; c += 64) {
+    D[o.con_dist + c] = e.con_dist[c];
+    for (int k = 0; k < 3; k++) D[o.con_pos + 3 * c + k] = e.con_pos[3 * c + k];
+    for (int k = 0; k < 9; k++) D[o.con_frame + 9 * c + k] = e.con_frame[9 * c + k];
+    D[o.con_geom + 2 * c] = (T)e.con_geom[2 * c];
+    D[o.con_geom + 2 * c + 1] = (T)e.con_geom[2 * c + 1];
+  }
   wsync();
   make_constraint(m, e);
   if (l < m.nv) e.vec0[l] = sqrt(e.diaginv);
@@ -126,13 +135,6 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   for (int k = l; k < 4 * m.nbody; k += 64) D[o.xquat + k] = e.xquat[k];
   for (int k = l; k < 6 * m.nv; k += 64) D[o.cdof + k] = e.cdof[k];
   if (l == 0) { D[o.ncon] = (T)e.ncon; D[o.nefc] = (T)e.nefc; D[o.niter] = (T)e.niter; }
-  for (int c = l; c < e.ncon; c += 64) {
-    D[o.con_dist + c] = e.con_dist[c];
-    for (int k = 0; k < 3; k++) D[o.con_pos + 3 * c + k] = e.con_pos[3 * c + k];
-    for (int k = 0; k < 9; k++) D[o.con_frame + 9 * c + k] = e.con_frame[9 * c + k];
-    D[o.con_geom + 2 * c] = (T)e.con_geom[2 * c];
-    D[o.con_geom + 2 * c + 1] = (T)e.con_geom[2 * c + 1];
-  }
   for (int r = l; r < e.nefc; r += 64) {
     D[o.efc_type + r] = (T)e.efc_type[r]; D[o.efc_id + r] = (T)e.efc_id[r]; D[o.efc_pos + r] = e.efc[8 * r + 7];
     D[o.efc_margin + r] = e.efc_margin[r]; D[o.efc_R + r] = e.efc[8 * r + 2]; D[o.efc_aref + r] = e.efc[8 * r + 5];
