@@ -46,6 +46,7 @@ _NP = {"i": np.int32, "u": np.uint32, "d": np.float64}
 
 
 MGX_KEEP_CVEL = 1  # mgx_model_desc.layout_flags (include/mgx.h)
+MGX_ROWS_IN_SCRATCH = 2  # layout_flags: constraint rows in per-env global scratch (include/mgx.h)
 
 
 class MgxModelDesc(C.Structure):

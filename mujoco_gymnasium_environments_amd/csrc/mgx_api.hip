@@ -682,7 +682,8 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   int max_active = d->npair <= 256 ? 128 : (d->npair < 768 ? d->npair : 768);
   m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false);
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
-  if (m->L.bytes > 160 * 1024) m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false, true);
+  if (m->L.bytes > 160 * 1024 || (d->layout_flags & MGX_ROWS_IN_SCRATCH))
+    m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false, true);
   // the staged soccer pipeline (register-ring solver) handles Euler models up to 192 rows
   m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS && condim13;
   m->Ls = make_layout(d, rb, max_ncon, m->staged_ok ? max_nefc : 4, 128, true);

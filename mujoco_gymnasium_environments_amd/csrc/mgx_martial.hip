@@ -35,7 +35,7 @@ __device__ __forceinline__ void martial_reset_philox(const DevModel<T>& m, Env<T
 }
 
 // MODE 0: one env step (+ same-step autoreset); MODE 1: reset (host draws or Philox)
-template <typename T, int MODE>
+template <typename T, int MODE, bool GB>
 __global__ void __launch_bounds__(64) k_martial(DevModel<T> m, MartialIds ids, mgx_state s, mgx_martial_env me,
                                                 const float* action, const T* draws, float* obs, double* reward,
                                                 uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(64) k_martial(DevModel<T> m, MartialIds ids, m
   if (env >= n_env) return;
   if (mask && !mask[env]) return;
   Env<T> e;
-  env_bind(m, e, smem);
+  env_bind<T, GB>(m, e, smem, GB ? (T*)s.scratch + (size_t)env * m.L.gB_stride : nullptr);
   const int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
@@ -114,8 +114,12 @@ template <typename T, int MODE>
 void launch(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const mgx_martial_env* e, const float* action,
             const T* draws, float* obs, double* reward, uint8_t* term, uint8_t* trunc, float* final_obs, int autoreset,
             uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st) {
-  hipLaunchKernelGGL((k_martial<T, MODE>), dim3(n_env), dim3(64), m->L.bytes, st, M, m->ma, *s, *e, action, draws, obs,
-                     reward, term, trunc, final_obs, autoreset, seed, env_offset, n_env, mask);
+  if (m->L.gB)
+    hipLaunchKernelGGL((k_martial<T, MODE, true>), dim3(n_env), dim3(64), m->L.bytes, st, M, m->ma, *s, *e, action, draws,
+                       obs, reward, term, trunc, final_obs, autoreset, seed, env_offset, n_env, mask);
+  else
+    hipLaunchKernelGGL((k_martial<T, MODE, false>), dim3(n_env), dim3(64), m->L.bytes, st, M, m->ma, *s, *e, action, draws,
+                       obs, reward, term, trunc, final_obs, autoreset, seed, env_offset, n_env, mask);
 }
 
 }  // namespace
@@ -127,8 +131,8 @@ int mgx_martial_configure(mgx_model* m, const mgx_martial_ids* ids) {
   const bool f32 = m->precision == MGX_F32;
   const int nq = f32 ? m->mf.nq : m->md.nq, nv = f32 ? m->mf.nv : m->md.nv, nu = f32 ? m->mf.nu : m->md.nu;
   const int nb = f32 ? m->mf.nbody : m->md.nbody;
-  if ((f32 ? m->mf.integrator : m->md.integrator) != 0 || m->L.gB)
-    return fail(MGX_E_UNSUPPORTED, "the martial-arts kernels need an Euler model whose rows fit LDS");
+  if ((f32 ? m->mf.integrator : m->md.integrator) != 0)
+    return fail(MGX_E_UNSUPPORTED, "the martial-arts kernels need an Euler model");
   if ((f32 ? m->mf.solver : m->md.solver) != 2)
     return fail(MGX_E_UNSUPPORTED, "the martial-arts kernels solve with Newton (martial_arts_scene.xml:163)");
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
@@ -143,10 +147,13 @@ int mgx_martial_configure(mgx_model* m, const mgx_martial_ids* ids) {
   o.n_act = ids->n_act;
   o.max_episode_steps = ids->max_episode_steps;
   for (int k = 0; k < 32; k++) o.ctrl_scale[k] = ids->ctrl_scale[k];
-  const int rc = f32 ? (mgx_set_lds(k_martial<float, 0>, m->L.bytes) | mgx_set_lds(k_martial<float, 1>, m->L.bytes) |
-                        mgx_set_lds(k_martial_logic<float>, m->L.bytes))
-                     : (mgx_set_lds(k_martial<double, 0>, m->L.bytes) | mgx_set_lds(k_martial<double, 1>, m->L.bytes) |
-                        mgx_set_lds(k_martial_logic<double>, m->L.bytes));
+  const int rc =
+      f32 ? (mgx_set_lds(k_martial<float, 0, false>, m->L.bytes) | mgx_set_lds(k_martial<float, 1, false>, m->L.bytes) |
+             mgx_set_lds(k_martial<float, 0, true>, m->L.bytes) | mgx_set_lds(k_martial<float, 1, true>, m->L.bytes) |
+             mgx_set_lds(k_martial_logic<float>, m->L.bytes))
+          : (mgx_set_lds(k_martial<double, 0, false>, m->L.bytes) | mgx_set_lds(k_martial<double, 1, false>, m->L.bytes) |
+             mgx_set_lds(k_martial<double, 0, true>, m->L.bytes) | mgx_set_lds(k_martial<double, 1, true>, m->L.bytes) |
+             mgx_set_lds(k_martial_logic<double>, m->L.bytes));
   if (rc != MGX_OK) return rc;
   m->martial_ok = true;
   return MGX_OK;
@@ -161,6 +168,7 @@ int mgx_martial_step(const mgx_model* m, const mgx_state* s, const mgx_martial_e
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   const int rc = host_check_state(s);
   if (rc) return rc;
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
   if (m->precision == MGX_F32)
@@ -181,6 +189,7 @@ int mgx_martial_reset(const mgx_model* m, const mgx_state* s, const mgx_martial_
   if (!draws && !e->episode) return fail(MGX_E_ARG, "device draws need the episode counter buffer");
   const int rc = host_check_state(s);
   if (rc) return rc;
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
   if (m->precision == MGX_F32)

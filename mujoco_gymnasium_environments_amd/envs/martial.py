@@ -41,6 +41,10 @@ def martial_model() -> mjcf.Model:
     with open(ASSET) as f:
         m = mjcf.compile_xml(f.read())
     m.layout_flags = cabi.MGX_KEEP_CVEL  # the observation and reward read cvel (:536-589)
+    # constraint rows in per-env global scratch: the env's LDS drops from 65 to 30 KiB (fp32),
+    # five envs per CU instead of two; MGX_MARTIAL_ROWS_LDS=1 keeps them in LDS
+    if os.environ.get("MGX_MARTIAL_ROWS_LDS", "0") != "1":
+        m.layout_flags |= cabi.MGX_ROWS_IN_SCRATCH
     return m
 
 
