@@ -37,7 +37,7 @@ __device__ __forceinline__ void parkour_reset_philox(const DevModel<T>& m, Env<T
 }
 
 // MODE 0: one env step (+ same-step autoreset); MODE 1: reset (host draws or Philox)
-template <typename T, int MODE>
+template <typename T, int MODE, bool GB>
 __global__ void __launch_bounds__(64) k_parkour(DevModel<T> m, ParkourIds<T> ids, mgx_state s, mgx_parkour_env ev,
                                                 const float* action, const T* draws, float* obs, double* reward,
                                                 uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(64) k_parkour(DevModel<T> m, ParkourIds<T> ids
   if (env >= n_env) return;
   if (mask && !mask[env]) return;
   Env<T> e;
-  env_bind(m, e, smem);
+  env_bind<T, GB>(m, e, smem, GB ? (T*)s.scratch + (size_t)env * m.L.gB_stride : nullptr);
   int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
@@ -135,6 +135,13 @@ bool parkour_env_ok(const mgx_parkour_env* e) {
 
 }  // namespace
 
+// rows in LDS or, with MGX_ROWS_IN_SCRATCH / an oversize model, in per-env global scratch
+#define MGX_PK_LAUNCH(T, MODE, ...)                                  \
+  do {                                                               \
+    if (m->L.gB) hipLaunchKernelGGL((k_parkour<T, MODE, true>), __VA_ARGS__);  \
+    else hipLaunchKernelGGL((k_parkour<T, MODE, false>), __VA_ARGS__);        \
+  } while (0)
+
 extern "C" {
 
 int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
@@ -143,7 +150,7 @@ int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
   int nu = m->precision == MGX_F32 ? m->mf.nu : m->md.nu;
   int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
   if (ids->max_episode_steps <= 0) return fail(MGX_E_ARG, "max_episode_steps must be > 0");
-  if (m->L.gB || (m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
+  if ((m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
     return fail(MGX_E_UNSUPPORTED, "the parkour kernels need an Euler model whose rows fit LDS");
   if ((m->precision == MGX_F32 ? m->mf.solver : m->md.solver) != 0)
     return fail(MGX_E_UNSUPPORTED, "the parkour kernels solve with PGS (quadruped.xml:4)");
@@ -157,11 +164,13 @@ int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
   int rc;
   if (m->precision == MGX_F32) {
     fill_parkour_ids(m->pkf, ids);
-    rc = mgx_set_lds(k_parkour<float, 0>, m->L.bytes) | mgx_set_lds(k_parkour<float, 1>, m->L.bytes) |
+    rc = mgx_set_lds(k_parkour<float, 0, false>, m->L.bytes) | mgx_set_lds(k_parkour<float, 1, false>, m->L.bytes) |
+         mgx_set_lds(k_parkour<float, 0, true>, m->L.bytes) | mgx_set_lds(k_parkour<float, 1, true>, m->L.bytes) |
          mgx_set_lds(k_parkour_logic<float>, m->L.bytes);
   } else {
     fill_parkour_ids(m->pkd, ids);
-    rc = mgx_set_lds(k_parkour<double, 0>, m->L.bytes) | mgx_set_lds(k_parkour<double, 1>, m->L.bytes) |
+    rc = mgx_set_lds(k_parkour<double, 0, false>, m->L.bytes) | mgx_set_lds(k_parkour<double, 1, false>, m->L.bytes) |
+         mgx_set_lds(k_parkour<double, 0, true>, m->L.bytes) | mgx_set_lds(k_parkour<double, 1, true>, m->L.bytes) |
          mgx_set_lds(k_parkour_logic<double>, m->L.bytes);
   }
   if (rc != MGX_OK) return rc;
@@ -178,14 +187,15 @@ int mgx_parkour_step(const mgx_model* m, const mgx_state* s, const mgx_parkour_e
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
   if (m->precision == MGX_F32)
-    hipLaunchKernelGGL((k_parkour<float, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->pkf, *s, *e, action,
+    MGX_PK_LAUNCH(float, 0, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->pkf, *s, *e, action,
                        (const float*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
                        env_offset, n_env, mask);
   else
-    hipLaunchKernelGGL((k_parkour<double, 0>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->pkd, *s, *e, action,
+    MGX_PK_LAUNCH(double, 0, dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->pkd, *s, *e, action,
                        (const double*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
                        env_offset, n_env, mask);
   MGX_HIPCHK(hipGetLastError());
@@ -200,14 +210,15 @@ int mgx_parkour_reset(const mgx_model* m, const mgx_state* s, const mgx_parkour_
   if (!draws && !e->episode) return fail(MGX_E_ARG, "device draws need the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
   if (m->precision == MGX_F32)
-    hipLaunchKernelGGL((k_parkour<float, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->pkf, *s, *e,
+    MGX_PK_LAUNCH(float, 1, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->pkf, *s, *e,
                        (const float*)nullptr, (const float*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
                        (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
   else
-    hipLaunchKernelGGL((k_parkour<double, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->pkd, *s, *e,
+    MGX_PK_LAUNCH(double, 1, dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->pkd, *s, *e,
                        (const float*)nullptr, (const double*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
                        (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
   MGX_HIPCHK(hipGetLastError());

@@ -43,7 +43,13 @@ FINISH_POS = np.array([98.0, 0.0, 0.0])
 @functools.lru_cache(maxsize=None)
 def parkour_model() -> mjcf.Model:
     with open(ASSET) as f:
-        return mjcf.compile_xml(f.read())
+        m = mjcf.compile_xml(f.read())
+    # constraint rows in per-env global scratch: 48 -> 32 KiB LDS per env (fp32), five envs per CU
+    # instead of three; 27.6 -> 22.2 ms per step at 4096 envs.
+    # MGX_PARKOUR_ROWS_LDS=1 keeps them in LDS.
+    if os.environ.get("MGX_PARKOUR_ROWS_LDS", "0") != "1":
+        m.layout_flags = cabi.MGX_ROWS_IN_SCRATCH
+    return m
 
 
 def action_limits() -> np.ndarray:
