@@ -16,7 +16,8 @@ import sys
 
 STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_finish", "k_soccer_fixup", "k_soccer<float, 0>",
                 "k_soccer<double, 0>", "k_bipedal<float, 0, true>", "k_bipedal<float, 0, false>",
-                "k_parkour<float, 0>",
+                "k_parkour<float, 0>", "k_parkour<float, 0, true>", "k_parkour<float, 0, false>",
+                "k_martial<float, 0, true>", "k_martial<float, 0, false>",
                 "k_assembly<double, 0, true>", "k_assembly<double, 0, false>"]
 
 
