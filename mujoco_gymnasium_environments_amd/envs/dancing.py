@@ -57,7 +57,10 @@ BEAT = 0.5
 @functools.lru_cache(maxsize=None)
 def dancing_model() -> mjcf.Model:
     with open(ASSET) as f:
-        return mjcf.compile_xml(f.read())
+        m = mjcf.compile_xml(f.read())
+    if os.environ.get("MGX_DANCING_ROWS_SCRATCH", "0") == "1":  # rows in global scratch
+        m.layout_flags = cabi.MGX_ROWS_IN_SCRATCH
+    return m
 
 
 class DancingTables:
