@@ -58,7 +58,9 @@ BEAT = 0.5
 def dancing_model() -> mjcf.Model:
     with open(ASSET) as f:
         m = mjcf.compile_xml(f.read())
-    if os.environ.get("MGX_DANCING_ROWS_SCRATCH", "0") == "1":  # rows in global scratch
+    # constraint rows in per-env global scratch: 41 -> 25 KiB LDS per env (fp32), six envs per CU
+    # instead of three. MGX_DANCING_ROWS_LDS=1 keeps them in LDS.
+    if os.environ.get("MGX_DANCING_ROWS_LDS", "0") != "1":
         m.layout_flags = cabi.MGX_ROWS_IN_SCRATCH
     return m
 
