@@ -164,6 +164,11 @@ def test_bipedal_end_to_end_f64_matches_oracle(bipedal_model, bipedal_packed):
     o0 = obs.cpu().numpy()
     for i in good:
         np.testing.assert_allclose(o0[i], oracles[i].L.obs(oracles[i].s), atol=1e-5, err_msg=f"reset obs env {i}")
+    # the ill-conditioned trajectories are still compared up to the step where their obs leave
+    # the 1e-5 band (flags exact, reward within 1e-3 on every step before that)
+    tracking = {i for i in range(n) if i not in good
+                and np.max(np.abs(o0[i] - oracles[i].L.obs(oracles[i].s))) <= 1e-5}
+    compared = 0
     for k in range(steps):
         obs, rew, term, trunc, _ = env.step(_t(acts[k], torch.float32))
         torch.cuda.synchronize()
@@ -174,6 +179,15 @@ def test_bipedal_end_to_end_f64_matches_oracle(bipedal_model, bipedal_packed):
             np.testing.assert_allclose(ob[i], o, atol=1e-5, err_msg=f"obs env {i} step {k}")
             assert (rw[i] == r) if not np.isfinite(r) else abs(rw[i] - r) < 1e-3, (i, k, rw[i], r)
             assert te[i] == t1 and tr[i] == t2, (i, k)
+        for i in sorted(tracking):
+            o, r, t1, t2 = oracles[i].step(acts[k, i])
+            if not np.max(np.abs(ob[i] - o)) <= 1e-5:
+                tracking.discard(i)  # diverged: the oracle itself is sensitive here
+                continue
+            assert (rw[i] == r) if not np.isfinite(r) else abs(rw[i] - r) < 1e-3, (i, k, rw[i], r)
+            assert te[i] == t1 and tr[i] == t2, (i, k)
+            compared += 1
+    print(f"ill-conditioned envs: {compared} (env, step) pairs compared before divergence")
 
 
 def test_bipedal_autoreset_and_sharding_invariance():
