@@ -54,13 +54,21 @@ DT = 0.01667
 BEAT = 0.5
 
 
+def dancing_model(rows_in_scratch: Optional[bool] = None) -> mjcf.Model:
+    """The compiled model; rows_in_scratch None = the MGX_DANCING_ROWS_LDS environment variable, read at
+    each call (not once per process), and part of the cache key."""
+    if rows_in_scratch is None:
+        rows_in_scratch = os.environ.get("MGX_DANCING_ROWS_LDS", "0") != "1"
+    return _dancing_model(bool(rows_in_scratch))
+
+
 @functools.lru_cache(maxsize=None)
-def dancing_model() -> mjcf.Model:
+def _dancing_model(rows_in_scratch: bool) -> mjcf.Model:
     with open(ASSET) as f:
         m = mjcf.compile_xml(f.read())
     # constraint rows in per-env global scratch: 41 -> 25 KiB LDS per env (fp32), six envs per CU
     # instead of three (DESIGN.md §4). MGX_DANCING_ROWS_LDS=1 keeps them in LDS.
-    if os.environ.get("MGX_DANCING_ROWS_LDS", "0") != "1":
+    if rows_in_scratch:
         m.layout_flags = cabi.MGX_ROWS_IN_SCRATCH
     return m
 
@@ -105,10 +113,11 @@ class DancingVectorEnv:
     metadata = {'render_modes': [], 'render_fps': 60}
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
-                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
+                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
+                 rows_in_scratch: Optional[bool] = None):
         self.num_envs = num_envs
         self.device = torch.device(device)
-        self.model = dancing_model()
+        self.model = dancing_model(rows_in_scratch)
         self.tables = DancingTables(self.model, max_episode_steps)
         self.batch = PhysicsBatch(self.model, num_envs, precision=precision, device=device)
         self.native = self.batch.native

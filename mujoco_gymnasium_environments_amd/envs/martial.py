@@ -35,15 +35,23 @@ STAT_KEYS = ('techniques_performed', 'successful_combos', 'balance_maintained', 
              'total_distance_moved', 'falls')
 
 
+def martial_model(rows_in_scratch: Optional[bool] = None) -> mjcf.Model:
+    """The compiled model; rows_in_scratch None = the MGX_MARTIAL_ROWS_LDS environment variable, read at
+    each call (not once per process), and part of the cache key."""
+    if rows_in_scratch is None:
+        rows_in_scratch = os.environ.get("MGX_MARTIAL_ROWS_LDS", "0") != "1"
+    return _martial_model(bool(rows_in_scratch))
+
+
 @functools.lru_cache(maxsize=None)
-def martial_model() -> mjcf.Model:
+def _martial_model(rows_in_scratch: bool) -> mjcf.Model:
     """The scene the reference's _generate_xml_files writes (martial_arts_env.py:150-381)."""
     with open(ASSET) as f:
         m = mjcf.compile_xml(f.read())
     m.layout_flags = cabi.MGX_KEEP_CVEL  # the observation and reward read cvel (:536-589)
     # constraint rows in per-env global scratch: the env's LDS drops from 65 to 30 KiB (fp32),
     # five envs per CU instead of two (DESIGN.md §4); MGX_MARTIAL_ROWS_LDS=1 keeps them in LDS
-    if os.environ.get("MGX_MARTIAL_ROWS_LDS", "0") != "1":
+    if rows_in_scratch:
         m.layout_flags |= cabi.MGX_ROWS_IN_SCRATCH
     return m
 
@@ -85,10 +93,11 @@ class MartialArtsVectorEnv:
     metadata = {'render_modes': [], 'render_fps': 60}
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
-                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
+                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
+                 rows_in_scratch: Optional[bool] = None):
         self.num_envs = num_envs
         self.device = torch.device(device)
-        self.model = martial_model()
+        self.model = martial_model(rows_in_scratch)
         self.tables = MartialTables(self.model, max_episode_steps)
         self.batch = PhysicsBatch(self.model, num_envs, precision=precision, device=device)
         self.native = self.batch.native

@@ -40,14 +40,22 @@ START_POS = np.array([2.0, 0.0, 0.6])
 FINISH_POS = np.array([98.0, 0.0, 0.0])
 
 
+def parkour_model(rows_in_scratch: Optional[bool] = None) -> mjcf.Model:
+    """The compiled model; rows_in_scratch None = the MGX_PARKOUR_ROWS_LDS environment variable, read at
+    each call (not once per process), and part of the cache key."""
+    if rows_in_scratch is None:
+        rows_in_scratch = os.environ.get("MGX_PARKOUR_ROWS_LDS", "0") != "1"
+    return _parkour_model(bool(rows_in_scratch))
+
+
 @functools.lru_cache(maxsize=None)
-def parkour_model() -> mjcf.Model:
+def _parkour_model(rows_in_scratch: bool) -> mjcf.Model:
     with open(ASSET) as f:
         m = mjcf.compile_xml(f.read())
     # constraint rows in per-env global scratch: 48 -> 32 KiB LDS per env (fp32), five envs per CU
     # instead of three; 27.6 -> 22.2 ms per step at 4096 envs (DESIGN.md §4).
     # MGX_PARKOUR_ROWS_LDS=1 keeps them in LDS.
-    if os.environ.get("MGX_PARKOUR_ROWS_LDS", "0") != "1":
+    if rows_in_scratch:
         m.layout_flags = cabi.MGX_ROWS_IN_SCRATCH
     return m
 
@@ -98,10 +106,11 @@ class ParkourVectorEnv:
     metadata = {'render_modes': [], 'render_fps': 100}
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
-                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
+                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
+                 rows_in_scratch: Optional[bool] = None):
         self.num_envs = num_envs
         self.device = torch.device(device)
-        self.model = parkour_model()
+        self.model = parkour_model(rows_in_scratch)
         self.tables = ParkourTables(self.model, max_episode_steps)
         self.batch = PhysicsBatch(self.model, num_envs, precision=precision, device=device)
         self.native = self.batch.native

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 import functools
+from collections.abc import Mapping
 import os
 from typing import Any, Dict, Optional, Tuple
 
@@ -218,27 +219,23 @@ class SoccerVectorEnv:
         pass
 
 
-class _CatInfo(dict):
+class _CatInfo(Mapping):
     """info() of a stream-sharded batch: each field is the shards' device views concatenated on
-    first access (no kernels are launched for fields the caller never reads)."""
+    first access (no kernels are launched for fields the caller never reads). A read-only
+    Mapping, so get / items / values / `in` all go through __getitem__ and agree with the
+    single-batch SoccerVectorEnv.info() dict."""
 
     def __init__(self, shards):
-        super().__init__()
         self._shards = shards
         self._keys = list(shards[0].info().keys())
+        self._cache: Dict[str, Any] = {}
 
     def __getitem__(self, k):
-        if not dict.__contains__(self, k):
+        if k not in self._cache:
             if k not in self._keys:
                 raise KeyError(k)
-            dict.__setitem__(self, k, torch.cat([s.info()[k] for s in self._shards]))
-        return dict.__getitem__(self, k)
-
-    def keys(self):
-        return list(self._keys)
-
-    def __contains__(self, k):
-        return k in self._keys
+            self._cache[k] = torch.cat([s.info()[k] for s in self._shards])
+        return self._cache[k]
 
     def __iter__(self):
         return iter(self._keys)

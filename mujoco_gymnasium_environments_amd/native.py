@@ -40,29 +40,43 @@ def build(force: bool = False, verbose: bool = False) -> str:
     def deps(src):
         return [os.path.join(CSRC, src)] + common + [os.path.join(CSRC, h) for h in TU_HEADERS.get(src, [])]
 
-    if not force and os.path.exists(LIB_PATH):
-        lib_t = os.path.getmtime(LIB_PATH)
-        if all(os.path.getmtime(d) <= lib_t for src in SOURCES for d in deps(src)):
-            return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
     build_dir = os.path.join(PKG, "_build")
+
+    def command(src, obj):
+        return [hipcc, *flags, *SOURCE_FLAGS.get(src, []), "-c", "-o", obj, os.path.join(CSRC, src)]
+
+    def stamp_ok(src, obj):
+        # an object is reused only when it is newer than its source and headers AND was built by
+        # the same command (compiler, common and per-source flags), recorded next to it
+        try:
+            with open(obj + ".cmd") as f:
+                if f.read() != " ".join(command(src, obj)):
+                    return False
+        except OSError:
+            return False
+        return all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in deps(src))
+
+    objs = [os.path.join(build_dir, src.replace(".hip", ".o")) for src in SOURCES]
+    if not force and os.path.exists(LIB_PATH):
+        lib_t = os.path.getmtime(LIB_PATH)
+        if all(os.path.exists(o) and stamp_ok(s, o) and os.path.getmtime(o) <= lib_t for s, o in zip(SOURCES, objs)):
+            return LIB_PATH
     os.makedirs(build_dir, exist_ok=True)
     # one translation unit per task family, compiled in parallel, then linked
     procs = []
-    objs = []
-    for src in SOURCES:
-        obj = os.path.join(build_dir, src.replace(".hip", ".o"))
-        objs.append(obj)
-        if not force and os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in deps(src)):
-            continue  # object newer than its source and headers
-        procs.append((src, subprocess.Popen([hipcc, *flags, *SOURCE_FLAGS.get(src, []), "-c", "-o", obj,
-                                             os.path.join(CSRC, src)],
-                                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
-    for src, p in procs:
+    for src, obj in zip(SOURCES, objs):
+        if not force and os.path.exists(obj) and stamp_ok(src, obj):
+            continue
+        cmd = command(src, obj)
+        procs.append((src, obj, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+    for src, obj, cmd, p in procs:
         _, err = p.communicate()
         if p.returncode != 0:
             raise NativeError(f"hipcc {src} failed ({p.returncode}):\n{err[-4000:]}")
+        with open(obj + ".cmd", "w") as f:
+            f.write(" ".join(cmd))
     r = subprocess.run([hipcc, *flags, "-shared", "-o", LIB_PATH + ".tmp", *objs], capture_output=True, text=True)
     if r.returncode != 0:
         raise NativeError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-4000:]}")

@@ -53,11 +53,20 @@ class TimeLimit:
         return self.env.reset(seed=seed, options=options)
 
     def step(self, action):
+        if self._elapsed_steps is None:  # gym.make's OrderEnforcing wrapper raises here
+            raise ResetNeeded("Cannot call env.step() before calling env.reset()")
         obs, reward, terminated, truncated, info = self.env.step(action)
         self._elapsed_steps += 1
         if self._elapsed_steps >= self._max_episode_steps:
             truncated = True
         return obs, reward, terminated, truncated, info
+
+
+try:  # gymnasium.error.ResetNeeded when gymnasium is importable, else a local stand-in
+    from gymnasium.error import ResetNeeded  # type: ignore
+except Exception:  # noqa: BLE001
+    class ResetNeeded(RuntimeError):
+        """step() before reset() (gymnasium.error.ResetNeeded)."""
 
 
 def _load(entry: str):

@@ -138,3 +138,12 @@ def test_stream_sharded_equals_single_batch(soccer_model):
     assert torch.equal(one.episode, sh.episode)
     assert torch.equal(one.info()["episode_stats"], sh.info()["episode_stats"])
     assert torch.equal(one.batch.qpos, torch.cat([s.batch.qpos for s in sh.shards]))
+    # info() of the sharded batch behaves as the single batch's dict through every Mapping call
+    i1, i2 = one.info(), sh.info()
+    assert set(i2) == set(i1) and len(i2) == len(i1)
+    assert torch.equal(i2.get("final_observation"), i1["final_observation"])
+    assert i2.get("no_such_key") is None
+    d2 = dict(i2.items())
+    for k, v in i1.items():
+        assert torch.equal(d2[k], v), k
+    assert all(torch.equal(a, i1[k]) for k, a in zip(i2.keys(), i2.values()))
