@@ -45,7 +45,8 @@ sys.path.insert(0, ROOT)
 METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
-PMC_PROFILE = "r02_v3_pmc.json"  # latest tools/profile_round.sh summary (HBM traffic per step)
+# latest tools/profile_round.sh summaries of the soccer step (HBM traffic per step), per precision
+PMC_PROFILE = {"f64": "r03_f64_pmc.json", "f32": "r03_f32_pmc.json"}
 PMC_PROFILE_BIPEDAL = "r02_bipedal_pmc.json"
 PMC_PROFILE_ASSEMBLY = "r02_assembly_2pcu_pmc.json"
 PMC_PROFILE_PARKOUR = "r02_parkour_scr_pmc.json"
@@ -53,6 +54,8 @@ PMC_PROFILE_PARKOUR = "r02_parkour_scr_pmc.json"
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
 ALG_BYTES_PER_ENV_STEP = 4 * (2 * 121 + 33 + 2 * 3 + 2 * 11 + 80) + 8 + 2
+# the same in the parity precision: state, goalkeeper / wind forces and task scalars in fp64
+ALG_BYTES_PER_ENV_STEP_F64 = 8 * (2 * 121 + 2 * 3 + 2 * 11) + 4 * (33 + 80) + 8 + 2
 # parkour: r/w qpos 38 + qvel 37 + qacc_warmstart 37, r/w the 2 obstacle-motor
 # ctrl, read action 16, r/w last_position 3 + max_progress 1 (fp32), r/w episode_reward (fp64)
 # + er_kind (u8) + reached/fall/stuck/step (int32), write obs 95, reward (fp64), flags (u8)
@@ -415,11 +418,13 @@ def soccer_flops(ro: torch.Tensor, nv: int) -> dict:
             "pgs_sweeps_mean": float(ro[5]) / max(steps, 1.0)}
 
 
-def f64_parity_line(args, dev, N, g) -> dict:
-    """The same step in parity precision (fp64, SURVEY §7 'report both'): a short timed run on the
-    staged fp64 kernels after the headline's timed region."""
+def other_precision_line(args, dev, N, g, precision: str) -> dict:
+    """The same staged step in the other precision (SURVEY §7 'report both'): a short timed run
+    after the headline's timed region. fp64 is the parity precision (tests/test_gpu_f32_staged.py:
+    1000-step drift vs the oracle < 1e-4); fp32 is faster but misses that bar (median drift 3e-4
+    at step 1000), so it is reported here and never as the headline."""
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
-    env = SoccerVectorEnv(N, device=str(dev), precision="f64", seed=1234, staged=True, banks=args.banks)
+    env = SoccerVectorEnv(N, device=str(dev), precision=precision, seed=1234, staged=True, banks=args.banks)
     pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(4)]
     env.reset()
     for k in range(5):
@@ -434,9 +439,11 @@ def f64_parity_line(args, dev, N, g) -> dict:
     b.record()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    note = ("parity precision (tests/test_gpu_f32_staged.py: 1000-step drift vs the oracle < 1e-4)"
+            if precision == "f64" else
+            "fast precision; misses the north_star 1e-4 drift bar over 1000 steps (median 3e-4, DESIGN.md §2)")
     return {"value": round(N * steps / el, 1), "unit": "env_steps/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "launch_ms": round(a.elapsed_time(b) / steps, 4), "steps": steps, "dtype": "f64",
-            "note": "parity precision (tests/test_gpu_f32_staged.py: 1000-step drift vs the oracle < 1e-4)"}
+            "launch_ms": round(a.elapsed_time(b) / steps, 4), "steps": steps, "dtype": precision, "note": note}
 
 
 def main():
@@ -445,7 +452,10 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default 4096; 8192 for bipedal)")
-    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    # soccer's headline precision is fp64: the precision that meets the north_star accuracy bar
+    # (qpos drift < 1e-4 over 1000 steps vs the fp64 oracle); fp32 rides along as an extra key
+    ap.add_argument("--precision", default=None, choices=["f32", "f64"],
+                    help="default: f64 for soccer (the headline), f32 for the other tasks")
     ap.add_argument("--cpu-envs", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -453,11 +463,14 @@ def main():
     ap.add_argument("--banks", type=int, default=4)
     ap.add_argument("--streams", type=int, default=1,
                     help="soccer: split the rank's envs into this many stream shards (overlapping pipelines)")
-    ap.add_argument("--no-f64-line", action="store_true", help="skip the fp64 parity-precision line (soccer)")
+    ap.add_argument("--no-f64-line", "--no-other-line", dest="no_f64_line", action="store_true",
+                    help="skip the other-precision soccer line (fp32 when the headline is fp64)")
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly"])
     args = ap.parse_args()
     if args.task != "soccer":
         args.mono = True  # one fused wave-per-env launch per step
+    if args.precision is None:
+        args.precision = "f64" if args.task == "soccer" else "f32"
     if args.envs <= 0:
         args.envs = {"bipedal": 8192, "mixed": 1024, "assembly": 1024}.get(args.task, 4096)
 
@@ -607,19 +620,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline_parkour(max(1, args.cpu_envs // 4), args.cpu_steps // 4)
         print(json.dumps(out))
     elif rank == 0:
-        bytes_per_launch = ALG_BYTES_PER_ENV_STEP * N
+        alg = ALG_BYTES_PER_ENV_STEP_F64 if args.precision == "f64" else ALG_BYTES_PER_ENV_STEP
+        bytes_per_launch = alg * N
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        traffic = None
         mode = "mono" if args.mono else "staged"
-        pmc = os.path.join(ROOT, "profiles", PMC_PROFILE)
-        if os.path.exists(pmc):
-            try:
-                with open(pmc) as f:
-                    p = json.load(f)
-                if p.get("envs") == N and p.get("precision") == args.precision and p.get("mode") == mode:
-                    traffic = p.get("hbm_bytes_per_step")
-            except Exception:  # noqa: BLE001
-                traffic = None
+        traffic = _pmc_traffic(PMC_PROFILE[args.precision], N, args.precision, mode)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -637,6 +642,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ("mgx_soccer_step = k_soccer_rows + k_pgs_groups + k_soccer_finish + k_soccer_fixup"
                                     if mode == "staged" else "mgx_soccer_step = k_soccer<T,0>"),
+                         "profile": f"profiles/{PMC_PROFILE[args.precision]}",
                          "alg_bytes_per_step": bytes_per_launch, "launch_ms": round(launch_ms, 4),
                          "note": "achieved = algorithmic bytes of one env step x envs / HIP-event time of the "
                                  "step's launches; traffic = PMC HBM bytes of those launches per step"},
@@ -649,8 +655,9 @@ def main():
                                  "nefc_mean": round(fl["nefc_mean"], 2), "pgs_sweeps_mean": round(fl["pgs_sweeps_mean"], 2),
                                  "definition": "SURVEY 8(d) dense-equivalent: 2 nefc^2 nv (A) + 2 sweeps nefc^2 (PGS) "
                                                "+ 300 nbody, summed per env step in the kernel"}
-        if not args.no_f64_line and world == 1 and args.precision == "f32":
-            out["f64_parity_mode"] = f64_parity_line(args, dev, N, g)
+        if not args.no_f64_line and world == 1 and not args.mono and args.streams == 1:
+            other = "f32" if args.precision == "f64" else "f64"
+            out[f"{other}_line"] = other_precision_line(args, dev, N, g, other)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_steps)
         print(json.dumps(out))
