@@ -17,10 +17,10 @@ metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
 step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obstacle motors,
 obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
 
---task mixed benchmarks BASELINE configs[4] over the tasks this build simulates (soccer,
-parkour, bipedal, dancing, martial arts, assembly; construction is not built yet): 1024 envs per task
-on one GPU, each task's fused step on its own HIP stream so the ragged models overlap on the
-chip; one step = one env step of every task; value = all tasks' env steps / wall time.
+--task mixed benchmarks BASELINE configs[4], all seven tasks (soccer, parkour, bipedal, dancing,
+martial arts, assembly, construction): 1024 envs per task on one GPU, each task's fused step on its
+own HIP stream so the ragged models overlap on the chip; one step = one env step of every task;
+value = all tasks' env steps / wall time.
 
 --task bipedal benchmarks BASELINE configs[3] (bipedal_rescue, 8192 envs/GPU by default): one
 step = BipedalVectorEnv.step = mgx_bipedal_step (clip, float32 energy, one RK4 mj_step with the
@@ -77,6 +77,9 @@ MARTIAL_ALG_BYTES = 4 * (2 * 144 + 2 * 28 + 28 + 2 * 4 + 113) + 8 * (2 * 5 + 1) 
 # assembly: r/w qpos 72 + qvel 63 + qacc_warmstart 63 and ctrl 9 (fp32), action 9, r/w 16 int32
 # task words + cumulative reward (fp64), obs 110, reward, flags
 ASSEMBLY_ALG_BYTES = 4 * (2 * 198 + 2 * 9 + 9 + 2 * 16 + 110) + 8 * (2 + 1) + 2
+# construction (fp64): r/w qpos 110 + qvel 99 + qacc_warmstart 99 and ctrl 33, action 33 (fp32), r/w
+# 4 fp64 + 5 int32 task scalars and the fp32 total, obs 135, reward, flags
+CONSTRUCTION_ALG_BYTES = 8 * (2 * 308 + 2 * 33 + 2 * 4 + 1) + 4 * (33 + 2 * 5 + 2 + 135) + 2
 ASSEMBLY_METRIC = "env steps/sec (whole node), robotic_arm_assembly 1024 envs/GPU (10 Newton substeps per env step)"
 MIXED_METRIC = "env steps/sec (whole node), all tasks mixed, 1024 envs each on 1 MI355X (BASELINE configs[4])"
 
@@ -309,6 +312,7 @@ def bench_mixed(args, dev, world, rank, dist):
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout
     from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
     from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+    from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
     from mujoco_gymnasium_environments_amd.envs.dancing import DancingVectorEnv
     from mujoco_gymnasium_environments_amd.envs.martial import MartialArtsVectorEnv
     from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv, action_limits
@@ -338,6 +342,11 @@ def bench_mixed(args, dev, world, rank, dist):
         # degenerate base contact breaks the fp32 Newton factorisation, envs/assembly.py)
         "robotic_arm_assembly": (AssemblyVectorEnv(N, device=str(dev), precision="f64"),
                                  lambda: torch.rand(N, 9, device=dev, generator=g) * alim + alo, ASSEMBLY_ALG_BYTES),
+        # construction: fp64 like assembly (RK4 + Newton on the wide kernels, nv 99; its parity
+        # tests run in fp64, tests/test_gpu_construction.py)
+        "humanoid_construction": (ConstructionVectorEnv(N, device=str(dev), precision="f64", seed=17, env_offset=off),
+                                  lambda: (torch.rand(N, 33, device=dev, generator=g) * 2 - 1) * 200.0,
+                                  CONSTRUCTION_ALG_BYTES),
     }
     streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
     pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
@@ -391,11 +400,12 @@ def bench_mixed(args, dev, world, rank, dist):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (uniform actions within each task's action_space, Philox reset draws)",
             "config": {"workload": "all tasks mixed, 1024 envs each on 1 GPU (BASELINE configs[4])",
-                       "tasks": list(tasks), "tasks_missing": ["humanoid_construction"],
+                       "tasks": list(tasks), "tasks_missing": [],
                        "envs_per_task": N, "global_batch": N * len(tasks) * world,
                        "parallelism": f"dp{world} (env shards), one HIP stream per task",
                        "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},
-                       "task_dtype": {k: ("f64" if k == "robotic_arm_assembly" else args.precision) for k in tasks},
+                       "task_dtype": {k: ("f64" if k in ("robotic_arm_assembly", "humanoid_construction")
+                                          else args.precision) for k in tasks},
                        "bad_state_resets": int(acc[5].item())},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": f"{dom} step (dominant stream)",

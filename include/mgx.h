@@ -545,6 +545,59 @@ typedef struct mgx_assembly_logic_io {
 int mgx_assembly_logic_test(const mgx_model *m, const mgx_assembly_logic_io *io, const mgx_assembly_env *e,
                             int n_env, void *stream);
 
+/* ---- humanoid_construction env logic fused with physics (RK4, Newton, nv 99: wide kernels) -- */
+#define MGX_CONSTRUCTION_OBS 135
+/* Index tables (humanoid_construction_env/construction_env.py:511-516, :38, :520-523). */
+typedef struct mgx_construction_ids {
+  int32_t humanoid;           /* body id of 'humanoid' (:513); its xpos[2] drives reward / termination */
+  int32_t n_act;              /* actuators written from the action (nu = 33, ctrl[:] = action :592) */
+  int32_t max_episode_steps;  /* 3000 (:38) */
+  float action_limit;         /* 200 (:522-523) */
+} mgx_construction_ids;
+
+/* Persistent per-env task state (device, env-major). */
+typedef struct mgx_construction_env {
+  double *scal;         /* [N][4] task_progress, wind_strength, rain_intensity, temperature */
+  int32_t *ints;        /* [N][5] current_task, current_step, blocks_placed, safety_violations,
+                           tasks_completed (episode_stats) */
+  float *total_reward;  /* [N] episode_stats['total_reward'] (np.float32 from the first step on, C2) */
+  int32_t *episode;     /* [N] episodes started (keys the device reset draws); nullable when every
+                           reset passes host draws */
+  double *rollout;      /* [N][4] fp64 running sums: reward, terminated, truncated, env steps (nullable) */
+} mgx_construction_env;
+
+/* Accepts only models with 64 < nv <= 128, RK4 and Newton (the wide kernels, mgx_wide.h). */
+int mgx_construction_configure(mgx_model *m, const mgx_construction_ids *ids);
+
+/* One env step for N envs (construction_env.py:586-623): clip to +-200, ctrl = action, one RK4
+ * mj_step (Newton), step counter, task progress, reward [N] float64 (the np.float32 value, C2),
+ * terminated / truncated, observation [N][135] float32. autoreset != 0: ended envs reset in the
+ * same launch (mj_resetData + Philox draws keyed by (seed, env_offset + env, episode)). */
+int mgx_construction_step(const mgx_model *m, const mgx_state *s, const mgx_construction_env *e,
+                          const float *action, float *obs, double *reward, uint8_t *terminated,
+                          uint8_t *truncated, float *final_obs, int autoreset, uint64_t seed, int env_offset,
+                          int n_env, const uint8_t *env_mask, void *stream);
+
+/* reset() for masked envs (:547-584): mj_resetData, task + weather draws (`draws` [N][4] real:
+ * task index, wind, rain, temperature in reference order; NULL = device Philox), counters
+ * cleared, observation (no forward pass: the reference calls none). */
+int mgx_construction_reset(const mgx_model *m, const mgx_state *s, const mgx_construction_env *e,
+                           const void *draws, float *obs, uint64_t seed, int env_offset, int n_env,
+                           const uint8_t *env_mask, void *stream);
+
+/* Test hook: construction env logic only (clip/ctrl, progress, reward, termination, obs) on
+ * caller-supplied state (no physics). */
+typedef struct mgx_construction_logic_io {
+  const void *qpos, *qvel, *xpos;  /* [N][nq] [N][nv] [N][nbody][3] */
+  void *ctrl;                      /* out [N][nu] */
+  const float *action;             /* [N][n_act] */
+  float *obs;                      /* [N][135] */
+  double *reward;
+  uint8_t *terminated, *truncated;
+} mgx_construction_logic_io;
+int mgx_construction_logic_test(const mgx_model *m, const mgx_construction_logic_io *io,
+                                const mgx_construction_env *e, int n_env, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

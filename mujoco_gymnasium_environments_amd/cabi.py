@@ -191,6 +191,20 @@ class MgxDancingLogicIO(C.Structure):
                 ("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p), ("truncated", C.c_void_p)]
 
 
+class MgxConstructionIds(C.Structure):
+    _fields_ = [("humanoid", C.c_int32), ("n_act", C.c_int32), ("max_episode_steps", C.c_int32),
+                ("action_limit", C.c_float)]
+
+
+class MgxConstructionEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["scal", "ints", "total_reward", "episode", "rollout"]]
+
+
+class MgxConstructionLogicIO(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["qpos", "qvel", "xpos", "ctrl", "action", "obs", "reward", "terminated",
+                                          "truncated"]]
+
+
 class MgxSoccerIds(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ["torso", "ball", "goalkeeper", "ball_geom", "right_foot", "left_foot", "field_geom",

@@ -375,9 +375,10 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb);
   L.qLD = take(d->nM); L.qMH = take(d->nM); L.con_dist = take(max_ncon); L.con_mu = take(max_ncon);
   L.carry_reals = p;
-  L.vec0 = take(64); L.vec1 = take(64); L.vec2 = take(64); L.vec3 = take(64);
+  const int nvw = nv > 64 ? 128 : 64;  // dof-indexed scratch vectors: one or two dofs per lane
+  L.vec0 = take(nvw); L.vec1 = take(nvw); L.vec2 = take(nvw); L.vec3 = take(nvw);
   int vec_end = p;
-  L.rk = (!staged && d->integrator == 1) ? take(((d->nq + 3) & ~3) + 64) : 0;
+  L.rk = (!staged && d->integrator == 1) ? take(((d->nq + 3) & ~3) + nvw) : 0;
   // persistent for the rest of the forward pass
   // Newton with rows in global scratch (gB): the Hessian / its factor overlay the phase-A union,
   // dead from the row transform on (newton() is its only user; no env logic reads a union array
@@ -494,14 +495,17 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
     for (int c = 0; c < depth[b]; c++) chain[b * MGX_MAX_DEPTH + c] = path[depth[b] - 1 - c];
   }
   std::vector<int> chainlen(nv), anc(nv * MGX_MAX_DEPTH, -1), ancadr(nv * MGX_MAX_DEPTH, 0);
-  std::vector<uint64_t> ancmask(nv, 0);
+  std::vector<uint64_t> ancmask(nv, 0), ancmask_hi(nv, 0);
   for (int k = 0; k < nv; k++) {
     int t = 0;
     for (int j = k; j >= 0; j = d->dof_parentid[j], t++) {
       if (t >= MGX_MAX_DEPTH) return fail(MGX_E_CAPACITY, "dof chain longer than MGX_MAX_DEPTH");
       anc[k * MGX_MAX_DEPTH + t] = j;
       ancadr[k * MGX_MAX_DEPTH + t] = d->dof_Madr[j];
-      if (j != k) ancmask[k] |= 1ull << j;
+      if (j != k) {
+        if (j < 64) ancmask[k] |= 1ull << j;
+        else ancmask_hi[k] |= 1ull << (j - 64);
+      }
     }
     chainlen[k] = t;
   }
@@ -526,6 +530,7 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
   B.ints(d->dof_parentid, nv, &M.dof_parentid); B.ints(d->dof_Madr, nv, &M.dof_Madr);
   B.ints(chainlen.data(), nv, &M.dof_chainlen); B.ints(anc.data(), anc.size(), &M.dof_anc);
   B.add(ancmask.data(), 8 * ancmask.size(), (const void**)&M.dof_ancmask);
+  B.add(ancmask_hi.data(), 8 * ancmask_hi.size(), (const void**)&M.dof_ancmask_hi);
   B.ints(ancadr.data(), ancadr.size(), &M.dof_ancadr);
   B.reals(d->dof_armature, nv, &M.dof_armature); B.reals(d->dof_damping, nv, &M.dof_damping);
   B.reals(d->dof_invweight0, nv, &M.dof_invweight0);
@@ -654,7 +659,10 @@ const char* mgx_last_error(void) { return g_err.c_str(); }
 int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_model** out) {
   if (!d || !out) return fail(MGX_E_ARG, "null argument");
   if (precision != MGX_F32 && precision != MGX_F64) return fail(MGX_E_ARG, "precision must be MGX_F32 or MGX_F64");
-  if (d->nv > MGX_MAX_NV) return fail(MGX_E_CAPACITY, "nv > 64 not supported by the wave-per-env kernel");
+  // nv <= 64: one dof per lane (every task kernel); 64 < nv <= 128: the wide kernels only
+  // (mgx_wide.h, two dofs per lane: humanoid_construction, nv 99), which every other configure
+  // entry point refuses
+  if (d->nv > MGX_MAX_NV_WIDE) return fail(MGX_E_CAPACITY, "nv > 128 not supported by the wave-per-env kernels");
   if (d->nbody > 4096 || (d->solver != 0 && d->solver != 2) || (d->integrator != 0 && d->integrator != 1))
     return fail(MGX_E_UNSUPPORTED, "this build implements PGS or Newton with Euler or RK4");
   bool condim13 = true;  // the staged row builder packs one contact per 4-row block
@@ -667,6 +675,7 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   m->precision = precision;
   m->device = device;
   m->npair = d->npair;
+  m->wide = d->nv > MGX_MAX_NV;
   const char* env_nefc = getenv("MGX_MAX_NEFC");
   const char* env_ncon = getenv("MGX_MAX_NCON");
   // capacities: the model's request (efc_capacity / con_capacity), else 192 rows / 64 contacts
@@ -700,6 +709,10 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   if (m->L.bytes > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "per-env LDS exceeds 160 KiB"); }
   int r2 = step_kernels_configure(m);
   if (r2 != MGX_OK) { delete m; return r2; }
+  if (m->wide) {
+    r2 = wide_kernels_configure(m);
+    if (r2 != MGX_OK) { delete m; return r2; }
+  }
   r2 = precision == MGX_F32
                ? (set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes) |
                   set_lds(k_soccer_logic<float>, m->L.bytes) | set_lds(k_soccer_fixup<float>, m->L.bytes) | set_lds(k_soccer_template<float>, m->L.bytes) |
@@ -740,6 +753,7 @@ int mgx_model_get_info(const mgx_model* m, mgx_model_info* o) {
 
 int mgx_soccer_configure(mgx_model* m, const mgx_soccer_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");
+  if (m->wide) return fail(MGX_E_UNSUPPORTED, MGX_WIDE_MSG);
   if (m->L.gB || (m->precision == MGX_F32 ? m->mf.integrator : m->md.integrator) != 0)
     return fail(MGX_E_UNSUPPORTED, "the soccer kernels need an Euler model whose rows fit LDS");
   if ((m->precision == MGX_F32 ? m->mf.solver : m->md.solver) != 0)

@@ -143,6 +143,7 @@ extern "C" {
 
 int mgx_assembly_configure(mgx_model* m, const mgx_assembly_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");
+  if (m->wide) return fail(MGX_E_UNSUPPORTED, MGX_WIDE_MSG);
   const bool f32 = m->precision == MGX_F32;
   const int nq = f32 ? m->mf.nq : m->md.nq, nu = f32 ? m->mf.nu : m->md.nu;
   const int nb = f32 ? m->mf.nbody : m->md.nbody, ng = f32 ? m->mf.ngeom : m->md.ngeom;

@@ -4,9 +4,11 @@
 // mj_step, humanoid_soccer_env/soccer_env.py:414): geom types ordered type1 <= type2, contact
 // normal points from geom1 to geom2, `dist` is the signed surface distance (negative =
 // penetration), `pos` is the midpoint between the two surfaces, and a contact exists when
-// dist <= margin. Box-box uses separating axes + reference/incident face clipping (<= 8
-// contacts); capsule-box uses the endpoint spheres plus the deepest interior point. The CPU
-// oracle (oracle/mjref.c) restates the same algorithms in fp64.
+// dist <= margin. Sphere-capsule and capsule-capsule restate mjc_SphereCapsule /
+// mjc_CapsuleCapsule (centre + half-axis form, parallel axes up to two contacts); capsule-box
+// follows mjc_CapsuleBox's structure (closest / deepest axis point as a sphere-box contact, a
+// second one along a face, <= 2); box-box uses separating axes + reference/incident face clipping
+// (<= 8 contacts, own design). The CPU oracle (oracle/mjref.c) restates the same algorithms in fp64.
 #pragma once
 #include "mgx_common.h"
 
@@ -14,17 +16,6 @@ namespace mgx {
 
 template <typename T>
 struct Con { T dist, pos[3], n[3]; };
-
-template <typename T>
-__device__ __forceinline__ int sph_sph(const T* c1, T r1, const T* c2, T r2, T margin, Con<T>* out) {
-  T dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
-  T L = normalize3(dv);
-  T dist = L - r1 - r2;
-  if (dist > margin) return 0;
-  out->dist = dist;
-  for (int k = 0; k < 3; k++) { out->n[k] = dv[k]; out->pos[k] = c1[k] + dv[k] * (r1 + (T)0.5 * dist); }
-  return 1;
-}
 
 template <typename T>
 __device__ __forceinline__ void seg_ends(const T* pos, const T* mat, T hl, T* a, T* b) {
@@ -50,11 +41,15 @@ __device__ __forceinline__ void seg_seg(const T* p1, const T* q1, const T* p2, c
 
 template <typename T>
 __device__ __forceinline__ T box_sd(const T* p, const T* h, T* e) {
+  // a coordinate within `tie` outside its face plane counts as on it: points placed on a face's
+  // boundary by construction (capsule_box) classify the same under any rounding
+  const T tie = (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6) * (h[0] + h[1] + h[2]);
   bool outside = false;
   T dv[3];
   for (int k = 0; k < 3; k++) {
     T q = clampv(p[k], -h[k], h[k]);
     dv[k] = p[k] - q;
+    if (fabs(dv[k]) <= tie) dv[k] = 0;
     if (dv[k] != 0) outside = true;
   }
   if (outside) {
@@ -62,14 +57,17 @@ __device__ __forceinline__ T box_sd(const T* p, const T* h, T* e) {
     e[0] = dv[0]; e[1] = dv[1]; e[2] = dv[2];
     return L;
   }
+  // nearest face; faces within `tie` of the nearest count as equally near and the lowest axis
+  // wins, so two implementations with different rounding pick the same face at a kink (the
+  // deepest point of a capsule axis inside a box is where two face distances are equal)
   int best = 0;
   T bd = h[0] - fabs(p[0]);
   for (int k = 1; k < 3; k++) {
     T dk = h[k] - fabs(p[k]);
-    if (dk < bd) { bd = dk; best = k; }
+    if (dk < bd - tie) { bd = dk; best = k; }
   }
   e[0] = e[1] = e[2] = 0;
-  e[best] = p[best] >= 0 ? (T)1 : (T)-1;
+  e[best] = p[best] >= -tie ? (T)1 : (T)-1;  // on the mid-plane (within tie) the + face
   return -bd;
 }
 
@@ -86,47 +84,204 @@ __device__ __forceinline__ int sphere_box_core(const T* c, T r, const T* bp, con
   return 1;
 }
 
+// Point of a capsule axis closest to (outside) or deepest in (inside) a box, in the box frame:
+// the axis is c + s a, s in [-1, 1]. The signed distance d(s) of the point to the box is convex
+// and piecewise smooth, so its minimum over [-1, 1] lies at an end, a kink or a stationary point
+// of a piece: the 2 ends, where a coordinate crosses a face plane (6) or zero (3), where two
+// inside face distances are equal (12), and the stationary point of every outside piece (26
+// sign patterns). All 49 candidates are evaluated exactly (generated on the fly, twice: no
+// per-lane arrays); the lowest s within tol of the minimum wins, so an axis lying flat on a face
+// starts at the end of its overlap with the face. The result depends only on the candidate set.
+template <typename T>
+__device__ __forceinline__ bool capsule_box_cand(int k, const T* c, const T* a, const T* h, T& s) {
+  if (k < 2) { s = k ? (T)1 : (T)-1; return true; }
+  if (k < 11) {
+    const int i = (k - 2) / 3, r = (k - 2) % 3;
+    if (!(fabs(a[i]) > minval<T>())) return false;
+    s = (r == 0 ? h[i] - c[i] : r == 1 ? -h[i] - c[i] : -c[i]) / a[i];
+    return true;
+  }
+  if (k < 23) {
+    const int q = (k - 11) >> 2, sg = (k - 11) & 3;
+    const int i = q == 2 ? 1 : 0, j = q == 0 ? 1 : 2;
+    const T si = (sg & 1) ? (T)-1 : (T)1, sj = (sg & 2) ? (T)-1 : (T)1;
+    const T den = sj * a[j] - si * a[i];
+    if (!(fabs(den) > minval<T>())) return false;
+    s = (h[j] - h[i] - sj * c[j] + si * c[i]) / den;
+    return true;
+  }
+  int q = k - 22;  // sign pattern 1..26: per axis 0 inside, 1 above +h, 2 below -h
+  T num = 0, den = 0;
+  for (int i = 0; i < 3; i++, q /= 3) {
+    const int st = q % 3;
+    if (st == 0) continue;
+    const T sg = st == 1 ? (T)1 : (T)-1;
+    num += a[i] * (sg * h[i] - c[i]);
+    den += a[i] * a[i];
+  }
+  if (!(den > minval<T>())) return false;
+  s = num / den;
+  return true;
+}
+
+template <typename T>
+__device__ __forceinline__ T capsule_box_segpos(const T* c, const T* a, const T* h) {
+  T e[3], p[3], s;
+  const T hm = h[0] > h[1] ? (h[0] > h[2] ? h[0] : h[2]) : (h[1] > h[2] ? h[1] : h[2]);
+  const T tol = (sizeof(T) == 8 ? (T)1e-10 : (T)1e-5) * ((T)1 + hm);
+  // pass 1 also keeps a lower bound `other` on d over candidates at an s other than the argmin's:
+  // when nothing else is within tol, the argmin is the answer and pass 2 is skipped
+  T best = (T)1e30, sb = (T)2, other = (T)1e30;
+  for (int k = 0; k < 49; k++) {
+    if (!capsule_box_cand(k, c, a, h, s)) continue;
+    s = clampv(s, (T)-1, (T)1);
+    for (int i = 0; i < 3; i++) p[i] = c[i] + s * a[i];
+    const T d = box_sd(p, h, e);
+    if (d < best) {
+      if (s != sb) other = best < other ? best : other;
+      best = d;
+      sb = s;
+    } else if (s != sb) {
+      other = d < other ? d : other;
+    }
+  }
+  if (other > best + tol) return sb;
+  T bs = (T)2;
+  for (int k = 0; k < 49; k++) {
+    if (!capsule_box_cand(k, c, a, h, s)) continue;
+    s = clampv(s, (T)-1, (T)1);
+    for (int i = 0; i < 3; i++) p[i] = c[i] + s * a[i];
+    const T d = box_sd(p, h, e);
+    if (d <= best + tol && s < bs) bs = s;
+  }
+  return bs;
+}
+
+// sphere of radius r at box-frame point pl (world point w) vs the box; e = outward face /
+// feature normal in the box frame
+template <typename T>
+__device__ __forceinline__ int sphere_box_local(const T* pl, const T* w, T r, const T* bm, const T* h, T margin, T* e,
+                                                Con<T>* out) {
+  const T sd = box_sd(pl, h, e);
+  const T dist = sd - r;
+  if (dist > margin) return 0;
+  T ew[3];
+  mulmatvec3(ew, bm, e);
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = -ew[k]; out->pos[k] = w[k] - ew[k] * (r + (T)0.5 * dist); }
+  return 1;
+}
+
+// capsule (geom1) vs box (geom2), at most 2 contacts, structured as mjc_CapsuleBox [ext]: the axis
+// point closest to / deepest in the box as a sphere-box contact; when that contact is on a box
+// face, a second sphere-box contact at the far end of the axis's overlap with the face rectangle
+// if that point is also within margin of the same face (a capsule lying along the face). The
+// second point is dropped when it is within a tenth of the radius of the first.
 template <typename T>
 __device__ __forceinline__ int capsule_box(const T* cp, const T* cm, const T* cs, const T* bp, const T* bm, const T* h, T margin,
                            Con<T>* out) {
-  T a[3], b[3], al[3], bl[3], tmp[3], e[3], p[3];
-  T r = cs[0];
-  seg_ends(cp, cm, cs[1], a, b);
-  for (int k = 0; k < 3; k++) tmp[k] = a[k] - bp[k];
-  mulmatTvec3(al, bm, tmp);
-  for (int k = 0; k < 3; k++) tmp[k] = b[k] - bp[k];
-  mulmatTvec3(bl, bm, tmp);
-  T lo = 0, hi = 1;
-  const T gr = (T)0.6180339887498949;
-  T x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), f1, f2;
-  for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
-  f1 = box_sd(p, h, e);
-  for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
-  f2 = box_sd(p, h, e);
-  for (int it = 0; it < 40; it++) {
-    if (f1 <= f2) {
-      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-      for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
-      f1 = box_sd(p, h, e);
-    } else {
-      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-      for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
-      f2 = box_sd(p, h, e);
+  const T r = cs[0], hl = cs[1];
+  T tmp[3] = {cp[0] - bp[0], cp[1] - bp[1], cp[2] - bp[2]}, c[3], a[3];
+  const T ax[3] = {cm[2] * hl, cm[5] * hl, cm[8] * hl};
+  mulmatTvec3(c, bm, tmp);
+  mulmatTvec3(a, bm, ax);
+  const T s1 = capsule_box_segpos(c, a, h);
+  T pl[3], w[3], e[3];
+  for (int k = 0; k < 3; k++) { pl[k] = c[k] + s1 * a[k]; w[k] = cp[k] + s1 * ax[k]; }
+  if (!sphere_box_local(pl, w, r, bm, h, margin, e, out)) return 0;
+  int fk = -1, nz = 0;
+  for (int k = 0; k < 3; k++)
+    if (e[k] != 0) { nz++; fk = k; }
+  if (nz != 1) return 1;  // edge or corner contact
+  T lo = -1, hi = 1;
+  for (int i = 0; i < 3; i++) {
+    if (i == fk) continue;
+    if (fabs(a[i]) > minval<T>()) {
+      T t0 = (-h[i] - c[i]) / a[i], t1 = (h[i] - c[i]) / a[i];
+      if (t0 > t1) { T t = t0; t0 = t1; t1 = t; }
+      lo = t0 > lo ? t0 : lo;
+      hi = t1 < hi ? t1 : hi;
+    } else if (fabs(c[i]) > h[i]) {
+      return 1;
     }
   }
-  T ts = (T)0.5 * (lo + hi);
-  for (int k = 0; k < 3; k++) p[k] = al[k] + ts * (bl[k] - al[k]);
-  T fs = box_sd(p, h, e);
-  T f0 = box_sd(al, h, e), f1e = box_sd(bl, h, e);
+  if (lo > hi) return 1;
+  const T s2 = (s1 - lo < hi - s1) ? hi : lo;
+  if (fabs(s2 - s1) * hl < (T)0.1 * r) return 1;
+  T e2[3];
+  for (int k = 0; k < 3; k++) { pl[k] = c[k] + s2 * a[k]; w[k] = cp[k] + s2 * ax[k]; }
+  if (!sphere_box_local(pl, w, r, bm, h, margin, e2, out + 1)) return 1;
+  // the far point must lie on the same face: one nonzero normal component, same axis and sign
+  if ((e2[0] != 0) + (e2[1] != 0) + (e2[2] != 0) != 1 || !(e2[fk] * e[fk] > 0)) return 1;
+  return 2;
+}
+
+// mjraw_SphereSphere [ext]: normal from 1 to 2; coincident centres take the cross product of the
+// two geoms' z axes (then [1, 0, 0] when they are parallel)
+template <typename T>
+__device__ __forceinline__ int sph_sph_raw(const T* c1, const T* m1, T r1, const T* c2, const T* m2, T r2, T margin,
+                                           Con<T>* out) {
+  T dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  const T dist = sqrt(dot3(dv, dv)) - r1 - r2;
+  if (dist > margin) return 0;
+  const T L = normalize3(dv);
+  if (L < minval<T>()) {
+    const T z1[3] = {m1[2], m1[5], m1[8]}, z2[3] = {m2[2], m2[5], m2[8]};
+    cross3(dv, z1, z2);
+    normalize3(dv);
+  }
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = dv[k]; out->pos[k] = c1[k] + dv[k] * (r1 + (T)0.5 * dist); }
+  return 1;
+}
+
+// mjc_CapsuleCapsule [ext]: closest points of the two axes in MuJoCo's centre + half-axis form
+// (x1, x2 in [-1, 1], the same clamping sequence); for parallel axes (|det| < mjMINVAL) up to two
+// sphere-sphere contacts from the axis ends (x1 = +-1, then x2 = +-1), stopping at two
+template <typename T>
+__device__ __forceinline__ int capsule_capsule(const T* p1, const T* m1, const T* s1, const T* p2, const T* m2, const T* s2,
+                                               T margin, Con<T>* out) {
+  const T a1[3] = {m1[2] * s1[1], m1[5] * s1[1], m1[8] * s1[1]};
+  const T a2[3] = {m2[2] * s2[1], m2[5] * s2[1], m2[8] * s2[1]};
+  const T dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  const T ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+  const T u = -dot3(a1, dif), v = dot3(a2, dif);
+  const T det = ma * mc - mb * mb;
+  T v1[3], v2[3];
+  if (fabs(det) >= minval<T>()) {
+    T x1 = (mc * u - mb * v) / det, x2 = (ma * v - mb * u) / det;
+    if (x1 > 1) { x1 = 1; x2 = (v - mb) / mc; }
+    else if (x1 < -1) { x1 = -1; x2 = (v + mb) / mc; }
+    if (x2 > 1) { x2 = 1; x1 = clampv((u - mb) / ma, (T)-1, (T)1); }
+    else if (x2 < -1) { x2 = -1; x1 = clampv((u + mb) / ma, (T)-1, (T)1); }
+    for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+    return sph_sph_raw(v1, m1, s1[0], v2, m2, s2[0], margin, out);
+  }
   int n = 0;
-  if (f0 - r <= margin) n += sphere_box_core(a, r, bp, bm, h, margin, out + n);
-  if (f1e - r <= margin) n += sphere_box_core(b, r, bp, bm, h, margin, out + n);
-  if (ts > (T)0.02 && ts < (T)0.98 && fs - r <= margin && fs < (f0 < f1e ? f0 : f1e) - (T)0.01 * r) {
-    T cw[3];
-    for (int k = 0; k < 3; k++) cw[k] = a[k] + ts * (b[k] - a[k]);
-    n += sphere_box_core(cw, r, bp, bm, h, margin, out + n);
+  for (int e = 0; e < 4 && n < 2; e++) {
+    const T sg = (e & 1) ? (T)-1 : (T)1;
+    if (e < 2) {  // x1 = +-1
+      const T x2 = clampv((v - sg * mb) / mc, (T)-1, (T)1);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + sg * a1[k]; v2[k] = p2[k] + a2[k] * x2; }
+    } else {      // x2 = +-1
+      const T x1 = clampv((u - sg * mb) / ma, (T)-1, (T)1);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + sg * a2[k]; }
+    }
+    n += sph_sph_raw(v1, m1, s1[0], v2, m2, s2[0], margin, out + n);
   }
   return n;
+}
+
+// mjc_SphereCapsule [ext]: the sphere centre projected on the capsule axis, clamped to the
+// half-length
+template <typename T>
+__device__ __forceinline__ int sphere_capsule(const T* p1, const T* m1, const T* s1, const T* p2, const T* m2, const T* s2,
+                                              T margin, Con<T>* out) {
+  const T ax[3] = {m2[2], m2[5], m2[8]};
+  const T dv[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  const T x = clampv(dot3(ax, dv), -s2[1], s2[1]);
+  const T q[3] = {p2[0] + ax[0] * x, p2[1] + ax[1] * x, p2[2] + ax[2] * x};
+  return sph_sph_raw(p1, m1, s1[0], q, m2, s2[0], margin, out);
 }
 
 // ---- cylinders (bipedal_rescue: sphere / capsule / box vs static cylinders) [ext]. MuJoCo
@@ -458,23 +613,9 @@ __device__ __forceinline__ int cyl_cyl(const T* ap, const T* am, const T* as, co
 template <typename T>
 __device__ __forceinline__ int collide_pair(int t1, int t2, const T* p1, const T* m1, const T* s1, const T* p2, const T* m2,
                             const T* s2, T margin, Con<T>* out) {
-  if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph(p1, s1[0], p2, s2[0], margin, out);
-  if (t1 == GSPHERE && t2 == GCAPSULE) {
-    T a[3], b[3], q[3];
-    seg_ends(p2, m2, s2[1], a, b);
-    T ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p1[0] - a[0], p1[1] - a[1], p1[2] - a[2]};
-    T L2 = dot3(ab, ab), t = L2 > minval<T>() ? clampv(dot3(ap, ab) / L2, (T)0, (T)1) : (T)0;
-    for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k];
-    return sph_sph(p1, s1[0], q, s2[0], margin, out);
-  }
-  if (t1 == GCAPSULE && t2 == GCAPSULE) {
-    T a1[3], b1[3], a2[3], b2[3], s, t, P[3], Q[3];
-    seg_ends(p1, m1, s1[1], a1, b1);
-    seg_ends(p2, m2, s2[1], a2, b2);
-    seg_seg(a1, b1, a2, b2, &s, &t);
-    for (int k = 0; k < 3; k++) { P[k] = a1[k] + s * (b1[k] - a1[k]); Q[k] = a2[k] + t * (b2[k] - a2[k]); }
-    return sph_sph(P, s1[0], Q, s2[0], margin, out);
-  }
+  if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph_raw(p1, m1, s1[0], p2, m2, s2[0], margin, out);
+  if (t1 == GSPHERE && t2 == GCAPSULE) return sphere_capsule(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GCAPSULE && t2 == GCAPSULE) return capsule_capsule(p1, m1, s1, p2, m2, s2, margin, out);
   if (t1 == GSPHERE && t2 == GBOX) return sphere_box_core(p1, s1[0], p2, m2, s2, margin, out);
   if (t1 == GCAPSULE && t2 == GBOX) return capsule_box(p1, m1, s1, p2, m2, s2, margin, out);
   if (t1 == GBOX && t2 == GBOX) return box_box(p1, m1, s1, p2, m2, s2, margin, out);

@@ -11,6 +11,7 @@
 
 #define MGX_WAVE 64
 #define MGX_MAX_NV 64
+#define MGX_MAX_NV_WIDE 128   // wide kernels (mgx_wide.h): two dofs per lane, dof d on lane d % 64
 #define MGX_MAX_NBODY 64
 #define MGX_MAX_DEPTH 16      // longest dof chain (root..dof), soccer: 13
 #define MGX_MAX_CONPAIR 8     // contacts per geom pair (box-box)
@@ -66,6 +67,7 @@ struct DevModel {
   // dofs
   const int *dof_bodyid, *dof_jntid, *dof_parentid, *dof_Madr, *dof_chainlen, *dof_anc;  // anc: [nv][MAX_DEPTH]
   const uint64_t *dof_ancmask;  // bit i set if dof i is a strict ancestor of the dof
+  const uint64_t *dof_ancmask_hi;  // the same for ancestors i = 64 .. 127 (bit i - 64; wide models)
   const int *dof_ancadr;        // [nv][MAX_DEPTH]: dof_Madr of ancestor t (0 past the chain)
   const T *dof_armature, *dof_damping, *dof_invweight0;
   // geoms

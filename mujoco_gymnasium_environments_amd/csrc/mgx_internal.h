@@ -8,6 +8,7 @@
 
 #include "../../include/mgx.h"
 #include "mgx_bipedal.h"
+#include "mgx_construction.h"
 #include "mgx_dancing.h"
 #include "mgx_martial.h"
 #include "mgx_parkour.h"
@@ -35,11 +36,40 @@ struct mgx_model {
   mgx::DancingIds dn;
   bool assembly_ok = false;
   mgx_assembly_ids as;
+  bool construction_ok = false;
+  mgx::ConstructionIds cn;
   int npair;
+  bool wide = false;       // nv > 64: only the wide kernels (mgx_wide.h) run this model
   bool staged_ok = false;  // the staged soccer pipeline supports this model's capacities
 };
 
 namespace mgx {
+// Debug dump of one forward pass (stage outputs): offsets into one env's record
+// (mgx_debug_forward / mgx_debug_layout; the wide kernels write the same layout)
+struct DbgOff {
+  int xpos, xquat, xipos, subtree_com, cinert, cdof, qM, qLD, geom_xpos, geom_xmat, ncon, con_dist, con_pos,
+      con_frame, con_geom, nefc, efc_type, efc_id, efc_pos, efc_margin, efc_R, efc_aref, Bmat, cvel, cdof_dot,
+      qfrc_smooth, qacc_smooth, efc_force, qacc, qfrc_constraint, niter, total;
+};
+inline DbgOff dbg_offsets(int nb, int nv, int nM, int ng, int C, int E) {
+  DbgOff o;
+  int p = 0;
+  auto take = [&](int n) { int r = p; p += n; return r; };
+  o.xpos = take(3 * nb); o.xquat = take(4 * nb); o.xipos = take(3 * nb); o.subtree_com = take(3 * nb);
+  o.cinert = take(10 * nb); o.cdof = take(6 * nv); o.qM = take(nM); o.qLD = take(nM);
+  o.geom_xpos = take(3 * ng); o.geom_xmat = take(9 * ng); o.ncon = take(1); o.con_dist = take(C);
+  o.con_pos = take(3 * C); o.con_frame = take(9 * C); o.con_geom = take(2 * C); o.nefc = take(1);
+  o.efc_type = take(E); o.efc_id = take(E); o.efc_pos = take(E); o.efc_margin = take(E); o.efc_R = take(E);
+  o.efc_aref = take(E); o.Bmat = take(E * nv); o.cvel = take(6 * nb); o.cdof_dot = take(6 * nv);
+  o.qfrc_smooth = take(nv); o.qacc_smooth = take(nv); o.efc_force = take(E); o.qacc = take(nv);
+  o.qfrc_constraint = take(nv); o.niter = take(1); o.total = p;
+  return o;
+}
+// the wide (nv > 64) physics kernels (mgx_construction.hip)
+int wide_step(const mgx_model* m, const mgx_state* s, const mgx_frames& fr, int n_env, int nsub, const uint8_t* mask,
+              hipStream_t st);
+int wide_debug(const mgx_model* m, const mgx_state* s, int n_env, void* dbg, const DbgOff& o, hipStream_t st);
+int wide_kernels_configure(const mgx_model* m);
 // records the message returned by mgx_last_error() and returns `code`
 int host_fail(int code, const std::string& msg);
 int host_check_state(const mgx_state* s);
@@ -50,6 +80,8 @@ template <typename T>
 void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale);
 int pgs_configure_lds(int precision, int bytes);
 }  // namespace mgx
+
+#define MGX_WIDE_MSG "nv > 64: this model runs on the wide (two dofs per lane) kernels only"
 
 #define MGX_HIPCHK(x)                                                                                   \
   do {                                                                                                  \

@@ -128,6 +128,7 @@ extern "C" {
 
 int mgx_martial_configure(mgx_model* m, const mgx_martial_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");
+  if (m->wide) return fail(MGX_E_UNSUPPORTED, MGX_WIDE_MSG);
   const bool f32 = m->precision == MGX_F32;
   const int nq = f32 ? m->mf.nq : m->md.nq, nv = f32 ? m->mf.nv : m->md.nv, nu = f32 ? m->mf.nu : m->md.nu;
   const int nb = f32 ? m->mf.nbody : m->md.nbody;

@@ -146,6 +146,7 @@ extern "C" {
 
 int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
   if (!m || !ids) return fail(MGX_E_ARG, "null argument");
+  if (m->wide) return fail(MGX_E_UNSUPPORTED, MGX_WIDE_MSG);
   int nq = m->precision == MGX_F32 ? m->mf.nq : m->md.nq;
   int nu = m->precision == MGX_F32 ? m->mf.nu : m->md.nu;
   int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;

@@ -238,13 +238,13 @@ __device__ __forceinline__ void com_crb(const DevModel<T>& m, Env<T>& e) {
     for (int k = 0; k < 3; k++) off[k] = e.xipos[3 * b + k] - e.subtree_com[3 * r + k];
     inertcom(e.cinert + 10 * b, m.body_inertia + 3 * b, e.ximat + 9 * b, off, m.body_mass[b]);
   }
-  // cdof: lane = dof
-  if (l < m.nv) {
-    int b = m.dof_bodyid[l], j = m.dof_jntid[l], t = m.jnt_type[j], k = l - m.jnt_dofadr[j];
+  // cdof: lane = dof (dofs l, l + 64, ... when nv > 64)
+  for (int d = l; d < m.nv; d += 64) {
+    int b = m.dof_bodyid[d], j = m.dof_jntid[d], t = m.jnt_type[j], k = d - m.jnt_dofadr[j];
     T off[3];
     int r = m.body_rootid[b];
     for (int c = 0; c < 3; c++) off[c] = e.subtree_com[3 * r + c] - e.xanchor[3 * j + c];
-    T* cd = e.cdof + 6 * l;
+    T* cd = e.cdof + 6 * d;
     if (t == JFREE && k < 3) {
       for (int c = 0; c < 6; c++) cd[c] = 0;
       cd[3 + k] = 1;
@@ -275,16 +275,16 @@ __device__ __forceinline__ void com_crb(const DevModel<T>& m, Env<T>& e) {
   }
   wsync();
   // qM rows (tree-sparse, dof_Madr layout) and qMH = qM + h*diag(damping)
-  if (l < m.nv) {
+  for (int d = l; d < m.nv; d += 64) {
     T buf[6];
-    mulinertvec(buf, e.crb + 10 * m.dof_bodyid[l], e.cdof + 6 * l);
-    int adr = m.dof_Madr[l];
-    int j = l;
+    mulinertvec(buf, e.crb + 10 * m.dof_bodyid[d], e.cdof + 6 * d);
+    int adr = m.dof_Madr[d];
+    int j = d;
     for (int t = 0; j >= 0; t++, j = m.dof_parentid[j]) {
       T v = dot6(e.cdof + 6 * j, buf);
-      if (t == 0) v += m.dof_armature[l];
+      if (t == 0) v += m.dof_armature[d];
       e.qLD[adr + t] = v;
-      e.qMH[adr + t] = t == 0 ? v + m.timestep * m.dof_damping[l] : v;
+      e.qMH[adr + t] = t == 0 ? v + m.timestep * m.dof_damping[d] : v;
     }
   }
   wsync();
@@ -294,14 +294,16 @@ __device__ __forceinline__ void com_crb(const DevModel<T>& m, Env<T>& e) {
 // Step k updates the (t, s) pairs of its ancestor block in parallel: lane -> t = (l & 15) + 1,
 // s = s0 + (l >> 4), 4 values of s per pass; the ancestors' Madr come from the host table
 // dof_ancadr, prefetched one step ahead.
-template <typename T>
+// WIDE (nv > 64, mgx_wide.h): the pivot's Madr / chain length come from the model tables instead
+// of the dof-lane registers (which only cover dofs 0..63); the returned diaginv is then unused.
+template <typename T, bool WIDE = false>
 __device__ __forceinline__ T factor_ld(const DevModel<T>& m, const Env<T>& e, T* LD) {
   int l = lane_id();
   const int t = (l & 15) + 1, sl = l >> 4;
   int ai_next = m.nv > 0 ? m.dof_ancadr[(m.nv - 1) * MGX_MAX_DEPTH + (t & 15)] : 0;
   for (int k = m.nv - 1; k >= 0; k--) {
-    int akk = readlane(e.madr, k);
-    int mk = readlane(e.chainlen, k) - 1;  // number of ancestors
+    int akk = WIDE ? m.dof_Madr[k] : readlane(e.madr, k);
+    int mk = (WIDE ? m.dof_chainlen[k] : readlane(e.chainlen, k)) - 1;  // number of ancestors
     int ai = ai_next;
     if (k > 0) ai_next = m.dof_ancadr[(k - 1) * MGX_MAX_DEPTH + (t & 15)];
     T dkk = LD[akk];
@@ -337,12 +339,12 @@ __device__ __forceinline__ T usum(T x) { return readlane(wave_sum(x), 0); }
 // B_r = D^-1/2 L'^-1 J_r' for one row x (LDS, lane-private): for k = nv-1 .. 0 the ancestors
 // of k get x[anc] -= L[k][anc] x[k]. The ancestors of one k are distinct, so all their loads
 // are issued before any store (one LDS latency per k instead of one per ancestor).
-template <typename T>
+template <typename T, bool WIDE = false>
 __device__ __forceinline__ void transform_row(const DevModel<T>& m, const Env<T>& e, T* x, const T* dinv_sqrt) {
   for (int k = m.nv - 1; k >= 0; k--) {
     const int* ak = m.dof_anc + k * MGX_MAX_DEPTH;
-    int mk = readlane(e.chainlen, k) - 1;
-    int a = readlane(e.madr, k) + 1;
+    int mk = (WIDE ? m.dof_chainlen[k] : readlane(e.chainlen, k)) - 1;
+    int a = (WIDE ? m.dof_Madr[k] : readlane(e.madr, k)) + 1;
     T xk = x[k];
     T xa[MGX_MAX_DEPTH], la[MGX_MAX_DEPTH];
 #pragma unroll
@@ -565,16 +567,16 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
     int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
     const T* fr = e.con_frame + 9 * c;
     const T* pos = e.con_pos + 3 * c;
-    if (l < m.nv) {
+    for (int d = l; d < m.nv; d += 64) {  // lane = dof (l, l + 64 when nv > 64)
       T j1[3] = {0, 0, 0}, j2[3] = {0, 0, 0};
-      const T* cd = e.cdof + 6 * l;
-      if (b2 > 0 && body_has_dof(m, b2, l)) {
+      const T* cd = e.cdof + 6 * d;
+      if (b2 > 0 && body_has_dof(m, b2, d)) {
         int r2 = m.body_rootid[b2];
         T off[3] = {pos[0] - e.subtree_com[3 * r2], pos[1] - e.subtree_com[3 * r2 + 1], pos[2] - e.subtree_com[3 * r2 + 2]}, t[3];
         cross3(t, cd, off);
         j2[0] = cd[3] + t[0]; j2[1] = cd[4] + t[1]; j2[2] = cd[5] + t[2];
       }
-      if (b1 > 0 && body_has_dof(m, b1, l)) {
+      if (b1 > 0 && body_has_dof(m, b1, d)) {
         int r1 = m.body_rootid[b1];
         T off[3] = {pos[0] - e.subtree_com[3 * r1], pos[1] - e.subtree_com[3 * r1 + 1], pos[2] - e.subtree_com[3 * r1 + 2]}, t[3];
         cross3(t, cd, off);
@@ -583,7 +585,7 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
       T jd[3] = {j2[0] - j1[0], j2[1] - j1[1], j2[2] - j1[2]};
       T cj0 = fr[0] * jd[0] + fr[1] * jd[1] + fr[2] * jd[2];
       if (dim == 1) {
-        e.Bm[nefc * e.Bs + l] = cj0;
+        e.Bm[nefc * e.Bs + d] = cj0;
       } else {
         T cj[6];
         cj[1] = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
@@ -591,16 +593,16 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
         if (dim > 3) {
           // relative angular motion: the rotational parts of the dof's motion subspace
           T jr[3] = {0, 0, 0};
-          if (b2 > 0 && body_has_dof(m, b2, l)) { jr[0] += cd[0]; jr[1] += cd[1]; jr[2] += cd[2]; }
-          if (b1 > 0 && body_has_dof(m, b1, l)) { jr[0] -= cd[0]; jr[1] -= cd[1]; jr[2] -= cd[2]; }
+          if (b2 > 0 && body_has_dof(m, b2, d)) { jr[0] += cd[0]; jr[1] += cd[1]; jr[2] += cd[2]; }
+          if (b1 > 0 && body_has_dof(m, b1, d)) { jr[0] -= cd[0]; jr[1] -= cd[1]; jr[2] -= cd[2]; }
           cj[3] = fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2];
           cj[4] = fr[3] * jr[0] + fr[4] * jr[1] + fr[5] * jr[2];
           cj[5] = fr[6] * jr[0] + fr[7] * jr[1] + fr[8] * jr[2];
         }
         for (int k = 1; k < dim; k++) {
           T mu = m.pair_friction[5 * p + k - 1];
-          e.Bm[(nefc + 2 * (k - 1)) * e.Bs + l] = cj0 + mu * cj[k];
-          e.Bm[(nefc + 2 * (k - 1) + 1) * e.Bs + l] = cj0 - mu * cj[k];
+          e.Bm[(nefc + 2 * (k - 1)) * e.Bs + d] = cj0 + mu * cj[k];
+          e.Bm[(nefc + 2 * (k - 1) + 1) * e.Bs + d] = cj0 - mu * cj[k];
         }
       }
     }
@@ -654,7 +656,7 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
 // (Layout.gB) are staged through LDS in chunks of L.tchunk rows (the phase-A union is dead once
 // the rows exist): coalesced row copies in and out (lane = dof), the lane-per-row transform on
 // LDS, instead of lane-strided global read-modify-writes along every row.
-template <typename T>
+template <typename T, bool WIDE = false>
 __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
@@ -665,29 +667,71 @@ __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) 
     for (int r0 = 0; r0 < ne; r0 += C) {
       const int nr = ne - r0 < C ? ne - r0 : C;
       T* G = e.Bm + (size_t)r0 * Bs;
-      for (int q0 = 0; q0 < nr; q0 += MGX_RB) {
-        T xb[MGX_RB];
-        load_rows(xb, G, Bs, q0, nr, l < nv ? l : 0, l < nv);
+      for (int d0 = 0; d0 < (WIDE ? nv : 1); d0 += 64) {
+        const int d = d0 + l;
+        for (int q0 = 0; q0 < nr; q0 += MGX_RB) {
+          T xb[MGX_RB];
+          load_rows(xb, G, Bs, q0, nr, d < nv ? d : 0, d < nv);
 #pragma unroll
-        for (int j = 0; j < MGX_RB; j++)
-          if (q0 + j < nr && l < nv) S[(q0 + j) * Bs + l] = xb[j];
+          for (int j = 0; j < MGX_RB; j++)
+            if (q0 + j < nr && d < nv) S[(q0 + j) * Bs + d] = xb[j];
+        }
       }
       wsync();
-      if (l < nr) transform_row(m, e, S + l * Bs, e.vec0);
+      if (l < nr) transform_row<T, WIDE>(m, e, S + l * Bs, e.vec0);
       wsync();
-      if (l < nv)
-        for (int r = 0; r < nr; r++) G[r * Bs + l] = S[r * Bs + l];
+      for (int d = l; d < nv; d += 64)
+        for (int r = 0; r < nr; r++) G[r * Bs + d] = S[r * Bs + d];
       wsync();
     }
     return;
   }
-  for (int r = l; r < ne; r += 64) transform_row(m, e, e.Bm + r * e.Bs, e.vec0);
+  for (int r = l; r < ne; r += 64) transform_row<T, WIDE>(m, e, e.Bm + r * e.Bs, e.vec0);
   wsync();
 }
 
-// ---------------------------------------------------------------- velocity stage
+// qfrc_smooth of dof d before the register store: passive (damping, springs) - bias (RNE,
+// subtree sums in crb storage) + applied + actuation + J(xipos)' xfrc_applied; qfrc_applied comes
+// from the dof's register (applied, passed by the caller)
 template <typename T>
-__device__ __forceinline__ void velocity(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ T dof_force_applied(const DevModel<T>& m, const Env<T>& e, int d, T applied) {
+  int b = m.dof_bodyid[d];
+  T bias = dot6(e.cdof + 6 * d, e.crb + 10 * b);
+  T passive = -m.dof_damping[d] * e.qvel[d];
+  int j = m.dof_jntid[d];
+  T st = m.jnt_stiffness[j];
+  if (st != 0) {
+    int t = m.jnt_type[j], a = m.jnt_qposadr[j], k = d - m.jnt_dofadr[j];
+    if (t == JHINGE || t == JSLIDE) passive -= st * (e.qpos[a] - m.qpos_spring[a]);
+    else if (t == JFREE && k < 3) passive -= st * (e.qpos[a + k] - m.qpos_spring[a + k]);
+  }
+  T act = 0;
+  for (int u = 0; u < m.nu; u++)
+    if (m.jnt_dofadr[m.actuator_trnid[u]] == d) act += m.actuator_gear[u] * e.act_force[u];
+  // xfrc_applied: J(xipos)' f for every body with a nonzero wrench whose chain holds this dof
+  T xf = 0;
+  for (int i = 1; i < m.nbody; i++) {
+    const T* f = e.xfrc + 6 * i;
+    if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
+    if (!body_has_dof(m, i, d)) continue;
+    int r = m.body_rootid[i];
+    const T* cd = e.cdof + 6 * d;
+    T off[3] = {e.xipos[3 * i] - e.subtree_com[3 * r], e.xipos[3 * i + 1] - e.subtree_com[3 * r + 1],
+                e.xipos[3 * i + 2] - e.subtree_com[3 * r + 2]}, t[3];
+    cross3(t, cd, off);
+    xf += (cd[3] + t[0]) * f[0] + (cd[4] + t[1]) * f[1] + (cd[5] + t[2]) * f[2] + cd[0] * f[3] + cd[1] * f[4] + cd[2] * f[5];
+  }
+  return passive - bias + applied + act + xf;
+}
+template <typename T>
+__device__ __forceinline__ T dof_force(const DevModel<T>& m, const Env<T>& e, int d) {
+  return dof_force_applied(m, e, d, e.qfrc_applied);
+}
+
+// ---------------------------------------------------------------- velocity stage
+// comVel, actuator forces, RNE and its subtree sums (everything but the per-dof forces)
+template <typename T>
+__device__ __forceinline__ void velocity_bodies(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   // comVel: lane b walks its chain; cdof_dot for the body's own dofs
   for (int b = l; b < m.nbody; b += 64) {
@@ -764,38 +808,14 @@ __device__ __forceinline__ void velocity(const DevModel<T>& m, Env<T>& e) {
     for (int k = 0; k < 6; k++) e.crb[10 * b + k] = acc[k];  // crb no longer needed
   }
   wsync();
+}
+
+template <typename T>
+__device__ __forceinline__ void velocity(const DevModel<T>& m, Env<T>& e) {
+  velocity_bodies(m, e);
   // per-dof forces
-  if (l < m.nv) {
-    int b = m.dof_bodyid[l];
-    T bias = dot6(e.cdof + 6 * l, e.crb + 10 * b);
-    T passive = -m.dof_damping[l] * e.qvel[l];
-    int j = m.dof_jntid[l];
-    T st = m.jnt_stiffness[j];
-    if (st != 0) {
-      int t = m.jnt_type[j], a = m.jnt_qposadr[j], k = l - m.jnt_dofadr[j];
-      if (t == JHINGE || t == JSLIDE) passive -= st * (e.qpos[a] - m.qpos_spring[a]);
-      else if (t == JFREE && k < 3) passive -= st * (e.qpos[a + k] - m.qpos_spring[a + k]);
-    }
-    T act = 0;
-    for (int u = 0; u < m.nu; u++)
-      if (m.jnt_dofadr[m.actuator_trnid[u]] == l) act += m.actuator_gear[u] * e.act_force[u];
-    // xfrc_applied: J(xipos)' f for every body with a nonzero wrench whose chain holds this dof
-    T xf = 0;
-    for (int i = 1; i < m.nbody; i++) {
-      const T* f = e.xfrc + 6 * i;
-      if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
-      if (!body_has_dof(m, i, l)) continue;
-      int r = m.body_rootid[i];
-      const T* cd = e.cdof + 6 * l;
-      T off[3] = {e.xipos[3 * i] - e.subtree_com[3 * r], e.xipos[3 * i + 1] - e.subtree_com[3 * r + 1],
-                  e.xipos[3 * i + 2] - e.subtree_com[3 * r + 2]}, t[3];
-      cross3(t, cd, off);
-      xf += (cd[3] + t[0]) * f[0] + (cd[4] + t[1]) * f[1] + (cd[5] + t[2]) * f[2] + cd[0] * f[3] + cd[1] * f[4] + cd[2] * f[5];
-    }
-    e.qfrc_smooth = passive - bias + e.qfrc_applied + act + xf;
-  } else {
-    e.qfrc_smooth = 0;
-  }
+  const int l = lane_id();
+  e.qfrc_smooth = l < m.nv ? dof_force(m, e, l) : (T)0;
 }
 
 // ---------------------------------------------------------------- constraint solver (PGS)
@@ -1032,6 +1052,23 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
 // (safeguarded Newton on its piecewise-linear derivative, as the oracle); MuJoCo's stop rules
 // (scaled dof-space gradient, scaled improvement). Row scalars: q[0] b, q[1] x (efc_force at
 // exit), q[2] R, q[3] B_r.p, q[4] D.
+//
+// The improvement is the cost decrease along the accepted step evaluated term by term, al u.p +
+// al^2 p.p / 2 + sum_r row_cost_change — algebraically MuJoCo's cost(old) - cost(new), without
+// subtracting two totals: on construction states (steel beams deep in the floor) the cost is
+// ~1e10 and the difference of totals rounds to 0 or a few ulps, so the stop test, the iteration
+// count and qacc (at the 1e-3 level, along the weakly constrained light-block directions) would
+// be decided by rounding. oracle/mjref.c newton_solve evaluates the same expression.
+template <typename T>
+__device__ __forceinline__ T row_cost_change(T x, T dx, T D) {
+  // s(x + dx) - s(x) for s(x) = D x^2 / 2 on x < 0, 0 otherwise
+  const T xn = x + dx;
+  if (x < 0 && xn < 0) return (T)0.5 * D * dx * (x + xn);
+  if (x < 0) return (T)-0.5 * D * x * x;
+  if (xn < 0) return (T)0.5 * D * xn * xn;
+  return 0;
+}
+
 template <typename T>
 __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   const int l = lane_id();
@@ -1083,7 +1120,6 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   cw += usum((T)0.5 * uw * uw);
   const bool warm = cw < c0;
   T u = warm ? uw : (T)0;
-  T cost = warm ? cw : c0;
   if (warm) for (int r = l; r < ne; r += 64) efc[8 * r + 1] = efc[8 * r + 3];
   wsync();
   T* H = e.hess;
@@ -1175,36 +1211,52 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     }
     wsync();
     MGX_STAMP(14);  // J p
-    // exact line search: f'(al) = u.p + al p.p + sum_{x + al jp < 0} D (x + al jp) jp
+    // line search along p (oracle/mjref.c newton_solve, MuJoCo's stop rule [ext]): f'(al) = u.p +
+    // al p.p + sum_{x + al jp < 0} D (x + al jp) jp; first point the Newton step from al = 0, then
+    // safeguarded Newton in the bracket until |f'| < gtol = tolerance * ls_tolerance * |s| *
+    // meaninertia * max(1, nv) with s = L^-1 D^-1/2 p the dof-space direction, <= 50 evaluations
     const T g0 = usum(u * p), pp = usum(p * p);
-    T al = 1, lo = 0, hi = (T)1e30;
-    for (int ls = 0; ls < 50; ls++) {
+    T sdof = dl ? p * e.diaginv * sqrtD : (T)0;  // D^-1/2 p
+    sdof = solve_L(m, e, e.qLD, sdof);
+    const T snorm = sqrt(usum(dl ? sdof * sdof : (T)0));
+    auto ls_eval = [&](T al, T& d1, T& d2) {
       T d1p = 0, d2p = 0;
       for (int r = l; r < ne; r += 64) {
         const T* q = efc + 8 * r;
         T jp = q[3], xr = q[1] + al * jp;
         if (xr < 0) { d1p += q[4] * xr * jp; d2p += q[4] * jp * jp; }
       }
-      T d1 = g0 + al * pp + usum(d1p), d2 = pp + usum(d2p);
-      if (d1 < 0) lo = al; else hi = al;
-      T nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
-      if (!(nxt > lo && nxt < hi)) nxt = hi < (T)1e30 ? (T)0.5 * (lo + hi) : 2 * al;
-      bool done = fabs(nxt - al) <= eps * (1 + fabs(al));
-      al = nxt;
-      if (done) break;
+      d1 = g0 + al * pp + usum(d1p);
+      d2 = pp + usum(d2p);
+    };
+    T al = 0;
+    if (snorm >= minval<T>()) {
+      const T gtol = tol * (T)0.01 * snorm * m.meaninertia * (T)(nv > 1 ? nv : 1);
+      T d1, d2;
+      ls_eval((T)0, d1, d2);
+      al = -d1 / d2;
+      T lo = 0, hi = (T)1e30;
+      for (int ls = 0; ls < 50; ls++) {
+        ls_eval(al, d1, d2);
+        if (fabs(d1) < gtol) break;
+        if (d1 < 0) lo = al; else hi = al;
+        T nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
+        if (!(nxt > lo && nxt < hi)) nxt = hi < (T)1e30 ? (T)0.5 * (lo + hi) : 2 * al;
+        const bool stall = fabs(nxt - al) <= eps * (1 + fabs(al));  // no change in floating point
+        al = nxt;
+        if (stall) break;
+      }
     }
     MGX_STAMP(15);  // line search
     u += al * p;
-    T cp = 0;
+    T dc = 0;
     for (int r = l; r < ne; r += 64) {
       T* q = efc + 8 * r;
-      T xr = q[1] + al * q[3];
-      q[1] = xr;
-      if (xr < 0) cp += (T)0.5 * q[4] * xr * xr;
+      dc += row_cost_change(q[1], al * q[3], q[4]);
+      q[1] += al * q[3];
     }
-    T cnew = usum(cp + (T)0.5 * u * u);
-    T improvement = scale * (cost - cnew);
-    cost = cnew;
+    // the cost decrease along the step, evaluated term by term (newton_step_decrease)
+    const T improvement = -scale * (al * g0 + (T)0.5 * al * al * pp + usum(dc));
     iter++;
     wsync();
     g = gradient();

@@ -62,28 +62,6 @@ __global__ void k_reset(DevModel<T> m, mgx_state s, int n_env, const uint8_t* ma
   if (l == 0) ((T*)s.time)[env] = 0;
 }
 
-// Debug dump of one forward pass (stage outputs), offsets from mgx_debug_layout.
-struct DbgOff {
-  int xpos, xquat, xipos, subtree_com, cinert, cdof, qM, qLD, geom_xpos, geom_xmat, ncon, con_dist, con_pos,
-      con_frame, con_geom, nefc, efc_type, efc_id, efc_pos, efc_margin, efc_R, efc_aref, Bmat, cvel, cdof_dot,
-      qfrc_smooth, qacc_smooth, efc_force, qacc, qfrc_constraint, niter, total;
-};
-
-DbgOff dbg_offsets(int nb, int nv, int nM, int ng, int C, int E) {
-  DbgOff o;
-  int p = 0;
-  auto take = [&](int n) { int r = p; p += n; return r; };
-  o.xpos = take(3 * nb); o.xquat = take(4 * nb); o.xipos = take(3 * nb); o.subtree_com = take(3 * nb);
-  o.cinert = take(10 * nb); o.cdof = take(6 * nv); o.qM = take(nM); o.qLD = take(nM);
-  o.geom_xpos = take(3 * ng); o.geom_xmat = take(9 * ng); o.ncon = take(1); o.con_dist = take(C);
-  o.con_pos = take(3 * C); o.con_frame = take(9 * C); o.con_geom = take(2 * C); o.nefc = take(1);
-  o.efc_type = take(E); o.efc_id = take(E); o.efc_pos = take(E); o.efc_margin = take(E); o.efc_R = take(E);
-  o.efc_aref = take(E); o.Bmat = take(E * nv); o.cvel = take(6 * nb); o.cdof_dot = take(6 * nv);
-  o.qfrc_smooth = take(nv); o.qacc_smooth = take(nv); o.efc_force = take(E); o.qacc = take(nv);
-  o.qfrc_constraint = take(nv); o.niter = take(1); o.total = p;
-  return o;
-}
-
 template <typename T, bool GB, bool NT>
 __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s, int n_env, T* dbg, DbgOff o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -211,6 +189,7 @@ int mgx_step(const mgx_model* m, const mgx_state* s, mgx_frames* frames, int n_e
   if (frames) fr = *frames;
   if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   hipStream_t st = (hipStream_t)stream;
+  if (m->wide) return wide_step(m, s, fr, n_env, nsub, mask, st);
   if (m->precision == MGX_F32) launch_step<float>(m, m->mf, s, fr, n_env, nsub, mask, st);
   else launch_step<double>(m, m->md, s, fr, n_env, nsub, mask, st);
   HIPCHK(hipGetLastError());
@@ -249,6 +228,12 @@ int mgx_debug_forward(const mgx_model* m, const mgx_state* s, int n_env, void* d
   if (n_env <= 0) return MGX_OK;
   if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   hipStream_t st = (hipStream_t)stream;
+  if (m->wide) {
+    DbgOff o = m->precision == MGX_F32
+                   ? dbg_offsets(m->mf.nbody, m->mf.nv, m->mf.nM, m->mf.ngeom, m->L.max_ncon, m->L.max_nefc)
+                   : dbg_offsets(m->md.nbody, m->md.nv, m->md.nM, m->md.ngeom, m->L.max_ncon, m->L.max_nefc);
+    return wide_debug(m, s, n_env, dbg, o, st);
+  }
   if (m->precision == MGX_F32) {
     DbgOff o = dbg_offsets(m->mf.nbody, m->mf.nv, m->mf.nM, m->mf.ngeom, m->L.max_ncon, m->L.max_nefc);
     if (m->L.gB) launch_debug_v<float, true>(m, m->mf, s, n_env, (float*)dbg, o, st);

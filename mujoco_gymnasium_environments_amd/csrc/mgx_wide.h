@@ -1,0 +1,621 @@
+// mgx_wide.h — one mj_step for one env with 64 < nv <= 128, executed by one wavefront.
+//
+// The execution model of mgx_physics.h with two dofs per lane: dof d lives on lane d % 64, in
+// register word d / 64 (humanoid_construction: nv 99 = humanoid 36 + crane 3 + ten free blocks
+// 60, construction_site.xml). Every stage that is lane-per-body / -geom / -pair / -row
+// (kinematics, comPos, CRB, collision, makeConstraint, the row transform, the line search) is
+// the mgx_physics.h code itself, which loops over dofs past 64; what changes is everything that
+// keeps a dof-indexed vector in registers: the tree-sparse solves, the per-dof forces, the
+// Newton solver (gradient, MFMA Hessian in tile-row passes, Cholesky with two rows per lane,
+// triangular solves) and RK4's stage vectors. One wave per env keeps every cross-dof step a
+// readlane (no cross-wave LDS barrier); the rows B live in per-env global scratch (Layout.gB)
+// and the nv x nv Hessian overlays the dead phase-A LDS union (make_layout).
+//
+// Restates MuJoCo's mj_step [ext] for RK4 + Newton, the combination construction_site.xml:10
+// selects (integrator="RK4", the default solver); oracle/mjref.c is the stage-level reference.
+#pragma once
+#include "mgx_physics.h"
+
+namespace mgx {
+
+template <typename T>
+struct WEnv {
+  Env<T> e;  // LDS views, contacts, rows; the dof-lane registers of Env are unused
+  T qacc_ws[2], qfrc_applied[2], qfrc_smooth[2], qacc_smooth[2], qacc[2], qfrc_constraint[2], diaginv[2];
+  int chainlen[2], madr[2];
+  uint64_t anc_lo[2], anc_hi[2];  // strict ancestors of dof 64 w + lane among dofs 0..63 / 64..127
+};
+
+__device__ __forceinline__ int wdof(int w) { return 64 * w + lane_id(); }
+
+// value of dof k (uniform) from a two-word lane vector
+template <typename T>
+__device__ __forceinline__ T wread(const T (&x)[2], int k) {
+  return k < 64 ? readlane(x[0], k) : readlane(x[1], k - 64);
+}
+template <typename T>
+__device__ __forceinline__ T wdot(const T (&a)[2], const T (&b)[2]) {
+  return usum(a[0] * b[0] + a[1] * b[1]);
+}
+
+template <typename T>
+__device__ __forceinline__ void wenv_bind(const DevModel<T>& m, WEnv<T>& w, char* smem, T* gB) {
+  env_bind<T, true>(m, w.e, smem, gB);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int d = wdof(k);
+    const bool ok = d < m.nv;
+    w.chainlen[k] = ok ? m.dof_chainlen[d] : 0;
+    w.madr[k] = ok ? m.dof_Madr[d] : 0;
+    w.anc_lo[k] = ok ? m.dof_ancmask[d] : 0ull;
+    w.anc_hi[k] = ok ? m.dof_ancmask_hi[d] : 0ull;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void wload_state(const DevModel<T>& m, WEnv<T>& w, const T* gqpos, const T* gqvel,
+                                            const T* gqacc, const T* gctrl, const T* gqfrc, const T* gxfrc, const T* gtime,
+                                            int env) {
+  Env<T>& e = w.e;
+  const int l = lane_id();
+  for (int k = l; k < m.nq; k += 64) e.qpos[k] = gqpos[(size_t)env * m.nq + k];
+  for (int k = l; k < m.nv; k += 64) e.qvel[k] = gqvel[(size_t)env * m.nv + k];
+  for (int k = l; k < m.nu; k += 64) e.ctrl[k] = gctrl[(size_t)env * m.nu + k];
+  for (int k = l; k < 6 * m.nbody; k += 64) e.xfrc[k] = gxfrc[(size_t)env * 6 * m.nbody + k];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int d = wdof(k);
+    w.qacc_ws[k] = d < m.nv ? gqacc[(size_t)env * m.nv + d] : (T)0;
+    w.qfrc_applied[k] = d < m.nv ? gqfrc[(size_t)env * m.nv + d] : (T)0;
+  }
+  e.time = gtime[env];
+  wsync();
+}
+
+template <typename T>
+__device__ __forceinline__ void wstore_state(const DevModel<T>& m, WEnv<T>& w, T* gqpos, T* gqvel, T* gqacc, T* gctrl,
+                                             T* gqfrc, T* gxfrc, T* gtime, int env) {
+  Env<T>& e = w.e;
+  wsync();
+  const int l = lane_id();
+  for (int k = l; k < m.nq; k += 64) gqpos[(size_t)env * m.nq + k] = e.qpos[k];
+  for (int k = l; k < m.nv; k += 64) gqvel[(size_t)env * m.nv + k] = e.qvel[k];
+  for (int k = l; k < m.nu; k += 64) gctrl[(size_t)env * m.nu + k] = e.ctrl[k];
+  for (int k = l; k < 6 * m.nbody; k += 64) gxfrc[(size_t)env * 6 * m.nbody + k] = e.xfrc[k];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int d = wdof(k);
+    if (d < m.nv) {
+      gqacc[(size_t)env * m.nv + d] = w.qacc_ws[k];
+      gqfrc[(size_t)env * m.nv + d] = w.qfrc_applied[k];
+    }
+  }
+  if (l == 0) gtime[env] = e.time;
+}
+
+// mj_resetData on the LDS copy and the dof registers
+template <typename T>
+__device__ __forceinline__ void wreset_env(const DevModel<T>& m, WEnv<T>& w) {
+  reset_env(m, w.e);
+#pragma unroll
+  for (int k = 0; k < 2; k++) { w.qacc_ws[k] = 0; w.qfrc_applied[k] = 0; }
+}
+
+// ---------------------------------------------------------------- tree-sparse solves
+// x <- L'^-1 x: for k = nv-1 .. 0 the ancestors j of k get x[j] -= L[k][j] x[k]
+template <typename T>
+__device__ __forceinline__ void wsolve_LT(const DevModel<T>& m, const WEnv<T>& w, const T* LD, T (&x)[2]) {
+  const int l = lane_id();
+  const bool v0 = l < m.nv, v1 = 64 + l < m.nv;
+  for (int k = m.nv - 1; k >= 0; k--) {
+    const T xk = wread(x, k);
+    const uint64_t alo = m.dof_ancmask[k], ahi = m.dof_ancmask_hi[k];
+    const int base = m.dof_Madr[k] + m.dof_chainlen[k];
+    if (v0 && ((alo >> l) & 1ull)) x[0] -= LD[base - w.chainlen[0]] * xk;
+    if (v1 && ((ahi >> l) & 1ull)) x[1] -= LD[base - w.chainlen[1]] * xk;
+  }
+}
+// x <- L^-1 x: for i = 0 .. nv-1 every descendant d of i gets x[d] -= L[d][i] x[i]
+template <typename T>
+__device__ __forceinline__ void wsolve_L(const DevModel<T>& m, const WEnv<T>& w, const T* LD, T (&x)[2]) {
+  const int l = lane_id();
+  const bool v0 = l < m.nv, v1 = 64 + l < m.nv;
+  const int b0 = w.madr[0] + w.chainlen[0], b1 = w.madr[1] + w.chainlen[1];
+  for (int i = 0; i < m.nv; i++) {
+    const T xi = wread(x, i);
+    const int ci = m.dof_chainlen[i];
+    if (i < 64) {
+      if (v0 && ((w.anc_lo[0] >> i) & 1ull)) x[0] -= LD[b0 - ci] * xi;
+      if (v1 && ((w.anc_lo[1] >> i) & 1ull)) x[1] -= LD[b1 - ci] * xi;
+    } else {
+      if (v1 && ((w.anc_hi[1] >> (i - 64)) & 1ull)) x[1] -= LD[b1 - ci] * xi;
+    }
+  }
+}
+// y = L x
+template <typename T>
+__device__ __forceinline__ void wmul_L(const DevModel<T>& m, const WEnv<T>& w, const T* LD, const T (&x)[2], T (&y)[2]) {
+  const int l = lane_id();
+  const bool v0 = l < m.nv, v1 = 64 + l < m.nv;
+  const int b0 = w.madr[0] + w.chainlen[0], b1 = w.madr[1] + w.chainlen[1];
+  y[0] = x[0];
+  y[1] = x[1];
+  for (int i = 0; i < m.nv; i++) {
+    const T xi = wread(x, i);
+    const int ci = m.dof_chainlen[i];
+    if (i < 64) {
+      if (v0 && ((w.anc_lo[0] >> i) & 1ull)) y[0] += LD[b0 - ci] * xi;
+      if (v1 && ((w.anc_lo[1] >> i) & 1ull)) y[1] += LD[b1 - ci] * xi;
+    } else {
+      if (v1 && ((w.anc_hi[1] >> (i - 64)) & 1ull)) y[1] += LD[b1 - ci] * xi;
+    }
+  }
+}
+// y = L' u
+template <typename T>
+__device__ __forceinline__ void wmul_LT(const DevModel<T>& m, const WEnv<T>& w, const T* LD, const T (&u)[2], T (&y)[2]) {
+  const int l = lane_id();
+  const bool v0 = l < m.nv, v1 = 64 + l < m.nv;
+  y[0] = u[0];
+  y[1] = u[1];
+  for (int k = 0; k < m.nv; k++) {
+    const T uk = wread(u, k);
+    const uint64_t alo = m.dof_ancmask[k], ahi = m.dof_ancmask_hi[k];
+    const int base = m.dof_Madr[k] + m.dof_chainlen[k];
+    if (v0 && ((alo >> l) & 1ull)) y[0] += LD[base - w.chainlen[0]] * uk;
+    if (v1 && ((ahi >> l) & 1ull)) y[1] += LD[base - w.chainlen[1]] * uk;
+  }
+}
+// x = M^-1 y
+template <typename T>
+__device__ __forceinline__ void wsolve_M(const DevModel<T>& m, const WEnv<T>& w, const T* LD, const T (&y)[2], T (&x)[2]) {
+  x[0] = y[0];
+  x[1] = y[1];
+  wsolve_LT(m, w, LD, x);
+  x[0] *= w.diaginv[0];
+  x[1] *= w.diaginv[1];
+  wsolve_L(m, w, LD, x);
+}
+
+// ---------------------------------------------------------------- Newton Hessian on MFMA
+// H = I + sum_{x_r<0} D_r B_r B_r' for nv <= 128 (8 tile rows of 16): the lower tiles of tile
+// rows [T0, T1) per pass, so the accumulators of one pass stay in registers (hessian_mfma's
+// fragment layout, mgx_physics.h); passes over tile rows beyond the model's are skipped.
+template <typename T, int T0, int T1>
+__device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
+  typedef T V4 __attribute__((ext_vector_type(4)));
+  constexpr int NT = (T1 * (T1 + 1) - T0 * (T0 + 1)) / 2;
+  const int l = lane_id(), i = l & 15, kq = l >> 4;
+  const int nt = (nv + 15) >> 4;
+  if (T0 >= nt) return;
+  auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
+  V4 acc[NT];
+#pragma unroll
+  for (int t = T0, q = 0; t < T1; t++)
+#pragma unroll
+    for (int u = 0; u <= t; u++, q++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) acc[q][v] = (t == u && row_of(v) == i) ? (T)1 : (T)0;
+  auto load = [&](int r0, T* b, T& sc) {
+    const int r = r0 + kq;
+    sc = 0;
+    if (r < ne) {
+      const T x = efc[8 * r + 1];
+      sc = x < 0 ? efc[8 * r + 4] : (T)0;
+    }
+#pragma unroll
+    for (int t = 0; t < T1; t++) {
+      const int c = 16 * t + i;
+      b[t] = (r < ne && c < nv) ? Bm[r * Bs + c] : (T)0;
+    }
+  };
+  T bn[T1], sn;
+  load(0, bn, sn);
+  for (int r0 = 0; r0 < ne; r0 += 4) {
+    T b[T1];
+#pragma unroll
+    for (int t = 0; t < T1; t++) b[t] = bn[t];
+    const T sc = sn;
+    load(r0 + 4, bn, sn);
+#pragma unroll
+    for (int t = T0, q = 0; t < T1; t++)
+#pragma unroll
+      for (int u = 0; u <= t; u++, q++) {
+        if (t < nt) {
+          if constexpr (sizeof(T) == 8)
+            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sc * b[t], b[u], acc[q], 0, 0, 0);
+          else
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(sc * b[t], b[u], acc[q], 0, 0, 0);
+        }
+      }
+  }
+#pragma unroll
+  for (int t = T0, q = 0; t < T1; t++)
+#pragma unroll
+    for (int u = 0; u <= t; u++, q++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        const int row = 16 * t + row_of(v), col = 16 * u + i;
+        if (t < nt && row < nv && col <= row) H[row * nv + col] = acc[q][v];
+      }
+}
+
+template <typename T>
+__device__ __forceinline__ void whessian(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
+  whess_pass<T, 0, 4>(Bm, Bs, efc, ne, nv, H);  // 10 tiles
+  whess_pass<T, 4, 6>(Bm, Bs, efc, ne, nv, H);  // 11 tiles
+  whess_pass<T, 6, 7>(Bm, Bs, efc, ne, nv, H);  // 7 tiles
+  whess_pass<T, 7, 8>(Bm, Bs, efc, ne, nv, H);  // 8 tiles
+}
+
+// ---------------------------------------------------------------- Newton (mj_solNewton)
+// newton() of mgx_physics.h with two-word dof vectors; same whitened coordinates, row scalars
+// (q[0] b, q[1] x / force, q[2] R, q[3] B_r.p, q[4] D, q[5] aref, q[6] B damping), the same line
+// search and stop rules.
+template <typename T>
+__device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
+  Env<T>& e = w.e;
+  const int l = lane_id();
+  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+  const int nv = m.nv;
+  const bool dl[2] = {l < nv, 64 + l < nv};
+  const int lc[2] = {dl[0] ? l : 0, dl[1] ? 64 + l : 0};
+  T sqrtD[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) sqrtD[k] = dl[k] ? sqrt(e.qLD[w.madr[k]]) : (T)0;
+  if (ne == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) { w.qacc[k] = w.qacc_smooth[k]; w.qfrc_constraint[k] = 0; }
+    e.niter = 0;
+    return;
+  }
+  T qv[2] = {dl[0] ? e.qvel[l] : (T)0, dl[1] ? e.qvel[64 + l] : (T)0};
+  T wv[2], ws[2], ww[2], wd[2];
+  wmul_L(m, w, e.qLD, qv, wv);
+  wmul_L(m, w, e.qLD, w.qacc_smooth, ws);
+  wmul_L(m, w, e.qLD, w.qacc_ws, ww);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    wv[k] *= sqrtD[k];
+    ws[k] *= sqrtD[k];
+    ww[k] *= sqrtD[k];
+    wd[k] = dl[k] ? ww[k] - ws[k] : (T)0;
+  }
+  T* efc = e.efc;
+  const T* Bm = e.Bm;
+  const int Bs = e.Bs;
+  // per row: aref, b = J qacc_smooth - aref, D; x at u = 0 (q[1]) and at the warmstart (q[3])
+  T c0 = 0, cw = 0;
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T xa[MGX_RB], xb[MGX_RB];
+    load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
+    load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      if (r < ne) {
+        T dv = xa[j] * wv[0] + xb[j] * wv[1], ds = xa[j] * ws[0] + xb[j] * ws[1];
+        T dw = xa[j] * wd[0] + xb[j] * wd[1], z = 0;
+        wave_sum4(dv, ds, dw, z);
+        T* q = efc + 8 * r;
+        const T aref = -q[6] * dv - q[5];
+        const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
+        if (b < 0) c0 += (T)0.5 * D * b * b;
+        if (xw < 0) cw += (T)0.5 * D * xw * xw;
+        if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
+      }
+    }
+  }
+  wsync();
+  cw += (T)0.5 * wdot(wd, wd);
+  const bool warm = cw < c0;
+  T u[2] = {warm ? wd[0] : (T)0, warm ? wd[1] : (T)0};
+  if (warm) for (int r = l; r < ne; r += 64) efc[8 * r + 1] = efc[8 * r + 3];
+  wsync();
+  T* H = e.hess;
+  const T scale = (T)1 / (m.meaninertia * (T)(nv > 1 ? nv : 1));
+  const T tol = m.tolerance;
+  const T eps = sizeof(T) == 4 ? (T)1e-7 : (T)1e-15;
+  const int maxit = m.iterations;
+  int iter = 0;
+  // whitened gradient g = u + sum_{x<0} D x B_r
+  auto gradient = [&](T (&gg)[2]) {
+    gg[0] = u[0];
+    gg[1] = u[1];
+    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+      T xa[MGX_RB], xb[MGX_RB];
+      load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
+      load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
+#pragma unroll
+      for (int j = 0; j < MGX_RB; j++) {
+        const int r = r0 + j;
+        if (r < ne) {
+          const T xr = efc[8 * r + 1];
+          if (xr < 0) {
+            const T s = efc[8 * r + 4] * xr;
+            gg[0] += s * xa[j];
+            gg[1] += s * xb[j];
+          }
+        }
+      }
+    }
+    gg[0] = dl[0] ? gg[0] : (T)0;
+    gg[1] = dl[1] ? gg[1] : (T)0;
+  };
+  T g[2];
+  gradient(g);
+  while (iter < maxit) {
+    whessian(Bm, Bs, efc, ne, nv, H);
+    wsync();
+    // Cholesky H = L L' in place, left-looking, lane = rows l and 64 + l
+    for (int k = 0; k < nv; k++) {
+      const T* Lk = H + k * nv;
+      T s2[2];
+#pragma unroll
+      for (int wd2 = 0; wd2 < 2; wd2++) {
+        const int i = 64 * wd2 + l;
+        const bool act = i < nv && i >= k;
+        const int li = act ? i : k;
+        const T* Li = H + li * nv;
+        T a8[8] = {H[li * nv + k], 0, 0, 0, 0, 0, 0, 0};
+        int j = 0;
+        for (; j + 7 < k; j += 8) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) a8[t] -= Li[j + t] * Lk[j + t];
+        }
+        for (; j < k; j++) a8[0] -= Li[j] * Lk[j];
+        s2[wd2] = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
+      }
+      const T dkk = wread(s2, k);
+      const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
+#pragma unroll
+      for (int wd2 = 0; wd2 < 2; wd2++) {
+        const int i = 64 * wd2 + l;
+        if (i < nv && i >= k) H[i * nv + k] = i == k ? d : s2[wd2] / d;
+      }
+      wsync();
+    }
+    // L y = -g, L' p = y
+    T rdiag[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) rdiag[k] = dl[k] ? (T)1 / H[(64 * k + l) * nv + 64 * k + l] : (T)0;
+    T y[2] = {-g[0], -g[1]};
+    for (int k = 0; k < nv; k++) {
+      const T yk = wread(y, k) * wread(rdiag, k);
+#pragma unroll
+      for (int wd2 = 0; wd2 < 2; wd2++) {
+        const int i = 64 * wd2 + l;
+        if (i == k) y[wd2] = yk;
+        else if (i < nv && i > k) y[wd2] -= H[i * nv + k] * yk;
+      }
+    }
+    T p[2] = {y[0], y[1]};
+    for (int k = nv - 1; k >= 0; k--) {
+      const T pk = wread(p, k) * wread(rdiag, k);
+#pragma unroll
+      for (int wd2 = 0; wd2 < 2; wd2++) {
+        const int i = 64 * wd2 + l;
+        if (i == k) p[wd2] = pk;
+        else if (i < k) p[wd2] -= H[k * nv + i] * pk;
+      }
+    }
+    p[0] = dl[0] ? p[0] : (T)0;
+    p[1] = dl[1] ? p[1] : (T)0;
+    // J p per row (row-major, wave reductions); lane 0 stores
+    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+      T xa[MGX_RB], xb[MGX_RB];
+      load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
+      load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
+#pragma unroll
+      for (int j = 0; j < MGX_RB; j += 4) {
+        T s0 = xa[j] * p[0] + xb[j] * p[1], s1 = xa[j + 1] * p[0] + xb[j + 1] * p[1];
+        T s2 = xa[j + 2] * p[0] + xb[j + 2] * p[1], s3 = xa[j + 3] * p[0] + xb[j + 3] * p[1];
+        wave_sum4(s0, s1, s2, s3);
+        if (l == 0) {
+          if (r0 + j < ne) efc[8 * (r0 + j) + 3] = s0;
+          if (r0 + j + 1 < ne) efc[8 * (r0 + j + 1) + 3] = s1;
+          if (r0 + j + 2 < ne) efc[8 * (r0 + j + 2) + 3] = s2;
+          if (r0 + j + 3 < ne) efc[8 * (r0 + j + 3) + 3] = s3;
+        }
+      }
+    }
+    wsync();
+    // line search (newton(), mgx_physics.h: MuJoCo's stop rule)
+    const T g0 = wdot(u, p), pp = wdot(p, p);
+    T sdof[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) sdof[k] = dl[k] ? p[k] * w.diaginv[k] * sqrtD[k] : (T)0;
+    wsolve_L(m, w, e.qLD, sdof);
+    const T snorm = sqrt(wdot(sdof, sdof));
+    auto ls_eval = [&](T al, T& d1, T& d2) {
+      T d1p = 0, d2p = 0;
+      for (int r = l; r < ne; r += 64) {
+        const T* q = efc + 8 * r;
+        T jp = q[3], xr = q[1] + al * jp;
+        if (xr < 0) { d1p += q[4] * xr * jp; d2p += q[4] * jp * jp; }
+      }
+      d1 = g0 + al * pp + usum(d1p);
+      d2 = pp + usum(d2p);
+    };
+    T al = 0;
+    if (snorm >= minval<T>()) {
+      const T gtol = tol * (T)0.01 * snorm * m.meaninertia * (T)(nv > 1 ? nv : 1);
+      T d1, d2;
+      ls_eval((T)0, d1, d2);
+      al = -d1 / d2;
+      T lo = 0, hi = (T)1e30;
+      for (int ls = 0; ls < 50; ls++) {
+        ls_eval(al, d1, d2);
+        if (fabs(d1) < gtol) break;
+        if (d1 < 0) lo = al; else hi = al;
+        T nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
+        if (!(nxt > lo && nxt < hi)) nxt = hi < (T)1e30 ? (T)0.5 * (lo + hi) : 2 * al;
+        const bool stall = fabs(nxt - al) <= eps * (1 + fabs(al));
+        al = nxt;
+        if (stall) break;
+      }
+    }
+    u[0] += al * p[0];
+    u[1] += al * p[1];
+    T dc = 0;
+    for (int r = l; r < ne; r += 64) {
+      T* q = efc + 8 * r;
+      dc += row_cost_change(q[1], al * q[3], q[4]);
+      q[1] += al * q[3];
+    }
+    const T improvement = -scale * (al * g0 + (T)0.5 * al * al * pp + usum(dc));
+    iter++;
+    wsync();
+    gradient(g);
+    // the gradient rule is on the dof-space gradient L' D^1/2 g
+    T sg[2] = {sqrtD[0] * g[0], sqrtD[1] * g[1]}, ga[2];
+    wmul_LT(m, w, e.qLD, sg, ga);
+    ga[0] = dl[0] ? ga[0] : (T)0;
+    ga[1] = dl[1] ? ga[1] : (T)0;
+    const bool stop = improvement < tol || scale * sqrt(wdot(ga, ga)) < tol;
+    if (stop) break;
+  }
+  e.niter = iter;
+  for (int r = l; r < ne; r += 64) {
+    T* q = efc + 8 * r;
+    q[1] = q[1] < 0 ? -q[4] * q[1] : (T)0;
+  }
+  wsync();
+  // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = L' D^1/2 (sum f_r B_r)
+  T v[2] = {0, 0};
+  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
+    T xa[MGX_RB], xb[MGX_RB];
+    load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
+    load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++)
+      if (r0 + j < ne) {
+        const T f = efc[8 * (r0 + j) + 1];
+        v[0] += f * xa[j];
+        v[1] += f * xb[j];
+      }
+  }
+  T z[2], sv[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    z[k] = dl[k] ? u[k] * w.diaginv[k] * sqrtD[k] : (T)0;
+    sv[k] = dl[k] ? sqrtD[k] * v[k] : (T)0;
+  }
+  wsolve_L(m, w, e.qLD, z);
+#pragma unroll
+  for (int k = 0; k < 2; k++) w.qacc[k] = w.qacc_smooth[k] + z[k];
+  wmul_LT(m, w, e.qLD, sv, w.qfrc_constraint);
+  wsync();
+}
+
+// ---------------------------------------------------------------- forward + step
+template <typename T>
+__device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
+  Env<T>& e = w.e;
+  kinematics(m, e);
+  com_crb(m, e);
+  factor_ld<T, true>(m, e, e.qLD);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int d = wdof(k);
+    w.diaginv[k] = d < m.nv ? (T)1 / e.qLD[m.dof_Madr[d]] : (T)0;
+  }
+  velocity_bodies(m, e);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int d = wdof(k);
+    w.qfrc_smooth[k] = d < m.nv ? dof_force_applied(m, e, d, w.qfrc_applied[k]) : (T)0;
+  }
+  wsolve_M(m, w, e.qLD, w.qfrc_smooth, w.qacc_smooth);
+  collision(m, e);
+  make_constraint(m, e);
+  // D^-1/2 per dof for the row transform
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int d = wdof(k);
+    if (d < m.nv) e.vec0[d] = sqrt(w.diaginv[k]);
+  }
+  wsync();
+  transform_rows<T, true>(m, e);
+  wnewton(m, w);
+}
+
+// mj_RungeKutta(m, d, 4) [ext] (rk4() of mgx_physics.h with two-word stage vectors)
+template <typename T>
+__device__ __forceinline__ void wrk4(const DevModel<T>& m, WEnv<T>& w) {
+  Env<T>& e = w.e;
+  const T A[9] = {(T)0.5, 0, 0, 0, (T)0.5, 0, 0, 0, (T)1};
+  const T B[4] = {(T)(1.0 / 6.0), (T)(1.0 / 3.0), (T)(1.0 / 3.0), (T)(1.0 / 6.0)};
+  const int l = lane_id(), nq = m.nq, nv = m.nv;
+  const bool dl[2] = {l < nv, 64 + l < nv};
+  T* q0 = e.rk;
+  T* dxv = e.rk + ((nq + 3) & ~3);
+  const T h = m.timestep, t0 = e.time;
+  for (int k = l; k < nq; k += 64) q0[k] = e.qpos[k];
+  T v[4][2], f[4][2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    v[0][k] = dl[k] ? e.qvel[64 * k + l] : (T)0;
+    f[0][k] = dl[k] ? w.qacc[k] : (T)0;
+  }
+  for (int i = 1; i < 4; i++) {
+    T C = 0, dv[2] = {0, 0}, da[2] = {0, 0};
+    for (int j = 0; j < i; j++) {
+      const T a = A[(i - 1) * 3 + j];
+      C += a;
+#pragma unroll
+      for (int k = 0; k < 2; k++) { dv[k] += a * v[j][k]; da[k] += a * f[j][k]; }
+    }
+    wsync();
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+      if (dl[k]) dxv[64 * k + l] = dv[k];
+    for (int k = l; k < nq; k += 64) e.qpos[k] = q0[k];
+    wsync();
+    integrate_pos(m, e.qpos, dxv, h);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      v[i][k] = v[0][k] + h * da[k];
+      if (dl[k]) e.qvel[64 * k + l] = v[i][k];
+    }
+    e.time = t0 + C * h;
+    wsync();
+    wforward(m, w);
+#pragma unroll
+    for (int k = 0; k < 2; k++) f[i][k] = dl[k] ? w.qacc[k] : (T)0;
+  }
+  T dv[2] = {0, 0}, da[2] = {0, 0};
+  for (int j = 0; j < 4; j++)
+#pragma unroll
+    for (int k = 0; k < 2; k++) { dv[k] += B[j] * v[j][k]; da[k] += B[j] * f[j][k]; }
+#pragma unroll
+  for (int k = 0; k < 2; k++) w.qacc_ws[k] = w.qacc[k];  // mj_advance keeps the last evaluation's qacc
+  wsync();
+  for (int k = l; k < nq; k += 64) e.qpos[k] = q0[k];
+#pragma unroll
+  for (int k = 0; k < 2; k++)
+    if (dl[k]) { dxv[64 * k + l] = dv[k]; e.qvel[64 * k + l] = v[0][k] + h * da[k]; }
+  wsync();
+  integrate_pos(m, e.qpos, dxv, h);
+  e.time = t0 + h;
+}
+
+// mj_step for RK4 + Newton; returns the number of bad-state resets (mj_checkPos / Vel / Acc)
+template <typename T>
+__device__ __forceinline__ int wmj_step(const DevModel<T>& m, WEnv<T>& w) {
+  Env<T>& e = w.e;
+  int warn = 0;
+  if (any_bad(e.qpos, m.nq)) { wreset_env(m, w); warn++; }
+  if (any_bad(e.qvel, m.nv)) { wreset_env(m, w); warn++; }
+  wforward(m, w);
+  const int l = lane_id();
+  if (ballot((l < m.nv && isbad(w.qacc[0])) || (64 + l < m.nv && isbad(w.qacc[1]))) != 0ull) {
+    wreset_env(m, w);
+    warn++;
+    wforward(m, w);
+  }
+  wrk4(m, w);
+  return warn;
+}
+
+}  // namespace mgx

@@ -16,11 +16,11 @@ ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
 SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip", "mgx_dancing.hip",
-           "mgx_martial.hip", "mgx_assembly.hip"]
+           "mgx_martial.hip", "mgx_assembly.hip", "mgx_construction.hip"]
 # per-translation-unit flags: the staged solver's FMA chains must not be SLP-packed (mgx_pgs.hip)
 SOURCE_FLAGS = {"mgx_pgs.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
-           "mgx_bipedal.h", "mgx_dancing.h", "mgx_martial.h", "mgx_internal.h"]
+           "mgx_bipedal.h", "mgx_dancing.h", "mgx_martial.h", "mgx_internal.h", "mgx_wide.h", "mgx_construction.h"]
 # task headers included by one translation unit only (so editing one rebuilds one object)
 TU_HEADERS = {"mgx_assembly.hip": ["mgx_assembly.h"]}
 
@@ -135,6 +135,13 @@ _SIGS = {
                            C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_martial_logic_test": ([_VP, C.POINTER(cabi.MgxMartialLogicIO), C.POINTER(cabi.MgxMartialEnv), C.c_int, _VP],
                                C.c_int),
+    "mgx_construction_configure": ([_VP, C.POINTER(cabi.MgxConstructionIds)], C.c_int),
+    "mgx_construction_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxConstructionEnv), _VP, _VP, _VP, _VP,
+                               _VP, _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_construction_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxConstructionEnv), _VP, _VP,
+                                C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),
+    "mgx_construction_logic_test": ([_VP, C.POINTER(cabi.MgxConstructionLogicIO), C.POINTER(cabi.MgxConstructionEnv),
+                                     C.c_int, _VP], C.c_int),
     "mgx_assembly_configure": ([_VP, C.POINTER(cabi.MgxAssemblyIds)], C.c_int),
     "mgx_assembly_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxAssemblyEnv), _VP, _VP, _VP, _VP, _VP,
                            _VP, C.c_int, C.c_int, _VP, _VP], C.c_int),

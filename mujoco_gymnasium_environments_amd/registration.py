@@ -29,6 +29,8 @@ REGISTRY: Dict[str, tuple] = {
     'HumanoidDancing-v0': ('mujoco_gymnasium_environments_amd.envs.dancing:HumanoidDancingEnv', 3600, 5000.0, {}),
     'RoboticArmAssembly-v0': ('mujoco_gymnasium_environments_amd.envs.assembly:RoboticArmAssemblyEnv', 150000, 8000.0,
                               {}),   # robotic_arm_assembly_env/__init__.py:12-17
+    'HumanoidConstruction-v0': ('mujoco_gymnasium_environments_amd.envs.construction:HumanoidConstructionEnv', 3000,
+                                10000.0, {'render_mode': None}),   # humanoid_construction_env/__init__.py:18-26
     # martial arts registers nothing in the reference (humanoid_martial_arts_env/__init__.py)
 }
 

@@ -13,6 +13,8 @@
 #define MINIMP 0.0001
 #define MAXIMP 0.9999
 #define MAXCONPAIR 8
+#define LS_TOLERANCE 0.01 /* mjOption.ls_tolerance default [ext] */
+#define LS_ITERATIONS 50  /* mjOption.ls_iterations default [ext] */
 
 enum { JFREE = 0, JBALL = 1, JSLIDE = 2, JHINGE = 3 };
 enum { GPLANE = 0, GHFIELD = 1, GSPHERE = 2, GCAPSULE = 3, GELLIPSOID = 4, GCYLINDER = 5, GBOX = 6 };
@@ -473,17 +475,6 @@ static void make_frame(double *f) {
 
 typedef struct { double dist, pos[3], n[3]; } rcon;
 
-/* sphere-sphere core: normal from 1 to 2, pos = midpoint of the surfaces */
-static int sph_sph(const double *c1, double r1, const double *c2, double r2, double margin, rcon *out) {
-  double dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
-  double L = normalize3(dv);
-  double dist = L - r1 - r2;
-  if (dist > margin) return 0;
-  out->dist = dist;
-  for (int k = 0; k < 3; k++) { out->n[k] = dv[k]; out->pos[k] = c1[k] + dv[k] * (r1 + 0.5 * dist); }
-  return 1;
-}
-
 static void seg_ends(const double *pos, const double *mat, double hl, double *a, double *b) {
   for (int k = 0; k < 3; k++) { a[k] = pos[k] - hl * mat[3 * k + 2]; b[k] = pos[k] + hl * mat[3 * k + 2]; }
 }
@@ -506,13 +497,17 @@ static void seg_seg(const double *p1, const double *q1, const double *p2, const 
 }
 
 /* signed distance of a box-local point to the box; e = outward unit normal at the closest
- * surface feature (box frame). Inside: nearest face, ties -> lowest axis. */
+ * surface feature (box frame). Inside: nearest face, ties (within 1e-12 of the size) -> lowest axis. */
 static double box_sd(const double *p, const double *h, double *e) {
+  /* a coordinate within `tie` outside its face plane counts as on it (points placed on a face
+     boundary by construction classify the same under any rounding) */
+  const double tie = 1e-12 * (h[0] + h[1] + h[2]);
   int outside = 0;
   double q[3], dv[3];
   for (int k = 0; k < 3; k++) {
     q[k] = clampd(p[k], -h[k], h[k]);
     dv[k] = p[k] - q[k];
+    if (fabs(dv[k]) <= tie) dv[k] = 0;
     if (dv[k] != 0) outside = 1;
   }
   if (outside) {
@@ -520,14 +515,16 @@ static double box_sd(const double *p, const double *h, double *e) {
     e[0] = dv[0]; e[1] = dv[1]; e[2] = dv[2];
     return L;
   }
+  /* faces within `tie` of the nearest count as equally near: the lowest axis wins (a capsule
+     axis's deepest point inside a box sits where two face distances are equal) */
   int best = 0;
   double bd = h[0] - fabs(p[0]);
   for (int k = 1; k < 3; k++) {
     double dk = h[k] - fabs(p[k]);
-    if (dk < bd) { bd = dk; best = k; }
+    if (dk < bd - tie) { bd = dk; best = k; }
   }
   e[0] = e[1] = e[2] = 0;
-  e[best] = p[best] >= 0 ? 1 : -1;
+  e[best] = p[best] >= -tie ? 1 : -1; /* on the mid-plane (within tie) the + face */
   return -bd;
 }
 
@@ -545,48 +542,182 @@ static int sphere_box_core(const double *c, double r, const double *bp, const do
   return 1;
 }
 
-/* capsule (geom1) vs box (geom2): endpoint spheres + the deepest interior point when it is
- * deeper than both ends (golden-section over the convex signed-distance profile). */
+/* Narrowphase branch counters (test infrastructure: tools/narrowphase_stats.py reads them at
+ * bench conditions): [0] capsule-box pairs with 1 contact, [1] with 2, [2] capsule-capsule
+ * general, [3] capsule-capsule parallel branch, [4] its contacts, [5..13] box-box pairs by
+ * contact count 0..8 */
+static long g_np_stats[16];
+void ref_narrowphase_stats(long *out, int reset) {
+  for (int k = 0; k < 16; k++) out[k] = g_np_stats[k];
+  if (reset) memset(g_np_stats, 0, sizeof(g_np_stats));
+}
+
+/* point of a capsule axis c + s a (box frame, s in [-1, 1]) closest to / deepest in the box:
+ * the convex signed distance d(s) is minimised over its ends, kinks (face-plane and zero
+ * crossings, equal inside face distances) and the stationary points of its outside pieces (26
+ * sign patterns); the lowest s within tol of the minimum wins (mgx_collide.h capsule_box_segpos) */
+static double capsule_box_segpos(const double *c, const double *a, const double *h) {
+  double best = 1e30, e[3], p[3], cand[49], dv[49];
+  double hm = h[0] > h[1] ? (h[0] > h[2] ? h[0] : h[2]) : (h[1] > h[2] ? h[1] : h[2]);
+  const double tol = 1e-10 * (1 + hm);
+  int nc = 0;
+  cand[nc++] = -1;
+  cand[nc++] = 1;
+  for (int i = 0; i < 3; i++)
+    if (fabs(a[i]) > MINVAL) {
+      cand[nc++] = (h[i] - c[i]) / a[i];
+      cand[nc++] = (-h[i] - c[i]) / a[i];
+      cand[nc++] = -c[i] / a[i];
+    }
+  for (int i = 0; i < 3; i++)
+    for (int j = i + 1; j < 3; j++)
+      for (int sg = 0; sg < 4; sg++) {
+        double si = (sg & 1) ? -1 : 1, sj = (sg & 2) ? -1 : 1;
+        double den = sj * a[j] - si * a[i];
+        if (fabs(den) > MINVAL) cand[nc++] = (h[j] - h[i] - sj * c[j] + si * c[i]) / den;
+      }
+  for (int pat = 1; pat < 27; pat++) {
+    double num = 0, den = 0;
+    int q = pat;
+    for (int i = 0; i < 3; i++, q /= 3) {
+      int st = q % 3;
+      if (!st) continue;
+      double sg = st == 1 ? 1 : -1;
+      num += a[i] * (sg * h[i] - c[i]);
+      den += a[i] * a[i];
+    }
+    if (den > MINVAL) cand[nc++] = num / den;
+  }
+  for (int k = 0; k < nc; k++) {
+    double sk = clampd(cand[k], -1, 1);
+    cand[k] = sk;
+    for (int i = 0; i < 3; i++) p[i] = c[i] + sk * a[i];
+    dv[k] = box_sd(p, h, e);
+    if (dv[k] < best) best = dv[k];
+  }
+  double bs = 2;
+  for (int k = 0; k < nc; k++)
+    if (dv[k] <= best + tol && cand[k] < bs) bs = cand[k];
+  return bs;
+}
+
+/* sphere of radius r at box-frame point pl (world point w) vs the box */
+static int sphere_box_local(const double *pl, const double *w, double r, const double *bm, const double *h,
+                            double margin, double *e, rcon *out) {
+  double sd = box_sd(pl, h, e), dist = sd - r, ew[3];
+  if (dist > margin) return 0;
+  mulmatvec3(ew, bm, e);
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = -ew[k]; out->pos[k] = w[k] - ew[k] * (r + 0.5 * dist); }
+  return 1;
+}
+
+/* capsule (geom1) vs box (geom2), <= 2 contacts, structured as mjc_CapsuleBox [ext]: the axis
+ * point closest to / deepest in the box as a sphere-box contact; when it is on a box face, a
+ * second sphere-box contact at the far end of the axis's overlap with the face rectangle if
+ * that point is within margin of the same face (dropped within a tenth of the radius of the
+ * first). The thresholds are this restatement's: MuJoCo's source is not available here. */
 static int capsule_box(const double *cp, const double *cm, const double *cs, const double *bp, const double *bm,
                        const double *h, double margin, rcon *out) {
-  double a[3], b[3], al[3], bl[3], tmp[3], e[3];
-  double r = cs[0];
-  seg_ends(cp, cm, cs[1], a, b);
-  for (int k = 0; k < 3; k++) tmp[k] = a[k] - bp[k];
-  mulmatTvec3(al, bm, tmp);
-  for (int k = 0; k < 3; k++) tmp[k] = b[k] - bp[k];
-  mulmatTvec3(bl, bm, tmp);
-  double lo = 0, hi = 1;
-  const double gr = 0.6180339887498949;
-  double x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), f1, f2, p[3];
-  for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
-  f1 = box_sd(p, h, e);
-  for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
-  f2 = box_sd(p, h, e);
-  for (int it = 0; it < 40; it++) {
-    if (f1 <= f2) {
-      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-      for (int k = 0; k < 3; k++) p[k] = al[k] + x1 * (bl[k] - al[k]);
-      f1 = box_sd(p, h, e);
-    } else {
-      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-      for (int k = 0; k < 3; k++) p[k] = al[k] + x2 * (bl[k] - al[k]);
-      f2 = box_sd(p, h, e);
+  double r = cs[0], hl = cs[1];
+  double tmp[3] = {cp[0] - bp[0], cp[1] - bp[1], cp[2] - bp[2]}, c[3], a[3];
+  double ax[3] = {cm[2] * hl, cm[5] * hl, cm[8] * hl};
+  mulmatTvec3(c, bm, tmp);
+  mulmatTvec3(a, bm, ax);
+  double s1 = capsule_box_segpos(c, a, h), pl[3], w[3], e[3], e2[3];
+  for (int k = 0; k < 3; k++) { pl[k] = c[k] + s1 * a[k]; w[k] = cp[k] + s1 * ax[k]; }
+  if (!sphere_box_local(pl, w, r, bm, h, margin, e, out)) return 0;
+  int fk = -1, nz = 0, n = 1;
+  for (int k = 0; k < 3; k++)
+    if (e[k] != 0) { nz++; fk = k; }
+  double lo = -1, hi = 1;
+  int ok = nz == 1;
+  for (int i = 0; i < 3 && ok; i++) {
+    if (i == fk) continue;
+    if (fabs(a[i]) > MINVAL) {
+      double t0 = (-h[i] - c[i]) / a[i], t1 = (h[i] - c[i]) / a[i];
+      if (t0 > t1) { double t = t0; t0 = t1; t1 = t; }
+      lo = t0 > lo ? t0 : lo;
+      hi = t1 < hi ? t1 : hi;
+    } else if (fabs(c[i]) > h[i]) {
+      ok = 0;
     }
   }
-  double ts = 0.5 * (lo + hi);
-  for (int k = 0; k < 3; k++) p[k] = al[k] + ts * (bl[k] - al[k]);
-  double fs = box_sd(p, h, e);
-  double f0 = box_sd(al, h, e), f1e = box_sd(bl, h, e);
-  int n = 0;
-  double cw[3];
-  if (f0 - r <= margin) n += sphere_box_core(a, r, bp, bm, h, margin, out + n);
-  if (f1e - r <= margin) n += sphere_box_core(b, r, bp, bm, h, margin, out + n);
-  if (ts > 0.02 && ts < 0.98 && fs - r <= margin && fs < (f0 < f1e ? f0 : f1e) - 0.01 * r) {
-    for (int k = 0; k < 3; k++) cw[k] = a[k] + ts * (b[k] - a[k]);
-    n += sphere_box_core(cw, r, bp, bm, h, margin, out + n);
+  if (ok && lo <= hi) {
+    double s2 = (s1 - lo < hi - s1) ? hi : lo;
+    if (fabs(s2 - s1) * hl >= 0.1 * r) {
+      for (int k = 0; k < 3; k++) { pl[k] = c[k] + s2 * a[k]; w[k] = cp[k] + s2 * ax[k]; }
+      /* the far point must lie on the same face: one nonzero normal component, same axis and sign */
+      if (sphere_box_local(pl, w, r, bm, h, margin, e2, out + 1) && (e2[0] != 0) + (e2[1] != 0) + (e2[2] != 0) == 1 &&
+          e2[fk] * e[fk] > 0)
+        n = 2;
+    }
   }
+  g_np_stats[n - 1]++;
   return n;
+}
+
+/* mjraw_SphereSphere [ext]: coincident centres take the cross product of the geoms' z axes */
+static int sph_sph_raw(const double *c1, const double *m1, double r1, const double *c2, const double *m2, double r2,
+                       double margin, rcon *out) {
+  double dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  double dist = sqrt(dot3(dv, dv)) - r1 - r2;
+  if (dist > margin) return 0;
+  double L = normalize3(dv);
+  if (L < MINVAL) {
+    double z1[3] = {m1[2], m1[5], m1[8]}, z2[3] = {m2[2], m2[5], m2[8]};
+    cross3(dv, z1, z2);
+    normalize3(dv);
+  }
+  out->dist = dist;
+  for (int k = 0; k < 3; k++) { out->n[k] = dv[k]; out->pos[k] = c1[k] + dv[k] * (r1 + 0.5 * dist); }
+  return 1;
+}
+
+/* mjc_CapsuleCapsule [ext]: centre + half-axis form, MuJoCo's clamping sequence; parallel axes
+ * (|det| < mjMINVAL): axis ends x1 = +-1 then x2 = +-1, stopping at two contacts */
+static int capsule_capsule(const double *p1, const double *m1, const double *s1, const double *p2, const double *m2,
+                           const double *s2, double margin, rcon *out) {
+  double a1[3] = {m1[2] * s1[1], m1[5] * s1[1], m1[8] * s1[1]};
+  double a2[3] = {m2[2] * s2[1], m2[5] * s2[1], m2[8] * s2[1]};
+  double dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  double ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+  double u = -dot3(a1, dif), v = dot3(a2, dif);
+  double det = ma * mc - mb * mb, v1[3], v2[3];
+  if (fabs(det) >= MINVAL) {
+    double x1 = (mc * u - mb * v) / det, x2 = (ma * v - mb * u) / det;
+    if (x1 > 1) { x1 = 1; x2 = (v - mb) / mc; }
+    else if (x1 < -1) { x1 = -1; x2 = (v + mb) / mc; }
+    if (x2 > 1) { x2 = 1; x1 = clampd((u - mb) / ma, -1, 1); }
+    else if (x2 < -1) { x2 = -1; x1 = clampd((u + mb) / ma, -1, 1); }
+    for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+    g_np_stats[2]++;
+    return sph_sph_raw(v1, m1, s1[0], v2, m2, s2[0], margin, out);
+  }
+  int n = 0;
+  for (int e = 0; e < 4 && n < 2; e++) {
+    double sg = (e & 1) ? -1 : 1;
+    if (e < 2) {
+      double x2 = clampd((v - sg * mb) / mc, -1, 1);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + sg * a1[k]; v2[k] = p2[k] + a2[k] * x2; }
+    } else {
+      double x1 = clampd((u - sg * mb) / ma, -1, 1);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + sg * a2[k]; }
+    }
+    n += sph_sph_raw(v1, m1, s1[0], v2, m2, s2[0], margin, out + n);
+  }
+  g_np_stats[3]++;
+  g_np_stats[4] += n;
+  return n;
+}
+
+/* mjc_SphereCapsule [ext]: the sphere centre projected on the axis, clamped to the half-length */
+static int sphere_capsule(const double *p1, const double *m1, const double *s1, const double *p2, const double *m2,
+                          const double *s2, double margin, rcon *out) {
+  double ax[3] = {m2[2], m2[5], m2[8]}, dv[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  double x = clampd(dot3(ax, dv), -s2[1], s2[1]);
+  double q[3] = {p2[0] + ax[0] * x, p2[1] + ax[1] * x, p2[2] + ax[2] * x};
+  return sph_sph_raw(p1, m1, s1[0], q, m2, s2[0], margin, out);
 }
 
 /* ---- cylinders (bipedal_rescue: sphere/capsule/box vs static cylinders) [ext]
@@ -942,26 +1073,16 @@ static int collide_geoms(const mgx_model_desc *m, ref_data *d, int g1, int g2, d
     double dv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
     if (norm3(dv) > m->geom_rbound[g1] + m->geom_rbound[g2] + margin) return 0;
   }
-  if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph(p1, s1[0], p2, s2[0], margin, out);
-  if (t1 == GSPHERE && t2 == GCAPSULE) {
-    double a[3], b[3], q[3];
-    seg_ends(p2, m2, s2[1], a, b);
-    double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p1[0] - a[0], p1[1] - a[1], p1[2] - a[2]};
-    double L2 = dot3(ab, ab), t = L2 > MINVAL ? clampd(dot3(ap, ab) / L2, 0, 1) : 0;
-    for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k];
-    return sph_sph(p1, s1[0], q, s2[0], margin, out);
-  }
-  if (t1 == GCAPSULE && t2 == GCAPSULE) {
-    double a1[3], b1[3], a2[3], b2[3], s, t, P[3], Q[3];
-    seg_ends(p1, m1, s1[1], a1, b1);
-    seg_ends(p2, m2, s2[1], a2, b2);
-    seg_seg(a1, b1, a2, b2, &s, &t);
-    for (int k = 0; k < 3; k++) { P[k] = a1[k] + s * (b1[k] - a1[k]); Q[k] = a2[k] + t * (b2[k] - a2[k]); }
-    return sph_sph(P, s1[0], Q, s2[0], margin, out);
-  }
+  if (t1 == GSPHERE && t2 == GSPHERE) return sph_sph_raw(p1, m1, s1[0], p2, m2, s2[0], margin, out);
+  if (t1 == GSPHERE && t2 == GCAPSULE) return sphere_capsule(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GCAPSULE && t2 == GCAPSULE) return capsule_capsule(p1, m1, s1, p2, m2, s2, margin, out);
   if (t1 == GSPHERE && t2 == GBOX) return sphere_box_core(p1, s1[0], p2, m2, s2, margin, out);
   if (t1 == GCAPSULE && t2 == GBOX) return capsule_box(p1, m1, s1, p2, m2, s2, margin, out);
-  if (t1 == GBOX && t2 == GBOX) return box_box(p1, m1, s1, p2, m2, s2, margin, out);
+  if (t1 == GBOX && t2 == GBOX) {
+    int n = box_box(p1, m1, s1, p2, m2, s2, margin, out);
+    g_np_stats[5 + n]++;
+    return n;
+  }
   if (t1 == GPLANE && t2 == GSPHERE) return plane_sphere(p1, m1, p2, s2[0], margin, out);
   if (t1 == GPLANE && t2 == GCAPSULE) {
     double a[3], b[3];
@@ -1330,7 +1451,7 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
   double c0 = newton_cost(m, d, d->qacc_smooth, M, x, NULL);
   double cw = newton_cost(m, d, d->qacc_warmstart, M, x, NULL);
   memcpy(a, cw < c0 ? d->qacc_warmstart : d->qacc_smooth, sizeof(double) * nv);
-  double cost = newton_cost(m, d, a, M, x, g);
+  newton_cost(m, d, a, M, x, g);
   int iter = 0;
   /* mj_solNewton's loop order [ext]: every iteration updates, then tests the scaled improvement
      and the scaled gradient at the new point, so at least one iteration always runs */
@@ -1382,27 +1503,60 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
       for (int k = 0; k < nv; k++) s += J[k] * p[k];
       jp[r] = s;
     }
-    double al = 1, lo = 0, hi = 1e300;
-    for (int ls = 0; ls < 50; ls++) {
-      double d1 = g0 + al * pMp, d2 = pMp;
-      for (int r = 0; r < ne; r++) {
-        double xr = x[r] + al * jp[r];
-        if (xr < 0) {
+    /* line search, MuJoCo's stop rule [ext]: the cost along p is convex piecewise quadratic; the
+       first point is the Newton step from alpha = 0, then safeguarded Newton steps inside the
+       bracket [lo, hi] (bisection when a step leaves it) until |f'(alpha)| < gtol =
+       tolerance * ls_tolerance * |p| * meaninertia * max(1, nv), at most ls_iterations = 50
+       evaluations (MuJoCo defaults ls_tolerance 0.01, ls_iterations 50; no model sets them) */
+    double snorm = 0;
+    for (int k = 0; k < nv; k++) snorm += p[k] * p[k];
+    snorm = sqrt(snorm);
+    double al = 0;
+    if (snorm >= MINVAL) {
+      const double gtol = m->tolerance * LS_TOLERANCE * snorm * m->meaninertia * (nv > 1 ? nv : 1);
+      double d1 = g0, d2 = pMp;
+      for (int r = 0; r < ne; r++)
+        if (x[r] < 0) {
           double Dr = 1 / d->efc_R[r];
-          d1 += Dr * xr * jp[r];
+          d1 += Dr * x[r] * jp[r];
           d2 += Dr * jp[r] * jp[r];
         }
+      al = -d1 / d2;
+      double lo = 0, hi = 1e300;
+      for (int ls = 0; ls < LS_ITERATIONS; ls++) {
+        d1 = g0 + al * pMp;
+        d2 = pMp;
+        for (int r = 0; r < ne; r++) {
+          double xr = x[r] + al * jp[r];
+          if (xr < 0) {
+            double Dr = 1 / d->efc_R[r];
+            d1 += Dr * xr * jp[r];
+            d2 += Dr * jp[r] * jp[r];
+          }
+        }
+        if (fabs(d1) < gtol) break;
+        if (d1 < 0) lo = al; else hi = al;
+        double nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
+        if (!(nxt > lo && nxt < hi)) nxt = hi < 1e300 ? 0.5 * (lo + hi) : 2 * al;
+        const int stall = fabs(nxt - al) <= 1e-15 * (1 + fabs(al));  /* no change in floating point */
+        al = nxt;
+        if (stall) break;
       }
-      if (d1 < 0) lo = al; else hi = al;
-      double nxt = d2 > 0 ? al - d1 / d2 : 2 * al;
-      if (!(nxt > lo && nxt < hi)) nxt = hi < 1e300 ? 0.5 * (lo + hi) : 2 * al;
-      if (fabs(nxt - al) <= 1e-15 * (1 + fabs(al))) { al = nxt; break; }
-      al = nxt;
+    }
+    /* the improvement cost(old) - cost(new) evaluated term by term along the step (the Gauss
+       term al g0 + al^2 pMp / 2 and each row's change of s_r): algebraically MuJoCo's
+       difference of totals, which at ~1e10 costs (construction states) rounds to 0 or a few
+       ulps and would let rounding decide the stop test; the device evaluates the same terms */
+    double dec = al * g0 + 0.5 * al * al * pMp;
+    for (int r = 0; r < ne; r++) {
+      const double xo = x[r], xn = x[r] + al * jp[r], Dr = 1 / d->efc_R[r];
+      if (xo < 0 && xn < 0) dec += 0.5 * Dr * (al * jp[r]) * (xo + xn);
+      else if (xo < 0) dec -= 0.5 * Dr * xo * xo;
+      else if (xn < 0) dec += 0.5 * Dr * xn * xn;
     }
     for (int k = 0; k < nv; k++) a[k] += al * p[k];
-    double cnew = newton_cost(m, d, a, M, x, g);
-    double improvement = scale * (cost - cnew);
-    cost = cnew;
+    newton_cost(m, d, a, M, x, g);
+    double improvement = -scale * dec;
     iter++;
     double gn = 0;
     for (int k = 0; k < nv; k++) gn += g[k] * g[k];

@@ -40,7 +40,19 @@ def lib():
         _lib.ref_field.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_int)]
         _lib.ref_collide_pair.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         _lib.ref_collide_pair.restype = C.c_int
+        _lib.ref_narrowphase_stats.argtypes = [C.POINTER(C.c_long), C.c_int]
     return _lib
+
+
+NP_STATS = ("capsule_box_1", "capsule_box_2", "capsule_capsule", "capsule_capsule_parallel",
+            "capsule_capsule_parallel_contacts") + tuple(f"box_box_{k}" for k in range(9))
+
+
+def narrowphase_stats(reset: bool = False) -> dict:
+    """Process-wide narrowphase branch counters of the oracle (mjref.c g_np_stats)."""
+    buf = (C.c_long * 16)()
+    lib().ref_narrowphase_stats(buf, 1 if reset else 0)
+    return dict(zip(NP_STATS, list(buf)[:len(NP_STATS)]))
 
 
 class RefSim:

@@ -1,0 +1,249 @@
+"""GPU: humanoid_construction on the wide kernels (nv 99: two dofs per lane, RK4 + Newton) against
+the reference golden vectors and the CPU oracle (mjref physics with its Newton solver + RK4, and
+oracle/construction_logic.py).
+
+Bars:
+  logic kernel fp64 — obs, reward (the np.float32 value), flags, ctrl, step counter, progress,
+      tasks_completed and the float32 running total bit-exact against the reference's own step()
+      outputs (tests/golden/construction_envlogic.npz); reset obs bit-exact against its reset()
+      (construction_reset.npz), seeded and unseeded;
+  forward stages fp64 — kinematics / inertia 1e-10, identical contact list and rows, A = B B' + R
+      1e-7 relative, Newton forces and qacc 1e-6 relative, on oracle states;
+  step fp64 — 5 RK4 steps from oracle states: 1e-7 / 1e-6 relative on well-conditioned states,
+      20 x the oracle's own 1e-13-perturbation spread on the others;
+  end to end fp64 — seeded reset + 30 random-action RK4 steps: full qpos / qvel 1e-8 relative to
+      max(1, |x|), obs 1e-6 absolute + 1e-6 relative, reward 1e-6 relative, flags identical.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import load_states, oracle_at, oracle_states
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dtype, dev="cuda:0"):
+    return torch.as_tensor(np.ascontiguousarray(x)).to(device=dev, dtype=dtype).contiguous()
+
+
+@pytest.fixture(scope="module")
+def cmodel():
+    from mujoco_gymnasium_environments_amd.envs.construction import construction_model
+    return construction_model()
+
+
+@pytest.fixture(scope="module")
+def cpacked(cmodel):
+    from mujoco_gymnasium_environments_amd import cabi
+    return cabi.pack_model(cmodel)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_construction_logic_kernel_matches_reference(cmodel, prec):
+    from mujoco_gymnasium_environments_amd import cabi
+    from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
+    from mujoco_gymnasium_environments_amd.native import check, lib
+    g = dict(np.load("tests/golden/construction_envlogic.npz"))
+    n = g["obs"].shape[0]
+    m = cmodel
+    env = ConstructionVectorEnv(n, precision=prec, autoreset=False)
+    dt = env.batch.dtype
+    env.scal.copy_(_t(np.concatenate([g["progress_in"][:, None], g["weather"]], 1), torch.float64))
+    env.ints.copy_(_t(np.stack([g["task"], g["step_in"], g["blocks"], g["violations"], g["completed_in"]], 1),
+                      torch.int32))
+    env.total_reward.copy_(_t(g["total_in"].astype(np.float32), torch.float32))
+    hid = env.tables.humanoid
+    xpos = np.zeros((n, m.nbody, 3))
+    xpos[:, hid, 2] = g["torso_z"]
+    T = dict(qpos=_t(g["qpos"], dt), qvel=_t(g["qvel"], dt), xpos=_t(xpos, dt),
+             ctrl=torch.zeros(n, m.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float32),
+             obs=torch.zeros(n, 135, dtype=torch.float32, device="cuda:0"),
+             reward=torch.zeros(n, dtype=torch.float64, device="cuda:0"),
+             term=torch.zeros(n, dtype=torch.uint8, device="cuda:0"),
+             trunc=torch.zeros(n, dtype=torch.uint8, device="cuda:0"))
+    io = cabi.MgxConstructionLogicIO(*[T[k].data_ptr() for k in ("qpos", "qvel", "xpos", "ctrl", "action", "obs",
+                                                                  "reward", "term", "trunc")])
+    check(lib().mgx_construction_logic_test(env.native.handle, C.byref(io), C.byref(env._env), n, None), "logic")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(T["term"].cpu().numpy().astype(bool), g["terminated"])
+    np.testing.assert_array_equal(T["trunc"].cpu().numpy().astype(bool), g["truncated"])
+    ints, scal = env.ints.cpu().numpy(), env.scal.cpu().numpy()
+    np.testing.assert_array_equal(ints[:, 1], g["step_out"])
+    np.testing.assert_array_equal(ints[:, 4], g["completed_out"])
+    np.testing.assert_array_equal(scal[:, 0], g["progress_out"])
+    np.testing.assert_array_equal(env.total_reward.cpu().numpy().astype(np.float64), g["total_out"])
+    np.testing.assert_array_equal(T["reward"].cpu().numpy(), g["reward"])
+    if prec == "f64":
+        np.testing.assert_array_equal(T["obs"].cpu().numpy(), g["obs"])
+        np.testing.assert_array_equal(T["ctrl"].cpu().numpy(), g["ctrl"])
+    else:  # qpos / qvel pass through the fp32 state: one fp32 rounding
+        np.testing.assert_allclose(T["obs"].cpu().numpy(), g["obs"], rtol=1e-6, atol=1e-6)
+
+
+def test_construction_reset_matches_reference():
+    """HumanoidConstructionEnv.reset(seed) then an unseeded reset: task + weather draws from
+    gymnasium's PCG64 stream, observation of qpos0 (quirk C4), bit for bit."""
+    from mujoco_gymnasium_environments_amd.envs.construction import HumanoidConstructionEnv
+    g = dict(np.load("tests/golden/construction_reset.npz"))
+    env = HumanoidConstructionEnv(precision="f64")
+    for i, seed in enumerate(g["seeds"]):
+        o1, info = env.reset(seed=int(seed))
+        assert info["task"] == ('stack_blocks', 'operate_crane', 'transport_material', 'build_structure')[int(g["task"][i])]
+        np.testing.assert_array_equal(o1, g["obs"][i], err_msg=f"seed {seed}")
+        o2, _ = env.reset()
+        np.testing.assert_array_equal(o2, g["obs2"][i], err_msg=f"seed {seed} unseeded")
+
+
+def test_wide_forward_stages_match_oracle(cmodel, cpacked):
+    """One forward pass of the wide kernels (mgx_debug_forward) on oracle states: every stage."""
+    from mujoco_gymnasium_environments_amd.batch import PhysicsBatch
+    m = cmodel
+    states = oracle_states(cpacked, 6, seed=3, max_steps=40, action_scale=100.0)
+    b = PhysicsBatch(m, len(states), precision="f64")
+    load_states(b, states)
+    dbg = b.debug_forward()
+    for i, st in enumerate(states):
+        o = oracle_at(cpacked, st)
+        o.forward()
+        np.testing.assert_allclose(dbg["xpos"][i], o.xpos, atol=1e-10, err_msg=f"xpos env {i}")
+        np.testing.assert_allclose(dbg["subtree_com"][i], o.subtree_com, atol=1e-10)
+        np.testing.assert_allclose(dbg["cdof"][i], o.cdof, atol=1e-9)
+        assert np.max(np.abs(dbg["qM"][i] - o.qM)) / max(1, np.abs(o.qM).max()) < 1e-9, "qM"
+        assert np.max(np.abs(dbg["qLD"][i] - o.qLD)) / max(1, np.abs(o.qLD).max()) < 1e-8, "qLD"
+        nc = int(o.ncon[0])
+        assert int(dbg["ncon"][i][0]) == nc, (i, dbg["ncon"][i][0], nc)
+        np.testing.assert_array_equal(dbg["con_geom"][i][:2 * nc].astype(int), o.con_geom[:2 * nc])
+        np.testing.assert_allclose(dbg["con_dist"][i][:nc], o.con_dist[:nc], atol=1e-8)
+        ne = int(o.nefc[0])
+        assert int(dbg["nefc"][i][0]) == ne
+        np.testing.assert_array_equal(dbg["efc_type"][i][:ne].astype(int), o.efc_type[:ne])
+        np.testing.assert_array_equal(dbg["efc_id"][i][:ne].astype(int), o.efc_id[:ne])
+        B = dbg["Bmat"][i][:ne * m.nv].reshape(ne, m.nv)
+        A = B @ B.T + np.diag(dbg["efc_R"][i][:ne])
+        Ao = o.efc_AR[:ne * ne].reshape(ne, ne)
+        assert np.max(np.abs(A - Ao)) / max(1, np.abs(Ao).max()) < 1e-7, "efc_AR"
+        rel = lambda a, b: np.max(np.abs(a - b)) / max(1.0, np.max(np.abs(b)))  # noqa: E731
+        assert rel(dbg["qfrc_smooth"][i], o.qfrc_smooth) < 1e-8, "qfrc_smooth"
+        assert rel(dbg["qacc_smooth"][i], o.qacc_smooth) < 1e-7, "qacc_smooth"
+        assert rel(dbg["efc_force"][i][:ne], o.efc_force[:ne]) < 1e-6, ("efc_force", i)
+        assert rel(dbg["qacc"][i], o.qacc) < 1e-6, ("qacc", i)
+
+
+def _spread(cpacked, st, nsteps, eps=1e-13, reps=2):
+    """The oracle's own sensitivity: the largest change of qpos / qvel (relative to max(1, |x|))
+    after nsteps when every qpos entry is perturbed by eps x N(0, 1). Construction states with
+    steel beams deep in the floor and the crane foundation held by friction alone reach
+    ~1e-3 under a 1e-13 perturbation; no two fp64 implementations agree better than that there."""
+    base = oracle_at(cpacked, st)
+    base.step(nsteps)
+    rng = np.random.default_rng(0)
+    worst = 0.0
+    for _ in range(reps):
+        st2 = {k: v.copy() for k, v in st.items()}
+        st2["qpos"] = st2["qpos"] + rng.normal(size=st2["qpos"].shape) * eps
+        o = oracle_at(cpacked, st2)
+        o.step(nsteps)
+        for a, b in ((o.qpos, base.qpos), (o.qvel, base.qvel)):
+            worst = max(worst, float(np.max(np.abs(a - b) / np.maximum(1, np.abs(b)))))
+    return base, worst
+
+
+def test_wide_step_matches_oracle(cmodel, cpacked):
+    """mgx_step on the wide model (RK4 + Newton, 5 steps from oracle states) vs the oracle: 1e-7
+    (qpos) / 1e-6 (qvel) relative on well-conditioned states; on states where the oracle itself
+    moves by more than 1e-8 under a 1e-13 input perturbation, within 20 x that spread."""
+    from mujoco_gymnasium_environments_amd.batch import PhysicsBatch
+    states = oracle_states(cpacked, 8, seed=4, max_steps=40, action_scale=100.0)
+    b = PhysicsBatch(cmodel, len(states), precision="f64")
+    load_states(b, states)
+    b.step(nsub=5)
+    torch.cuda.synchronize()
+    qg, vg = b.qpos.cpu().numpy(), b.qvel.cpu().numpy()
+    good = 0
+    for i, st in enumerate(states):
+        o, spread = _spread(cpacked, st, 5)
+        e_q = np.max(np.abs(qg[i] - o.qpos) / np.maximum(1, np.abs(o.qpos)))
+        e_v = np.max(np.abs(vg[i] - o.qvel) / np.maximum(1, np.abs(o.qvel)))
+        if spread < 1e-8:
+            good += 1
+            assert e_q < 1e-7 and e_v < 1e-6, (i, e_q, e_v)
+        else:
+            assert max(e_q, e_v) < 20 * spread + 1e-6, (i, e_q, e_v, spread)
+    assert good >= 4, good
+
+
+def test_construction_end_to_end_f64(cmodel, cpacked):
+    """Seeded reset (host draws) + 30 random-action steps of the fp64 VectorEnv vs mjref + the
+    logic oracle, every env on every step: state 1e-8 relative (measured <= 1e-11), obs 1e-6,
+    reward 1e-6 relative, flags exact. qpos0 puts 11 humanoid hinges exactly on a range end
+    (range 0..1.5 etc.), so a perturbed copy of the oracle is no sensitivity measure here (any
+    perturbation moves them across the limit); the device and the oracle both start on the
+    boundary and leave it the same way."""
+    from mujoco_gymnasium_environments_amd.envs.construction import ConstructionTables, ConstructionVectorEnv
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.construction_logic import ConstructionLogic
+    from oracle.mjref import RefSim
+    m = cmodel
+    n = 6
+    env = ConstructionVectorEnv(n, precision="f64", autoreset=False)
+    tb = ConstructionTables(m)
+    L = ConstructionLogic(tb.humanoid, m.nu)
+    rngs = [np_random(70 + i)[0] for i in range(n)]
+    draws = np.stack([tb.reset_draws(np_random(70 + i)[0]) for i in range(n)])
+    obs, _ = env.reset(draws=draws)
+    torch.cuda.synchronize()
+    sims, states = [], []
+    for i in range(n):
+        s = L.reset(rngs[i])
+        sim = RefSim(cpacked)
+        sim.reset()
+        sims.append(sim)
+        states.append(s)
+        np.testing.assert_array_equal(obs[i].cpu().numpy(), L.observation(s, sim.qpos, sim.qvel), err_msg=f"reset {i}")
+    rng = np.random.default_rng(9)
+    worst = 0.0
+    for t in range(30):
+        act = rng.uniform(-200, 200, (n, m.nu)).astype(np.float32)
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        og, rg, tg, trg = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy()
+        qg, vg = env.batch.qpos.cpu().numpy(), env.batch.qvel.cpu().numpy()
+        for i in range(n):
+            a = L.pre(act[i])
+            sims[i].ctrl[:] = a
+            sims[i].step()
+            o, r, te, tr = L.post(states[i], a, sims[i].qpos, sims[i].qvel, sims[i].xpos.reshape(-1, 3))
+            eq = np.max(np.abs(qg[i] - sims[i].qpos) / np.maximum(1, np.abs(sims[i].qpos)))
+            ev = np.max(np.abs(vg[i] - sims[i].qvel) / np.maximum(1, np.abs(sims[i].qvel)))
+            worst = max(worst, eq, ev)
+            assert eq < 1e-8 and ev < 1e-8, (t, i, eq, ev)
+            np.testing.assert_allclose(og[i], o, rtol=1e-6, atol=1e-6, err_msg=f"step {t} env {i}")
+            assert abs(rg[i] - float(r)) <= 1e-6 * max(1.0, abs(float(r))), (t, i, rg[i], r)
+            assert bool(tg[i]) == te and bool(trg[i]) == tr, (t, i)
+    print(f"\nconstruction fp64 end to end: worst state error {worst:.3g}")
+    assert int(env.batch.overflow.sum()) == 0
+
+
+def test_construction_autoreset_and_sharding_invariance(cmodel):
+    """Device reset draws are keyed by global env index: a 2-env shard at offset 2 reproduces
+    envs 2..3 of a 4-env run bit for bit, including same-step autoresets (a short episode limit
+    forces them)."""
+    from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
+    full = ConstructionVectorEnv(4, seed=5, max_episode_steps=7)
+    part = ConstructionVectorEnv(2, seed=5, env_offset=2, max_episode_steps=7)
+    full.reset()
+    part.reset()
+    rng = np.random.default_rng(1)
+    ends = 0
+    for t in range(20):
+        a = torch.from_numpy(rng.uniform(-200, 200, (4, cmodel.nu)).astype(np.float32)).cuda()
+        of, rf, tf, trf, _ = full.step(a)
+        op, rp, tp, _, _ = part.step(a[2:].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(of[2:], op) and torch.equal(rf[2:], rp) and torch.equal(tf[2:], tp), t
+        ends += int((tf | trf).sum())
+    assert ends > 0
+    assert torch.equal(full.episode[2:], part.episode)

@@ -51,3 +51,4 @@ def test_registry_matches_reference_registrations():
     assert REGISTRY['BipedalRescue-v0'][1] == 10000
     assert REGISTRY['HumanoidDancing-v0'][1] == 3600
     assert REGISTRY['RoboticArmAssembly-v0'][1] == 150000
+    assert REGISTRY['HumanoidConstruction-v0'][1] == 3000
