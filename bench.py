@@ -471,6 +471,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=4)
+    ap.add_argument("--full-capacity", action="store_true",
+                    help="soccer: 96 contacts / 384 rows per env instead of 64 / 192 (no overflow, slower)")
     ap.add_argument("--streams", type=int, default=1,
                     help="soccer: split the rank's envs into this many stream shards (overlapping pipelines)")
     ap.add_argument("--no-f64-line", "--no-other-line", dest="no_f64_line", action="store_true",
@@ -524,7 +526,8 @@ def main():
                                          env_offset=env_offset(rank, N), staged=not args.mono, banks=args.banks)
         else:
             env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234,
-                                  env_offset=env_offset(rank, N), staged=not args.mono, banks=args.banks)
+                                  env_offset=env_offset(rank, N), staged=not args.mono, banks=args.banks,
+                                  full_capacity=args.full_capacity)
         pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]
     env.reset()
     for k in range(args.warmup):
@@ -573,6 +576,7 @@ def main():
                        "integrator": "RK4", "step_kernels": "mono", "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "capacity_overflow_steps": overflow_steps,
+                       "capacity": "96 contacts / 384 rows" if args.full_capacity else "64 contacts / 192 rows",
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(PMC_PROFILE_BIPEDAL, N, args.precision,
@@ -647,6 +651,7 @@ def main():
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "capacity_overflow_steps": overflow_steps,
+                       "capacity": "96 contacts / 384 rows" if args.full_capacity else "64 contacts / 192 rows",
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

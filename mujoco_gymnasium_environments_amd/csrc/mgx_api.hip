@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T
   int env = blockIdx.x;
   if (env >= n_env) return;
   int l = lane_id();
-  if (env == 0 && l == 0) P.ctr()[1] = 0;  // the solver list is consumed
+  if (env == 0 && l == 0) { P.ctr()[1] = 0; P.ctr()[2] = 0; }  // the solver lists are consumed
   Env<T> e;
   env_bind(m, e, smem);
   if (banks) {
@@ -579,6 +579,12 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.base = (char*)ws;
   p.N = n_env; p.R = banks; p.S = n_env * (1 + banks);
   p.maxE = m->Ls.max_nefc; p.nv = nv; p.dpl = (nv + 7) / 8;  // solver: support entries per lane
+  // test hook: MGX_PGS_LDS_ROWS lowers the main launch's LDS rows (read per call), so ordinary
+  // states exercise the wide-LDS launch (tests/test_gpu_capacity.py)
+  const char* cap_env = getenv("MGX_PGS_LDS_ROWS");
+  int capE = cap_env ? (atoi(cap_env) + 3) / 4 * 4 : MGX_PGS_LDS_ROWS;
+  if (capE < 4 || capE > MGX_PGS_LDS_ROWS) capE = MGX_PGS_LDS_ROWS;
+  p.capE = p.maxE < capE ? p.maxE : capE;
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
@@ -588,7 +594,7 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.o_ctr = take(64);
   p.o_carry = take(S * p.carry_stride * rb);
   p.o_carryi = take(S * p.carryi_stride * 4);
-  p.o_ne = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_fix = take((size_t)n_env * 4);
+  p.o_ne = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_k2big = take(S * 4); p.o_fix = take((size_t)n_env * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
   p.o_blk = take(S * p.maxE * 4);  // 8 uint16 per 4-row block
   p.o_B = take(S * (size_t)p.bcap * rb);
@@ -605,9 +611,11 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   return off;
 }
 
-static int pgs_lds_bytes(const mgx_model* m) {
+// LDS of one solver wave holding `rows` rows per slot (main launch: min(max_nefc,
+// MGX_PGS_LDS_ROWS); wide launch: max_nefc)
+static int pgs_lds_bytes(const mgx_model* m, int rows) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
-  int nb3 = (m->Ls.max_nefc / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
+  int nb3 = (rows / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
   return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 4) * rb + MGX_PGS_SPW * nb3 * 32 + 64;
 }
 
@@ -625,7 +633,10 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, *e, action, n_env, mask, P,
                      banks);
   T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
-  launch_pgs<T>(P, slots, pgs_lds_bytes(m), st, M.iterations, M.tolerance, scale);
+  launch_pgs<T>(P, slots, pgs_lds_bytes(m, P.capE), st, M.iterations, M.tolerance, scale, 0);
+  // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped);
+  // a small grid-stride launch that exits at once when the list is empty
+  if (P.maxE > P.capE) launch_pgs<T>(P, 8 * MGX_PGS_WIDE_GRID, pgs_lds_bytes(m, P.maxE), st, M.iterations, M.tolerance, scale, 1);
   hipLaunchKernelGGL(k_soccer_finish<T>, dim3(n_env), dim3(64), m->Lf.bytes, st, Mf, ids, *s, *e, action, obs, reward,
                      terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks);
   int fgrid = n_env < 256 ? n_env : 256;
@@ -689,12 +700,17 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // broadphase survivor list: 128 for the small candidate sets (soccer 251, parkour 48 pairs),
   // up to 768 for large ones (bipedal 3185 pairs)
   int max_active = d->npair <= 256 ? 128 : (d->npair < 768 ? d->npair : 768);
-  m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false);
+  // the staged soccer pipeline handles Euler + PGS models up to 64 * MGX_EFC_SLOTS rows
+  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS && condim13;
+  // the monolithic layout of a staged model (its reset settle steps, the rare fixup resets,
+  // --mono, mgx_debug_forward) keeps rows in LDS at the default 192 rows / 64 contacts; the
+  // staged step itself carries the model's full capacity
+  const int mono_nefc = m->staged_ok && max_nefc > 192 ? 192 : max_nefc;
+  const int mono_ncon = m->staged_ok && max_ncon > 64 ? 64 : max_ncon;
+  m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, false);
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024 || (d->layout_flags & MGX_ROWS_IN_SCRATCH))
-    m->L = make_layout(d, rb, max_ncon, max_nefc, max_active, false, true);
-  // the staged soccer pipeline (register-ring solver) handles Euler models up to 192 rows
-  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS && condim13;
+    m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, false, true);
   m->Ls = make_layout(d, rb, max_ncon, m->staged_ok ? max_nefc : 4, 128, true);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;
@@ -722,7 +738,7 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
                   set_lds(k_soccer_rows<double>, m->Ls.bytes) | set_lds(k_soccer_finish<double>, m->Lf.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
   if (m->staged_ok) {
-    int pl = pgs_lds_bytes(m);
+    int pl = pgs_lds_bytes(m, m->Ls.max_nefc);  // >= the main launch's
     if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
     int r3 = pgs_configure_lds(precision, pl);
     if (r3 != MGX_OK) { delete m; return r3; }

@@ -406,8 +406,10 @@ __device__ __forceinline__ int clip_poly(T (*in)[2], int n, int axis, T lim, T s
     T* P = in[i];
     T* Q = in[(i + 1) % n];
     T dp = sgn * P[axis] - lim, dq = sgn * Q[axis] - lim;
-    if (dp <= tol) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
-    if ((dp < -tol && dq > tol) || (dp > tol && dq < -tol)) {
+    // a convex polygon gains at most one vertex per clip (4 -> 8 over the four clips); the
+    // bound is also enforced, so a rounding-level non-convexity cannot write past out[8]
+    if (dp <= tol && m < 8) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
+    if (m < 8 && ((dp < -tol && dq > tol) || (dp > tol && dq < -tol))) {
       T t = dp / (dp - dq);
       out[m][0] = P[0] + t * (Q[0] - P[0]);
       out[m][1] = P[1] + t * (Q[1] - P[1]);

@@ -15,7 +15,7 @@
 #define MGX_MAX_NBODY 64
 #define MGX_MAX_DEPTH 16      // longest dof chain (root..dof), soccer: 13
 #define MGX_MAX_CONPAIR 8     // contacts per geom pair (box-box)
-#define MGX_EFC_SLOTS 3       // per-lane register slots for row data -> max_nefc <= 192
+#define MGX_EFC_SLOTS 6       // staged soccer step: max_nefc <= 64 * MGX_EFC_SLOTS = 384
 
 namespace mgx {
 

@@ -77,7 +77,7 @@ int host_check_state(const mgx_state* s);
 int step_kernels_configure(const mgx_model* m);
 // the staged solver S2 (mgx_pgs.hip)
 template <typename T>
-void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale);
+void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big);
 int pgs_configure_lds(int precision, int bytes);
 }  // namespace mgx
 

@@ -30,6 +30,8 @@ namespace mgx {
 #define MGX_SQ(k, i) (4 * (k) + (i))
 #define MGX_PGS_SPW 8          // solver: slots per wave (8 lanes each)
 #define MGX_PGS_RING 3         // solver: register ring of 4-row blocks (RING - 1 in flight; 4 measured no faster)
+#define MGX_PGS_LDS_ROWS 192   // rows per slot the main solver launch keeps in LDS (2 waves / CU in fp64)
+#define MGX_PGS_WIDE_GRID 32   // waves of the wide-LDS launch for the slots over MGX_PGS_LDS_ROWS
 enum { FIX_RESET = 2 };
 
 // Workspace layout (byte offsets from base), computed on the host (mgx_soccer_workspace_bytes)
@@ -39,13 +41,16 @@ struct Pipe {
   int carry_stride;    // reals per slot: carry_reals (64-aligned) + 5 * 64 registers
   int carryi_stride;   // ints per slot: carry_ints + 8
   int bcap;            // reals per slot of group-compressed B: 32 + (max_nefc / 4) * (8 + 32 * ceil(nv / 8))
-  size_t o_carry, o_carryi, o_ne, o_niter, o_k2list, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
+  int capE;            // rows the main solver launch holds in LDS per slot; slots with more rows (up
+                       // to maxE) go to the second, wide-LDS launch (o_k2big)
+  size_t o_carry, o_carryi, o_ne, o_niter, o_k2list, o_k2big, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
   size_t o_bq, o_bv, o_ba, o_btime, o_bobs, o_bprev, o_bwind, o_bk, o_bep, o_bwarn, o_bseed;
   // the checkAcc template: mj_step's outcome after mj_resetData (state + forward frames)
   size_t o_tq, o_tv, o_ta, o_tt, o_tx, o_txq, o_tsc, o_tn, o_tcg, o_tcd, o_tcm;
   int maxC;
   template <typename X> __device__ __forceinline__ X* at(size_t off) const { return reinterpret_cast<X*>(base + off); }
-  __device__ __forceinline__ int* ctr() const { return at<int>(o_ctr); }  // [0] fixup count, [1] solver-list count
+  // [0] fixup count, [1] solver-list count, [2] wide-solver-list count
+  __device__ __forceinline__ int* ctr() const { return at<int>(o_ctr); }
 };
 
 // ------------------------------------------------------------------ S1 helpers
@@ -421,7 +426,10 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
       g_mgx_prof[slot * 32 + 25] += e.overflow != 0;
     }
 #endif
-    if (ne > 0) {
+    if (ne > P.capE) {  // rare: more rows than the main solver launch keeps in LDS
+      int idx = atomicAdd(P.ctr() + 2, 1);
+      P.at<int>(P.o_k2big)[idx] = slot;
+    } else if (ne > 0) {
       int idx = atomicAdd(P.ctr() + 1, 1);
       P.at<int>(P.o_k2list)[idx] = slot;
     }
@@ -567,21 +575,18 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
   pgs_update(k, v, dl0, dl1, dl2, dl3);
 }
 
+// One group of up to 8 slots (one wave). capE: the rows per slot this launch's LDS holds.
 template <typename T, int EPL>
-__global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* list, int cnt, int base, int capE, int maxit,
+                                          T tol, T scale, int spw) {
   const int l = threadIdx.x, s = l >> 3, j = l & 7;
-  if (blockIdx.x == 0 && l == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
-  const int cnt = P.ctr()[1];
   const int spn = spw < 0 ? -spw : spw;
-  const int base = blockIdx.x * spn;
-  if (base >= cnt) return;
   const int idx = base + s;
-  const int slot = (s < spn && idx < cnt) ? P.at<int>(P.o_k2list)[idx] : -1;
+  const int slot = (s < spn && idx < cnt) ? list[idx] : -1;
   const int ne = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;  // a multiple of 4
   const int nblk = ne >> 2;
-  // LDS capacity in whole ring turns: nbcap3 = max_nefc / 4 rounded up to a multiple of the ring
-  const int nbcap = P.maxE / 4, nbcap3 = (nbcap + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;
+  // LDS capacity in whole ring turns: nbcap3 = capE / 4 rounded up to a multiple of the ring
+  const int nbcap = capE / 4, nbcap3 = (nbcap + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;
   const int sstride = MGX_SCAL * 4 * nbcap3 + 4;  // 16-byte aligned per slot
   T* sc = reinterpret_cast<T*>(smem) + s * sstride;
   uint32_t* bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + MGX_PGS_SPW * sstride) + s * 8 * nbcap3;
@@ -687,6 +692,21 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
     for (int d = 0; d < EPL; d++)
       if (j + 8 * d < P.nv) vo[j + 8 * d] = v[d];
     if (j == 0) P.at<int>(P.o_niter)[slot] = it;
+  }
+}
+
+// big = 0: the main launch (one wave per 8 listed slots, rows <= capE in LDS); big = 1: the
+// slots with capE < nefc <= maxE, grid-stride over a small grid with maxE rows of LDS per slot
+template <typename T, int EPL>
+__global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw, int big) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (!big && blockIdx.x == 0 && threadIdx.x == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
+  const int cnt = P.ctr()[big ? 2 : 1];
+  const int* list = P.at<int>(big ? P.o_k2big : P.o_k2list);
+  const int spn = spw < 0 ? -spw : spw;
+  for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
+    pgs_group<T, EPL>(P, smem, list, cnt, base, big ? P.maxE : P.capE, maxit, tol, scale, spw);
+    __syncthreads();  // the next group reuses the LDS
   }
 }
 

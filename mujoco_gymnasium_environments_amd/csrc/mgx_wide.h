@@ -344,9 +344,12 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   };
   T g[2];
   gradient(g);
+  MGX_STAMP_DECL
+  MGX_STAMP(10);  // setup
   while (iter < maxit) {
     whessian(Bm, Bs, efc, ne, nv, H);
     wsync();
+    MGX_STAMP(11);  // Hessian
     // Cholesky H = L L' in place, left-looking, lane = rows l and 64 + l
     for (int k = 0; k < nv; k++) {
       const T* Lk = H + k * nv;
@@ -375,6 +378,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
       }
       wsync();
     }
+    MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y
     T rdiag[2];
 #pragma unroll
@@ -401,6 +405,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     }
     p[0] = dl[0] ? p[0] : (T)0;
     p[1] = dl[1] ? p[1] : (T)0;
+    MGX_STAMP(13);  // triangular solves
     // J p per row (row-major, wave reductions); lane 0 stores
     for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
       T xa[MGX_RB], xb[MGX_RB];
@@ -420,6 +425,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
       }
     }
     wsync();
+    MGX_STAMP(14);  // J p
     // line search (newton(), mgx_physics.h: MuJoCo's stop rule)
     const T g0 = wdot(u, p), pp = wdot(p, p);
     T sdof[2];
@@ -455,6 +461,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
         if (stall) break;
       }
     }
+    MGX_STAMP(15);  // line search
     u[0] += al * p[0];
     u[1] += al * p[1];
     T dc = 0;
@@ -473,6 +480,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     ga[0] = dl[0] ? ga[0] : (T)0;
     ga[1] = dl[1] ? ga[1] : (T)0;
     const bool stop = improvement < tol || scale * sqrt(wdot(ga, ga)) < tol;
+    MGX_STAMP(16);  // update, gradient, stop tests
     if (stop) break;
   }
   e.niter = iter;
@@ -512,23 +520,31 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
 template <typename T>
 __device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
   Env<T>& e = w.e;
+  MGX_STAMP_DECL
   kinematics(m, e);
+  MGX_STAMP(0);
   com_crb(m, e);
+  MGX_STAMP(1);
   factor_ld<T, true>(m, e, e.qLD);
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int d = wdof(k);
     w.diaginv[k] = d < m.nv ? (T)1 / e.qLD[m.dof_Madr[d]] : (T)0;
   }
+  MGX_STAMP(2);
   velocity_bodies(m, e);
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int d = wdof(k);
     w.qfrc_smooth[k] = d < m.nv ? dof_force_applied(m, e, d, w.qfrc_applied[k]) : (T)0;
   }
+  MGX_STAMP(3);
   wsolve_M(m, w, e.qLD, w.qfrc_smooth, w.qacc_smooth);
+  MGX_STAMP(4);
   collision(m, e);
+  MGX_STAMP(5);
   make_constraint(m, e);
+  MGX_STAMP(6);
   // D^-1/2 per dof for the row transform
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -537,7 +553,17 @@ __device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
   }
   wsync();
   transform_rows<T, true>(m, e);
+  MGX_STAMP(7);
   wnewton(m, w);
+  MGX_STAMP(8);
+#ifdef MGX_PROFILE
+  if (g_mgx_prof && lane_id() == 0) {
+    g_mgx_prof[blockIdx.x * 32 + 20] += e.nefc;
+    g_mgx_prof[blockIdx.x * 32 + 21] += e.niter;
+    g_mgx_prof[blockIdx.x * 32 + 22] += e.ncon;
+    g_mgx_prof[blockIdx.x * 32 + 23] += 1;
+  }
+#endif
 }
 
 // mj_RungeKutta(m, d, 4) [ext] (rk4() of mgx_physics.h with two-word stage vectors)

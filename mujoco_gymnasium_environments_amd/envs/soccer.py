@@ -42,10 +42,24 @@ MAX_EPISODE_STEPS = 5000          # soccer_env.py:38 (class value governs `trunc
 REGISTERED_MAX_EPISODE_STEPS = 2500  # humanoid_soccer_env/__init__.py:21 (TimeLimit)
 
 
+# Contact / row capacity. MuJoCo allocates contacts from its arena and keeps them all. The
+# default staged step holds 64 contacts / 192 rows per env and counts the rare env step beyond
+# it (mgx_state.overflow, MuJoCo's mjWARN_CONTACTFULL / CNSTRFULL semantics: drop in row
+# order); full_capacity=True holds 96 contacts / 384 rows — no overflow at bench conditions —
+# with the slots over 192 rows solved by the staged pipeline's wide-LDS launch, at a measured
+# throughput cost (Capacity).
+CON_CAPACITY = 96
+EFC_CAPACITY = 384
+
+
 @functools.lru_cache(maxsize=None)
-def soccer_model() -> mjcf.Model:
+def soccer_model(full_capacity: bool = False) -> mjcf.Model:
     with open(ASSET) as f:
-        return mjcf.compile_xml(f.read())
+        m = mjcf.compile_xml(f.read())
+    if full_capacity:
+        m.con_capacity = CON_CAPACITY
+        m.efc_capacity = EFC_CAPACITY
+    return m
 
 
 class SoccerTables:
@@ -119,13 +133,15 @@ class SoccerVectorEnv:
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
-                 staged: bool = True, banks: int = 4):
+                 staged: bool = True, banks: int = 4, full_capacity: bool = False):
         """``staged`` selects the row-builder / lane-group PGS / finisher kernels
         with ``banks`` precomputed resets per env; ``staged=False`` runs one monolithic wave per
-        env. Both compute the same step (parity-tested against each other and the oracle)."""
+        env. Both compute the same step (parity-tested against each other and the oracle).
+        ``full_capacity`` raises the staged step's capacity from 64 contacts / 192 rows to
+        96 / 384 (see soccer_model)."""
         self.num_envs = num_envs
         self.device = torch.device(device)
-        self.model = soccer_model()
+        self.model = soccer_model(full_capacity)
         self.tables = SoccerTables(self.model, max_episode_steps)
         self.batch = PhysicsBatch(self.model, num_envs, precision=precision, device=device)
         self.native = self.batch.native

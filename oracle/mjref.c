@@ -904,8 +904,8 @@ static int clip_poly(double (*in)[2], int n, int axis, double lim, double sgn, d
   for (int i = 0; i < n; i++) {
     double *P = in[i], *Q = in[(i + 1) % n];
     double dp = sgn * P[axis] - lim, dq = sgn * Q[axis] - lim;
-    if (dp <= tol) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
-    if ((dp < -tol && dq > tol) || (dp > tol && dq < -tol)) {
+    if (dp <= tol && m < 8) { out[m][0] = P[0]; out[m][1] = P[1]; m++; }
+    if (m < 8 && ((dp < -tol && dq > tol) || (dp > tol && dq < -tol))) {
       double t = dp / (dp - dq);
       out[m][0] = P[0] + t * (Q[0] - P[0]);
       out[m][1] = P[1] + t * (Q[1] - P[1]);

@@ -1,7 +1,7 @@
 """Per-stage cycle breakdown of the step kernels (diagnostic build, -DMGX_PROFILE).
 
     python tools/stage_profile.py --build            # CPU: all translation units -> libmgx_prof.so
-    TASK=soccer|assembly|bipedal|martial N=... K=... python tools/stage_profile.py   # GPU
+    TASK=soccer|assembly|bipedal|martial|construction N=... K=... python tools/stage_profile.py   # GPU
 
 Loads libmgx_prof.so instead of libmgx.so, runs K steps of the task's VectorEnv and prints the
 mean cycles per env step for each stage of the forward pass (each translation unit has its own
@@ -45,7 +45,7 @@ def build():
 
 
 TASK_TU = {"assembly": "mgx_prof_set_buffer_assembly", "bipedal": "mgx_prof_set_buffer_bipedal",
-           "martial": "mgx_prof_set_buffer_martial"}
+           "martial": "mgx_prof_set_buffer_martial", "construction": "mgx_prof_set_buffer_construction"}
 
 
 def make_task(task, n):
@@ -58,6 +58,10 @@ def make_task(task, n):
         lo = torch.tensor([-2.0] * 7 + [0, 0], device="cuda:0")
         span = torch.tensor([4.0] * 7 + [100, 50], device="cuda:0")
         acts = [torch.rand(n, 9, device="cuda:0", generator=g) * span + lo for _ in range(4)]
+    elif task == "construction":
+        from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
+        env = ConstructionVectorEnv(n, seed=3, precision=os.environ.get("PREC", "f64"))
+        acts = [(torch.rand(n, 33, device="cuda:0", generator=g) * 2 - 1) * 200 for _ in range(4)]
     elif task == "bipedal":
         from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
         env = BipedalVectorEnv(n, seed=3)
