@@ -477,14 +477,15 @@ def main():
                     help="soccer: split the rank's envs into this many stream shards (overlapping pipelines)")
     ap.add_argument("--no-f64-line", "--no-other-line", dest="no_f64_line", action="store_true",
                     help="skip the other-precision soccer line (fp32 when the headline is fp64)")
-    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly"])
+    ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
+                                                          "construction"])
     args = ap.parse_args()
     if args.task != "soccer":
         args.mono = True  # one fused wave-per-env launch per step
     if args.precision is None:
         args.precision = "f64" if args.task == "soccer" else "f32"
     if args.envs <= 0:
-        args.envs = {"bipedal": 8192, "mixed": 1024, "assembly": 1024}.get(args.task, 4096)
+        args.envs = {"bipedal": 8192, "mixed": 1024, "assembly": 1024, "construction": 1024}.get(args.task, 4096)
 
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     world, rank, local = world_from_env()
@@ -518,6 +519,11 @@ def main():
         alo = torch.tensor([-2.0] * 7 + [0.0, 0.0], device=dev)
         alim = torch.tensor([4.0] * 7 + [100.0, 50.0], device=dev)
         pool = [(torch.rand(N, 9, device=dev, generator=g) * alim + alo).contiguous() for _ in range(16)]
+    elif args.task == "construction":
+        from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
+        args.precision = "f64"  # fp64 (its parity tests and the mixed run use fp64)
+        env = ConstructionVectorEnv(N, device=str(dev), precision="f64", seed=1234, env_offset=env_offset(rank, N))
+        pool = [((torch.rand(N, 33, device=dev, generator=g) * 2 - 1) * 200.0).contiguous() for _ in range(16)]
     else:
         from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
         if args.streams > 1:
@@ -576,7 +582,6 @@ def main():
                        "integrator": "RK4", "step_kernels": "mono", "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "capacity_overflow_steps": overflow_steps,
-                       "capacity": "96 contacts / 384 rows" if args.full_capacity else "64 contacts / 192 rows",
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(PMC_PROFILE_BIPEDAL, N, args.precision,
@@ -610,6 +615,28 @@ def main():
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_assembly(2, max(5, args.cpu_steps // 2))
+        print(json.dumps(out))
+    elif rank == 0 and args.task == "construction":
+        bytes_per_launch = CONSTRUCTION_ALG_BYTES * N
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        out = {
+            "metric": "env steps/sec (whole node), humanoid_construction 1024 envs/GPU (RK4 + Newton, nv 99)",
+            "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (U(-200,200) actions, Philox task / weather draws)",
+            "config": {"workload": "humanoid_construction_env, 1024 envs/GPU (BASELINE configs[4] task)",
+                       "envs_per_gpu": N, "global_batch": N * world, "parallelism": f"dp{world} (env shards)",
+                       "autoreset": "same-step", "integrator": "RK4", "solver": "Newton",
+                       "step_kernels": "wide (two dofs per lane)",
+                       "episodes_started": int(acc[1].item()), "terminated_total": int(acc[3].item()),
+                       "bad_state_resets": int(acc[5].item()), "capacity_overflow_steps": overflow_steps,
+                       "mean_reward": _finite(acc[2].item() / total_steps)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "mgx_construction_step = k_construction<double,0>",
+                         "alg_bytes_per_step": bytes_per_launch, "launch_ms": round(launch_ms, 4)},
+        }
         print(json.dumps(out))
     elif rank == 0 and args.task == "parkour":
         bytes_per_launch = PARKOUR_ALG_BYTES * N
