@@ -166,7 +166,31 @@ __device__ __forceinline__ float wave_sum_fast(float x) {
   x += dpp_upd<0x143, 0xc>(x);
   return readlane(x, 63);
 }
-__device__ __forceinline__ double wave_sum_fast(double x) { return wave_sum(x); }
+// fp64 through the same DPP patterns: both 32-bit halves move with v_mov_b32_dpp (pure data
+// movement, exact), so an fp64 reduction costs VALU steps instead of ds_bpermute round trips
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  int2 h = __builtin_bit_cast(int2, v);
+  h.x = __builtin_amdgcn_mov_dpp(h.x, CTRL, 0xf, 0xf, false);
+  h.y = __builtin_amdgcn_mov_dpp(h.y, CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, h);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_upd_d(double v) {
+  int2 h = __builtin_bit_cast(int2, v);
+  h.x = __builtin_amdgcn_update_dpp(0, h.x, CTRL, ROWS, 0xf, false);
+  h.y = __builtin_amdgcn_update_dpp(0, h.y, CTRL, ROWS, 0xf, false);
+  return __builtin_bit_cast(double, h);
+}
+__device__ __forceinline__ double wave_sum_fast(double x) {
+  x += dpp_d<0xB1>(x);
+  x += dpp_d<0x4E>(x);
+  x += dpp_d<0x141>(x);
+  x += dpp_d<0x140>(x);
+  x += dpp_upd_d<0x142, 0xa>(x);
+  x += dpp_upd_d<0x143, 0xc>(x);
+  return readlane(x, 63);
+}
 
 // four independent full-wave sums, DPP steps interleaved so the hazard wait states of one
 // chain are filled by the others (same per-chain order as wave_sum_fast)
@@ -186,7 +210,19 @@ __device__ __forceinline__ void wave_sum4(float& a, float& b, float& c, float& d
   a = readlane(a, 63); b = readlane(b, 63); c = readlane(c, 63); d = readlane(d, 63);
 }
 __device__ __forceinline__ void wave_sum4(double& a, double& b, double& c, double& d) {
-  a = wave_sum(a); b = wave_sum(b); c = wave_sum(c); d = wave_sum(d);
+#define MGX_STEP4(OP) a += OP(a); b += OP(b); c += OP(c); d += OP(d);
+  MGX_STEP4(dpp_d<0xB1>)
+  MGX_STEP4(dpp_d<0x4E>)
+  MGX_STEP4(dpp_d<0x141>)
+  MGX_STEP4(dpp_d<0x140>)
+#define MGX_B15(x) dpp_upd_d<0x142, 0xa>(x)
+#define MGX_B31(x) dpp_upd_d<0x143, 0xc>(x)
+  MGX_STEP4(MGX_B15)
+  MGX_STEP4(MGX_B31)
+#undef MGX_B15
+#undef MGX_B31
+#undef MGX_STEP4
+  a = readlane(a, 63); b = readlane(b, 63); c = readlane(c, 63); d = readlane(d, 63);
 }
 
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }

@@ -11,7 +11,7 @@ template <typename T>
 void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big) {
   static const int spw = getenv("MGX_PGS_SPW") ? atoi(getenv("MGX_PGS_SPW")) : MGX_PGS_SPW;  // debug: slots per wave
   int grid = (slots + (spw < 0 ? -spw : spw) - 1) / (spw < 0 ? -spw : spw);
-  switch (P.dpl) {
+  switch ((P.dpl + MGX_PGS_LPS / 8 - 1) / (MGX_PGS_LPS / 8)) {  // register entries per lane
 #define MGX_PGS_CASE(E) \
     case E: hipLaunchKernelGGL((k_pgs_groups<T, E>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw, big); break;
     MGX_PGS_CASE(1) MGX_PGS_CASE(2) MGX_PGS_CASE(3) MGX_PGS_CASE(4) MGX_PGS_CASE(5) MGX_PGS_CASE(6) MGX_PGS_CASE(7)

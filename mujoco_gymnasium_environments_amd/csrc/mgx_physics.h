@@ -334,7 +334,7 @@ __device__ __forceinline__ void load_rows(T* x, const T* Bm, int Bs, int r0, int
 }
 
 template <typename T>
-__device__ __forceinline__ T usum(T x) { return readlane(wave_sum(x), 0); }
+__device__ __forceinline__ T usum(T x) { return wave_sum_fast(x); }  // DPP, uniform result
 
 // B_r = D^-1/2 L'^-1 J_r' for one row x (LDS, lane-private): for k = nv-1 .. 0 the ancestors
 // of k get x[anc] -= L[k][anc] x[k]. The ancestors of one k are distinct, so all their loads

@@ -28,7 +28,8 @@ namespace mgx {
 // scalar layout per 4-row block (20 reals, 16-byte aligned): [b x4][f x4][R x4][1/AR x4][AR/2 x4],
 // so the solver reads each quantity of a block with one 16-byte LDS load
 #define MGX_SQ(k, i) (4 * (k) + (i))
-#define MGX_PGS_SPW 8          // solver: slots per wave (8 lanes each)
+#define MGX_PGS_LPS 16         // solver: lanes per slot (8 or 16)
+#define MGX_PGS_SPW (64 / MGX_PGS_LPS)  // solver: slots per wave
 #define MGX_PGS_RING 3         // solver: register ring of 4-row blocks (RING - 1 in flight; 4 measured no faster)
 #define MGX_PGS_LDS_ROWS 192   // rows per slot the main solver launch keeps in LDS (2 waves / CU in fp64)
 #define MGX_PGS_WIDE_GRID 32   // waves of the wide-LDS launch for the slots over MGX_PGS_LDS_ROWS
@@ -437,7 +438,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
 }
 
 // ------------------------------------------------------------------ S2: lane-group PGS
-// Gauss-Seidel sweeps of mj_solPGS [ext], 8 slots per wave, 8 lanes per slot. Row scalars
+// Gauss-Seidel sweeps of mj_solPGS [ext], MGX_PGS_SPW slots per wave, MGX_PGS_LPS lanes per slot. Row scalars
 // (b, f, R, 1/AR, AR/2), the block table (offset, support size S) and v = B'f (one real per
 // dof, plus a sink entry) live in LDS. Each 4-row block's B comes compressed to its dof support
 // (S ~ 6..25 of nv, index list + 4 value rows) with its couplings A_ij; lane j of a slot holds
@@ -453,17 +454,20 @@ __device__ __forceinline__ float dpp_row(float v) {
 }
 // four independent 8-lane sums (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror); every lane of
 // the 8-lane group ends with the identical total
+// With 16 lanes per slot a row_mirror step adds the two 8-lane halves (lane i and 15 - i).
 __device__ __forceinline__ void oct_sum4(float& a, float& b, float& c, float& d) {
 #define MGX_R4(CTRL) a += dpp_row<CTRL>(a); b += dpp_row<CTRL>(b); c += dpp_row<CTRL>(c); d += dpp_row<CTRL>(d);
   MGX_R4(0xB1)
   MGX_R4(0x4E)
   MGX_R4(0x141)
+  if constexpr (MGX_PGS_LPS == 16) { MGX_R4(0x140) }
 #undef MGX_R4
 }
 __device__ __forceinline__ double oct_sum(double x) {
-  x += __shfl_xor(x, 1);
-  x += __shfl_xor(x, 2);
-  x += __shfl_xor(x, 4);
+  x += dpp_d<0xB1>(x);
+  x += dpp_d<0x4E>(x);
+  x += dpp_d<0x141>(x);
+  if constexpr (MGX_PGS_LPS == 16) x += dpp_d<0x140>(x);
   return x;
 }
 __device__ __forceinline__ void oct_sum4(double& a, double& b, double& c, double& d) {
@@ -498,7 +502,12 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.a0 = pa[0];
   k.a1 = pa[1];
 #pragma unroll
-  for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t[1 + d] + 4 * j);
+  for (int d = 0; d < EPL; d++) {
+    // entry d of lane j is dof 8 gi + (j & 7) of 8-dof group gi (16 lanes: the two halves of
+    // the slot take alternate groups)
+    const int gi = MGX_PGS_LPS == 8 ? d : 2 * d + (j >> 3);
+    k.b[d] = *reinterpret_cast<const V4*>(Bsl + (gi < 7 ? t[1 + gi] : 0u) + 4 * (j & 7));
+  }
   const V4* q = reinterpret_cast<const V4*>(sc + 4 * MGX_SCAL * blk);
   k.qb = q[0];
   k.qR = q[2];
@@ -579,7 +588,7 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
 template <typename T, int EPL>
 __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* list, int cnt, int base, int capE, int maxit,
                                           T tol, T scale, int spw) {
-  const int l = threadIdx.x, s = l >> 3, j = l & 7;
+  const int l = threadIdx.x, s = l / MGX_PGS_LPS, j = l % MGX_PGS_LPS;
   const int spn = spw < 0 ? -spw : spw;
   const int idx = base + s;
   const int slot = (s < spn && idx < cnt) ? list[idx] : -1;
@@ -593,9 +602,9 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   const size_t sl = (size_t)(slot >= 0 ? slot : 0);
   const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
   const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * P.maxE);
-  for (int q = j; q < MGX_SCAL * 4 * nbcap3; q += 8) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
+  for (int q = j; q < MGX_SCAL * 4 * nbcap3; q += MGX_PGS_LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
   // block table: the slot's blocks, then zero-group entries up to the capacity
-  for (int q = j; q < 8 * nbcap3; q += 8) bt[q] = q < 8 * nblk ? (uint32_t)gbt[q] : 0u;
+  for (int q = j; q < 8 * nbcap3; q += MGX_PGS_LPS) bt[q] = q < 8 * nblk ? (uint32_t)gbt[q] : 0u;
   int nm = nblk;
   nm = max(nm, __shfl_xor(nm, 8));
   nm = max(nm, __shfl_xor(nm, 16));
@@ -637,7 +646,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     }
   }
   if (cpart > 0) {
-    for (int r = j; r < ne; r += 8) sc[(r >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, r & 3)] = 0;
+    for (int r = j; r < ne; r += MGX_PGS_LPS) sc[(r >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, r & 3)] = 0;
 #pragma unroll
     for (int d = 0; d < EPL; d++) v[d] = 0;
   }
@@ -690,7 +699,10 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     T* vo = P.at<T>(P.o_vout) + (size_t)slot * 64;
 #pragma unroll
     for (int d = 0; d < EPL; d++)
-      if (j + 8 * d < P.nv) vo[j + 8 * d] = v[d];
+      {
+        const int dof = 8 * (MGX_PGS_LPS == 8 ? d : 2 * d + (j >> 3)) + (j & 7);
+        if (dof < P.nv) vo[dof] = v[d];
+      }
     if (j == 0) P.at<int>(P.o_niter)[slot] = it;
   }
 }
