@@ -103,64 +103,105 @@ def _finite(x: float):
     return round(x, 3) if np.isfinite(x) else None
 
 
+def timed_region(step, steps: int, sync, dist=None) -> float:
+    """The timed region of every bench line: a barrier and a device sync on both sides of exactly
+    `steps` calls of step(k); returns this rank's wall seconds."""
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def whole_job_value(acc, elapsed: float):
+    """End-of-rollout reduction (SUM of the metric vector, MAX of the wall time over ranks) and
+    the whole-job value: env steps of all ranks / the slowest rank's time."""
+    from mujoco_gymnasium_environments_amd.distributed import reduce_rollout
+    acc, elapsed = reduce_rollout(acc, elapsed)
+    return acc, elapsed, acc[0].item() / elapsed
+
+
+class OracleSoccerEnv:
+    """One humanoid_soccer env on the oracle (mjref fp64 physics + the numpy logic oracle), reset
+    draws keyed by the GLOBAL env index like the device's (seed + global_env), same-step autoreset.
+    The CPU baseline and the gloo test of the bench harness step it."""
+
+    _shared = None  # (model, tables, logic, packed model): built once per process
+
+    def __init__(self, global_env: int, seed: int = 0):
+        from mujoco_gymnasium_environments_amd.seeding import np_random
+        from oracle.mjref import RefSim
+        if OracleSoccerEnv._shared is None:
+            from mujoco_gymnasium_environments_amd import cabi
+            from mujoco_gymnasium_environments_amd.envs.soccer import SoccerTables, soccer_model
+            from oracle.soccer_logic import SoccerLogic
+            m = soccer_model()
+            tb = SoccerTables(m)
+            OracleSoccerEnv._shared = (m, tb, SoccerLogic(tb), cabi.pack_model(m))
+        self.m, self.tb, self.L, pk = OracleSoccerEnv._shared
+        m = self.m
+        self.sim = RefSim(pk)
+        self.draws = self.tb.reset_draws(np_random(seed + global_env)[0])
+        nn = len(self.tb.noise_joints)
+        d = self.draws
+        self.s = dict(wind_strength=d[4 + nn], wind_direction=np.array([np.cos(d[5 + nn]), np.sin(d[5 + nn])]))
+        self.reset()
+
+    def reset(self):
+        m, tb, sim, d = self.m, self.tb, self.sim, self.draws
+        sim.reset()
+        q = sim.qpos
+        a0 = tb.root_qposadr
+        q[a0:a0 + 3] = [d[0], d[1], 1.4]
+        q[a0 + 3:a0 + 7] = [np.cos(d[2] / 2), 0, 0, np.sin(d[2] / 2)]
+        q[tb.ball_qposadr:tb.ball_qposadr + 3] = [d[0] + 2, d[1], 0.15]
+        for k, j in enumerate(tb.noise_joints):
+            lo, hi = m.jnt_range[j]
+            q[m.jnt_qposadr[j]] = np.clip((lo + hi) / 2 + d[3 + k], lo, hi)
+        q[tb.gk_qposadr] = d[3 + len(tb.noise_joints)]
+        sim.step(10)
+        self.view()
+        self.s.update(goal_scored=False, stats=np.zeros(5), prev_ball_pos=self.s["xpos"][tb.ball].copy(),
+                      prev_robot_pos=self.s["xpos"][tb.torso].copy())
+        self.nstep = 0
+
+    def view(self):
+        m, sim = self.m, self.sim
+        c = sim.contacts()
+        self.s.update(qpos=sim.qpos, qvel=sim.qvel, xpos=sim.xpos.reshape(-1, 3), xquat=sim.xquat.reshape(-1, 4),
+                      subtree_com=sim.subtree_com.reshape(-1, 3), con_geom=c["geom"], con_dist=c["dist"],
+                      con_mu=np.array([np.linalg.norm(m.pair_friction[p][:2]) for p in c["pair"]]), ctrl=sim.ctrl,
+                      qfrc_applied=sim.qfrc_applied, xfrc_applied=sim.xfrc_applied.reshape(-1, 6))
+
+    def step(self, action):
+        """-> (reward, terminated, truncated); an ended episode is reset in the same call."""
+        a = self.L.pre(self.s, action)
+        self.sim.step()
+        self.view()
+        self.nstep += 1
+        _, reward, term, trunc, _, _ = self.L.post(self.s, a, self.nstep)
+        if term or trunc:
+            self.reset()
+        return float(reward), bool(term), bool(trunc)
+
+
 def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
     """Oracle port on one host core: mjref (C, fp64) physics + numpy env logic."""
-    from mujoco_gymnasium_environments_amd import cabi
-    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerTables, soccer_model
-    from mujoco_gymnasium_environments_amd.seeding import np_random
-    from oracle.mjref import RefSim
-    from oracle.soccer_logic import SoccerLogic
-    m = soccer_model()
-    pk = cabi.pack_model(m)
-    tb = SoccerTables(m)
-    L = SoccerLogic(tb)
+    from mujoco_gymnasium_environments_amd.envs.soccer import soccer_model
     rng = np.random.default_rng(seed)
-    acts = rng.uniform(-150, 150, (64, m.nu)).astype(np.float32)
+    acts = rng.uniform(-150, 150, (64, soccer_model().nu)).astype(np.float32)
     total = 0
     t0 = time.perf_counter()
     for e in range(n_envs):
-        sim = RefSim(pk)
-        draws = tb.reset_draws(np_random(seed + e)[0])
-
-        def reset():
-            sim.reset()
-            q = sim.qpos
-            a0 = tb.root_qposadr
-            q[a0:a0 + 3] = [draws[0], draws[1], 1.4]
-            q[a0 + 3:a0 + 7] = [np.cos(draws[2] / 2), 0, 0, np.sin(draws[2] / 2)]
-            q[tb.ball_qposadr:tb.ball_qposadr + 3] = [draws[0] + 2, draws[1], 0.15]
-            for k, j in enumerate(tb.noise_joints):
-                lo, hi = m.jnt_range[j]
-                q[m.jnt_qposadr[j]] = np.clip((lo + hi) / 2 + draws[3 + k], lo, hi)
-            q[tb.gk_qposadr] = draws[3 + len(tb.noise_joints)]
-            sim.step(10)
-        reset()
-        nn = len(tb.noise_joints)
-        s = dict(wind_strength=draws[4 + nn], wind_direction=np.array([np.cos(draws[5 + nn]), np.sin(draws[5 + nn])]),
-                 goal_scored=False, stats=np.zeros(5))
-
-        def view():
-            c = sim.contacts()
-            s.update(qpos=sim.qpos, qvel=sim.qvel, xpos=sim.xpos.reshape(-1, 3), xquat=sim.xquat.reshape(-1, 4),
-                     subtree_com=sim.subtree_com.reshape(-1, 3), con_geom=c["geom"], con_dist=c["dist"],
-                     con_mu=np.array([np.linalg.norm(m.pair_friction[p][:2]) for p in c["pair"]]), ctrl=sim.ctrl,
-                     qfrc_applied=sim.qfrc_applied, xfrc_applied=sim.xfrc_applied.reshape(-1, 6))
-        view()
-        s["prev_ball_pos"], s["prev_robot_pos"] = s["xpos"][tb.ball].copy(), s["xpos"][tb.torso].copy()
-        step = 0
+        env = OracleSoccerEnv(e, seed)
         for k in range(n_steps):
-            a = L.pre(s, acts[k % 64])
-            sim.step()
-            view()
-            step += 1
-            _, _, term, trunc, _, _ = L.post(s, a, step)
+            env.step(acts[k % 64])
             total += 1
-            if term or trunc:
-                reset()
-                view()
-                s.update(goal_scored=False, stats=np.zeros(5), prev_ball_pos=s["xpos"][tb.ball].copy(),
-                         prev_robot_pos=s["xpos"][tb.torso].copy())
-                step = 0
     dt = time.perf_counter() - t0
     return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
             "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of humanoid_soccer, U(-150,150) actions, "
@@ -369,16 +410,7 @@ def bench_mixed(args, dev, world, rank, dist):
         env.rollout.zero_()
     evs = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in tasks}
            for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(i, evs[i])
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(lambda i: one_step(i, evs[i]), args.steps, lambda: torch.cuda.synchronize(dev), dist)
     per = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in tasks}
     acc = torch.zeros(6, dtype=torch.float64, device=dev)
     for env, _, _ in tasks.values():
@@ -388,7 +420,7 @@ def bench_mixed(args, dev, world, rank, dist):
         acc[3] += ro[1]
         acc[4] += ro[2]
         acc[5] += float(env.batch.warning.sum().item())
-    acc, elapsed = reduce_rollout(acc, elapsed)
+    acc, elapsed, _ = whole_job_value(acc, elapsed)
     total = acc[0].item()
     if rank == 0:
         dom = max(per, key=per.get)
@@ -547,18 +579,12 @@ def main():
         e.batch.overflow.zero_()
     ep0 = sum(int(e.episode.sum().item()) for e in shards)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
+
+    def one_step(k):
         ev[k][0].record()
         env.step(pool[k % len(pool)])
         ev[k][1].record()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(one_step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     ro = torch.cat([e.rollout for e in shards]).double().sum(0)
     acc[0] = ro[3]
@@ -566,9 +592,8 @@ def main():
     acc[2], acc[3], acc[4] = ro[0], ro[1], ro[2]
     acc[5] = float(sum(float(e.batch.warning.sum().item()) for e in shards))
     overflow_steps = sum(int(e.batch.overflow.sum().item()) for e in shards)
-    acc, elapsed = reduce_rollout(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
+    acc, elapsed, value = whole_job_value(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
-    value = total_steps / elapsed
     if rank == 0 and args.task == "bipedal":
         bytes_per_launch = BIPEDAL_ALG_BYTES * N
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9

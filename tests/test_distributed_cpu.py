@@ -51,3 +51,67 @@ def test_single_process_noop():
     from mujoco_gymnasium_environments_amd.distributed import reduce_rollout
     m, t = reduce_rollout(torch.ones(6, dtype=torch.float64), 3.5)
     assert m.tolist() == [1.0] * 6 and t == 3.5
+
+
+def _bench_worker(rank, world, port, q):
+    """One rank of bench.py's harness (timed_region + whole_job_value, the code every bench line
+    runs) over its env shard of the oracle soccer env, gloo standing in for RCCL."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import time
+
+    import numpy as np
+
+    import bench
+    from mujoco_gymnasium_environments_amd.distributed import env_offset
+    n, steps = 2, 4
+    envs = [bench.OracleSoccerEnv(env_offset(rank, n) + i, seed=5) for i in range(n)]
+    acts = np.random.default_rng(0).uniform(-150, 150, (steps, envs[0].m.nu)).astype(np.float32)
+    acc = torch.zeros(6, dtype=torch.float64)
+
+    def step(k):
+        for e in envs:
+            r, term, trunc = e.step(acts[k])
+            acc[0] += 1
+            acc[2] += r
+            acc[3] += term
+            acc[4] += trunc
+        time.sleep(0.05 * rank)  # rank 1 is the slow one: the value uses its time
+
+    own = bench.timed_region(step, steps, lambda: None, dist)
+    red, elapsed, value = bench.whole_job_value(acc, own)
+    q.put((rank, own, elapsed, value, red.tolist()))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_harness_env_shards():
+    """bench.py's N>1 path on CPU: barrier + timed region per rank, SUM of the metrics and MAX of
+    the time over ranks, value = all ranks' env steps / slowest time; and the env shards (global
+    index = env_offset + local) reproduce a single-process run over all envs."""
+    import numpy as np
+
+    import bench
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, own0, el0, v0, red0), (_, own1, el1, v1, red1) = out
+    assert red0 == red1, (red0, red1)
+    # the closing barrier holds the fast rank until the slow one (4 x 50 ms of sleeps) is done
+    assert el0 == el1 == max(own0, own1) and min(own0, own1) >= 4 * 0.05, (own0, own1, el0, el1)
+    assert red0[0] == 2 * 2 * 4 and v0 == v1 == red0[0] / el0
+    # one process over the 4 global envs: the same totals
+    envs = [bench.OracleSoccerEnv(g, seed=5) for g in range(4)]
+    acts = np.random.default_rng(0).uniform(-150, 150, (4, envs[0].m.nu)).astype(np.float32)
+    rew, term, trunc = 0.0, 0, 0
+    for k in range(4):
+        for e in envs:
+            r, t1, t2 = e.step(acts[k])
+            rew, term, trunc = rew + r, term + t1, trunc + t2
+    assert abs(red0[2] - rew) <= 1e-9 * abs(rew) and (red0[3], red0[4]) == (term, trunc)
