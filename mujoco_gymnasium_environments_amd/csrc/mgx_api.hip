@@ -207,7 +207,12 @@ __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T
   int env = blockIdx.x;
   if (env >= n_env) return;
   int l = lane_id();
-  if (env == 0 && l == 0) { P.ctr()[1] = 0; P.ctr()[2] = 0; }  // the solver lists are consumed
+  if (env == 0 && l == 0) {  // the solver lists are consumed; their sizes stay for diagnostics
+    P.ctr()[3] = P.ctr()[1];
+    P.ctr()[4] = P.ctr()[2];
+    P.ctr()[1] = 0;
+    P.ctr()[2] = 0;
+  }
   Env<T> e;
   env_bind(m, e, smem);
   if (banks) {
@@ -570,6 +575,14 @@ int host_check_state(const mgx_state* s) {
 }
 }  // namespace mgx
 
+// LDS bytes of one main-launch solver wave: its slots' row scalars, block tables and compressed B
+// (tools/pgs_census.py measures what the slots need at bench conditions); 16 lanes per slot =
+// 4 slots per wave, 64 lanes = 1
+static int pgs_arena_bytes(int precision) {
+  const int a = precision == MGX_F32 ? MGX_PGS_ARENA_F32 : MGX_PGS_ARENA_F64;
+  return pgs_lanes() == 64 ? a / 2 : a;
+}
+
 // Staged-step workspace layout for (model, n_env, banks); offsets in bytes, 256-aligned.
 static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
@@ -585,6 +598,12 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   int capE = cap_env ? (atoi(cap_env) + 3) / 4 * 4 : MGX_PGS_LDS_ROWS;
   if (capE < 4 || capE > MGX_PGS_LDS_ROWS) capE = MGX_PGS_LDS_ROWS;
   p.capE = p.maxE < capE ? p.maxE : capE;
+  // LDS arena of one main-launch solver wave (scalars + block table + B of its slots); the
+  // test / tuning hook MGX_PGS_ARENA overrides it (read per call; a small arena sends waves to
+  // the global-B launch)
+  const char* ar_env = getenv("MGX_PGS_ARENA");
+  p.arena = pgs_arena_bytes(m->precision);
+  if (ar_env && atoi(ar_env) > 0 && atoi(ar_env) <= 96 * 1024) p.arena = atoi(ar_env);
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
@@ -594,7 +613,7 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.o_ctr = take(64);
   p.o_carry = take(S * p.carry_stride * rb);
   p.o_carryi = take(S * p.carryi_stride * 4);
-  p.o_ne = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_k2big = take(S * 4); p.o_fix = take((size_t)n_env * 4);
+  p.o_ne = take(S * 4); p.o_blen = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_k2big = take(S * 4); p.o_fix = take((size_t)n_env * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
   p.o_blk = take(S * p.maxE * 4);  // 8 uint16 per 4-row block
   p.o_B = take(S * (size_t)p.bcap * rb);
@@ -616,7 +635,8 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 static int pgs_lds_bytes(const mgx_model* m, int rows) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nb3 = (rows / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
-  return MGX_PGS_SPW * (MGX_SCAL * 4 * nb3 + 4) * rb + MGX_PGS_SPW * nb3 * 32 + 64;
+  const int spw = 64 / pgs_lanes();
+  return spw * (MGX_SCAL * 4 * nb3 + 4) * rb + spw * nb3 * 32 + 64;
 }
 
 template <typename T>
@@ -633,10 +653,11 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, *e, action, n_env, mask, P,
                      banks);
   T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
-  launch_pgs<T>(P, slots, pgs_lds_bytes(m, P.capE), st, M.iterations, M.tolerance, scale, 0);
-  // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped);
-  // a small grid-stride launch that exits at once when the list is empty
-  if (P.maxE > P.capE) launch_pgs<T>(P, 8 * MGX_PGS_WIDE_GRID, pgs_lds_bytes(m, P.maxE), st, M.iterations, M.tolerance, scale, 1);
+  launch_pgs<T>(P, slots, pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE), st, M.iterations, M.tolerance, scale, 0);
+  // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped)
+  // and those of main-launch waves that did not fit their arena: a small grid-stride global-B
+  // launch that exits at once when the list is empty
+  launch_pgs<T>(P, 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, pgs_lds_bytes(m, P.maxE), st, M.iterations, M.tolerance, scale, 1);
   hipLaunchKernelGGL(k_soccer_finish<T>, dim3(n_env), dim3(64), m->Lf.bytes, st, Mf, ids, *s, *e, action, obs, reward,
                      terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks);
   int fgrid = n_env < 256 ? n_env : 256;
@@ -738,7 +759,8 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
                   set_lds(k_soccer_rows<double>, m->Ls.bytes) | set_lds(k_soccer_finish<double>, m->Lf.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
   if (m->staged_ok) {
-    int pl = pgs_lds_bytes(m, m->Ls.max_nefc);  // >= the main launch's
+    int pl = pgs_lds_bytes(m, m->Ls.max_nefc);  // the global-B launch's
+    if (pl < 96 * 1024) pl = 96 * 1024;  // the arena (MGX_PGS_ARENA tuning up to 96 KiB)
     if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
     int r3 = pgs_configure_lds(precision, pl);
     if (r3 != MGX_OK) { delete m; return r3; }
@@ -864,6 +886,17 @@ int64_t mgx_soccer_workspace_bytes(const mgx_model* m, int n_env, int banks) {
   if (!m || n_env <= 0 || banks < 0 || banks > 16) return fail(MGX_E_ARG, "bad argument");
   if (!m->staged_ok) return fail(MGX_E_UNSUPPORTED, "staged step: model exceeds the staged solver's capacity");
   return (int64_t)make_pipe(m, nullptr, n_env, banks, nullptr);
+}
+
+int mgx_soccer_workspace_layout(const mgx_model* m, int n_env, int banks, int64_t* out, int n_out) {
+  if (!m || !out || n_env <= 0 || banks < 0 || banks > 16 || n_out < 10) return fail(MGX_E_ARG, "bad argument");
+  if (!m->staged_ok) return fail(MGX_E_UNSUPPORTED, "staged step: model exceeds the staged solver's capacity");
+  Pipe P;
+  make_pipe(m, nullptr, n_env, banks, &P);
+  const int64_t v[10] = {(int64_t)P.o_ctr, (int64_t)P.o_ne, (int64_t)P.o_k2list, (int64_t)P.o_blk, (int64_t)P.o_B,
+                         P.bcap, P.maxE, P.capE, P.S, m->precision == MGX_F32 ? 4 : 8};
+  for (int i = 0; i < 10; i++) out[i] = v[i];
+  return MGX_OK;
 }
 
 int mgx_soccer_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, void* stream) {

@@ -79,6 +79,8 @@ int step_kernels_configure(const mgx_model* m);
 template <typename T>
 void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big);
 int pgs_configure_lds(int precision, int bytes);
+int pgs_lanes();
+int pgs_lds_b();
 }  // namespace mgx
 
 #define MGX_WIDE_MSG "nv > 64: this model runs on the wide (two dofs per lane) kernels only"

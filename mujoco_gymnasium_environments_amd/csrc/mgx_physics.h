@@ -999,6 +999,8 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
     for (int u = 0; u <= t; u++, q++)
 #pragma unroll
       for (int v = 0; v < 4; v++) acc[q][v] = (t == u && row_of(v) == i) ? (T)1 : (T)0;
+  // rows with x >= 0 add nothing (s_k = 0): their B is not loaded (zeros instead), and a chunk
+  // of four inactive rows skips its MFMAs — the same sums, without streaming inactive rows
   auto load = [&](int r0, T* b, T& sc) {
     const int r = r0 + kq;
     sc = 0;
@@ -1009,7 +1011,7 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const int c = 16 * t + i;
-      b[t] = (r < ne && c < nv) ? Bm[r * Bs + c] : (T)0;
+      b[t] = (sc != (T)0 && c < nv) ? Bm[r * Bs + c] : (T)0;
     }
   };
   T bn[4], sn;
@@ -1018,6 +1020,7 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
     T b[4] = {bn[0], bn[1], bn[2], bn[3]};
     const T sc = sn;
     load(r0 + 4, bn, sn);  // the next chunk is in flight during this chunk's MFMAs
+    if (__ballot(sc != (T)0) == 0ull) continue;
 #pragma unroll
     for (int t = 0, q = 0; t < 4; t++)
 #pragma unroll
@@ -1132,13 +1135,19 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   auto gradient = [&]() {
     T gg = u;
     for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-      T xb[MGX_RB];
-      load_rows(xb, Bm, Bs, r0, ne, lc, dl);
+      // only the active rows (x < 0) are loaded: the others add nothing
+      T xb[MGX_RB], xs[MGX_RB];
+#pragma unroll
+      for (int j = 0; j < MGX_RB; j++) {
+        const int r = r0 + j;
+        xs[j] = r < ne ? efc[8 * r + 1] : (T)0;
+        xb[j] = (xs[j] < 0 && dl) ? Bm[r * Bs + lc] : (T)0;
+      }
 #pragma unroll
       for (int j = 0; j < MGX_RB; j++) {
         const int r = r0 + j;
         if (r < ne) {
-          const T xr = efc[8 * r + 1];
+          const T xr = xs[j];
           if (xr < 0) gg += efc[8 * r + 4] * xr * xb[j];
         }
       }

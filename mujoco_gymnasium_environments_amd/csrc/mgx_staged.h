@@ -7,8 +7,9 @@
 //
 //   S1  k_soccer_rows   wave per slot   pre-logic, kinematics .. collision, constraint rows;
 //                                       B rows + row scalars -> HBM, carry -> HBM (27 KB LDS)
-//   S2  k_pgs_groups    8 lanes / slot PGS sweeps with B streamed from L2/MALL, v = B'f in
-//                                       registers (lane j holds dofs j, j+8, ...), 8 slots/wave
+//   S2  k_pgs_groups    16 lanes / slot PGS sweeps, 4 slots / wave, with the slots' B copied
+//                                       once into an LDS arena (global-B launch for waves whose
+//                                       slots do not fit), v = B'f in registers
 //   S3  k_soccer_finish wave per env    qacc, checkAcc, Euler, post-logic, autoreset (7 KB LDS)
 //   S4  k_soccer_fixup  wave per listed env, monolithic: reset whose bank was not ready
 //
@@ -28,11 +29,14 @@ namespace mgx {
 // scalar layout per 4-row block (20 reals, 16-byte aligned): [b x4][f x4][R x4][1/AR x4][AR/2 x4],
 // so the solver reads each quantity of a block with one 16-byte LDS load
 #define MGX_SQ(k, i) (4 * (k) + (i))
-#define MGX_PGS_LPS 16         // solver: lanes per slot (8 or 16)
-#define MGX_PGS_SPW (64 / MGX_PGS_LPS)  // solver: slots per wave
-#define MGX_PGS_RING 3         // solver: register ring of 4-row blocks (RING - 1 in flight; 4 measured no faster)
+#define MGX_PGS_LPS 16         // solver: lanes per slot (16 or 64; MGX_PGS_LPS env overrides per process)
+#define MGX_PGS_LDS_B 0        // main solver launch: 1 = B in an LDS arena, 0 = B from global memory
+#define MGX_PGS_RING 3         // global-B solver: register ring of 4-row blocks (RING - 1 in flight; 4 measured no faster)
+#define MGX_PGS_RING_LDS 2     // LDS-B solver: one block in flight covers the LDS latency
 #define MGX_PGS_LDS_ROWS 192   // rows per slot the main solver launch keeps in LDS (2 waves / CU in fp64)
-#define MGX_PGS_WIDE_GRID 32   // waves of the wide-LDS launch for the slots over MGX_PGS_LDS_ROWS
+#define MGX_PGS_WIDE_GRID 256  // waves of the global-B launch (slots over MGX_PGS_LDS_ROWS, waves over their arena)
+#define MGX_PGS_ARENA_F64 49152  // LDS arena per main-launch solver wave of 4 slots, fp64 (tools/pgs_census.py)
+#define MGX_PGS_ARENA_F32 32768  //                                                    fp32
 enum { FIX_RESET = 2 };
 
 // Workspace layout (byte offsets from base), computed on the host (mgx_soccer_workspace_bytes)
@@ -44,7 +48,8 @@ struct Pipe {
   int bcap;            // reals per slot of group-compressed B: 32 + (max_nefc / 4) * (8 + 32 * ceil(nv / 8))
   int capE;            // rows the main solver launch holds in LDS per slot; slots with more rows (up
                        // to maxE) go to the second, wide-LDS launch (o_k2big)
-  size_t o_carry, o_carryi, o_ne, o_niter, o_k2list, o_k2big, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
+  int arena;           // LDS bytes of one main-launch solver wave (scalars + block table + B of its slots)
+  size_t o_carry, o_carryi, o_ne, o_blen, o_niter, o_k2list, o_k2big, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
   size_t o_bq, o_bv, o_ba, o_btime, o_bobs, o_bprev, o_bwind, o_bk, o_bep, o_bwarn, o_bseed;
   // the checkAcc template: mj_step's outcome after mj_resetData (state + forward frames)
   size_t o_tq, o_tv, o_ta, o_tt, o_tx, o_txq, o_tsc, o_tn, o_tcg, o_tcd, o_tcm;
@@ -372,12 +377,12 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   e.nefc = ne;
   MGX_STAMP(6);
   const bool dl = l < nv;
+  int boff = 32;  // B reals of the slot; [0, 32): the zero group
   if (ne > 0) {
     const T dinvs = dl ? sqrt(e.diaginv) : (T)0;
     T* scal = P.at<T>(P.o_scal) + (size_t)slot * P.maxE * MGX_SCAL;
     T* Bo = P.at<T>(P.o_B) + (size_t)slot * P.bcap;
     int* blk = P.at<int>(P.o_blk) + (size_t)slot * P.maxE;  // 8 uint16 per 4-row block
-    int boff = 32;                                          // [0, 32): the zero group
     const int nlim4 = (nlim + 3) & ~3;
     // qacc_smooth / qacc_warmstart into LDS (limit rows) and their per-body chain sums
     if (dl) { e.vec1[l] = e.qacc_smooth; e.vec2[l] = e.qacc_ws; }
@@ -418,6 +423,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   if (l == 0) {
     cx[0] = e.ncon; cx[1] = ne; cx[2] = e.overflow; cx[3] = warn;
     P.at<int>(P.o_ne)[slot] = ne;
+    P.at<int>(P.o_blen)[slot] = boff;
 #ifdef MGX_PROFILE
     if (g_mgx_prof && slot < (int)gridDim.x) {
       g_mgx_prof[slot * 32 + 20] += ne;
@@ -438,15 +444,15 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
 }
 
 // ------------------------------------------------------------------ S2: lane-group PGS
-// Gauss-Seidel sweeps of mj_solPGS [ext], MGX_PGS_SPW slots per wave, MGX_PGS_LPS lanes per slot. Row scalars
-// (b, f, R, 1/AR, AR/2), the block table (offset, support size S) and v = B'f (one real per
-// dof, plus a sink entry) live in LDS. Each 4-row block's B comes compressed to its dof support
-// (S ~ 6..25 of nv, index list + 4 value rows) with its couplings A_ij; lane j of a slot holds
-// support entries j, j+8, ..; a 4-block register ring keeps 3 blocks in flight ahead of use,
-// and support entries past the wave's largest S are skipped uniformly. Per block the four
-// B_r.v use the pre-block v (interleaved 8-lane reductions) and row i adds
-// sum_{j<i} A_ij delta_j: the sequential Gauss-Seidel update. Per-slot results do not depend
-// on which slots share the wave (other slots only add masked no-op blocks / sweeps).
+// Gauss-Seidel sweeps of mj_solPGS [ext], 64 / LPS slots per wave, LPS lanes per slot (16: four
+// slots per wave; 64: one slot per wave, lane = dof). Row scalars (b, f, R, 1/AR, AR/2), the block
+// table and the slot's B live in LDS; v = B'f lives in registers. Each 4-row block's B comes
+// compressed to the 8-dof groups its support touches, with its couplings A_ij; lane j holds
+// dof 8 gi + (j & 7) of group gi. A register ring keeps the next block in flight ahead of use
+// (RING - 1 blocks: 1 from LDS, 2 from global memory). Per block the four B_r.v use the
+// pre-block v (interleaved DPP reductions) and row i adds sum_{j<i} A_ij delta_j: the
+// sequential Gauss-Seidel update. Per-slot results do not depend on which slots share the wave
+// (other slots only add masked no-op blocks / sweeps) nor on the launch that solves the slot.
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float v) {
   // bound_ctrl: every source lane of these patterns is valid, so the mov folds into its add
@@ -455,23 +461,33 @@ __device__ __forceinline__ float dpp_row(float v) {
 // four independent 8-lane sums (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror); every lane of
 // the 8-lane group ends with the identical total
 // With 16 lanes per slot a row_mirror step adds the two 8-lane halves (lane i and 15 - i).
+template <int LPS>
 __device__ __forceinline__ void oct_sum4(float& a, float& b, float& c, float& d) {
 #define MGX_R4(CTRL) a += dpp_row<CTRL>(a); b += dpp_row<CTRL>(b); c += dpp_row<CTRL>(c); d += dpp_row<CTRL>(d);
   MGX_R4(0xB1)
   MGX_R4(0x4E)
   MGX_R4(0x141)
-  if constexpr (MGX_PGS_LPS == 16) { MGX_R4(0x140) }
+  if constexpr (LPS == 16) { MGX_R4(0x140) }
 #undef MGX_R4
 }
+template <int LPS>
 __device__ __forceinline__ double oct_sum(double x) {
   x += dpp_d<0xB1>(x);
   x += dpp_d<0x4E>(x);
   x += dpp_d<0x141>(x);
-  if constexpr (MGX_PGS_LPS == 16) x += dpp_d<0x140>(x);
+  if constexpr (LPS == 16) x += dpp_d<0x140>(x);
   return x;
 }
+template <int LPS>
 __device__ __forceinline__ void oct_sum4(double& a, double& b, double& c, double& d) {
-  a = oct_sum(a); b = oct_sum(b); c = oct_sum(c); d = oct_sum(d);
+  a = oct_sum<LPS>(a); b = oct_sum<LPS>(b); c = oct_sum<LPS>(c); d = oct_sum<LPS>(d);
+}
+// the slot's four row dots: 8 / 16 lanes in-row DPP butterflies; a whole wave (one slot per
+// wave) the full-wave DPP reduction, totals uniform
+template <int LPS, typename T>
+__device__ __forceinline__ void slot_sum4(T& a, T& b, T& c, T& d) {
+  if constexpr (LPS == 64) wave_sum4(a, b, c, d);
+  else oct_sum4<LPS>(a, b, c, d);
 }
 
 template <typename T>
@@ -485,35 +501,59 @@ template <typename T, int EPL>
 struct PgsBlk {
   typename Vec4T<T>::type b[EPL];  // B of the block's 4 rows at this lane's dof j + 8d
   typename Vec4T<T>::type a0, a1;  // A10 A20 A21 A30 | A31 A32 - -
-  typename Vec4T<T>::type qb, qR, qi, qh;  // the rows' b, R, 1/AR, AR/2
+  typename Vec4T<T>::type qb, qf, qR, qi, qh;  // the rows' b, f, R, 1/AR, AR/2
 };
+// a block's table entry for this lane: the A offset and the offsets of its EPL dof groups,
+// loaded one ring step before the data they address
+template <int EPL>
+struct PgsTab {
+  uint32_t a, g[EPL];
+};
+
+template <int EPL, int LPS>
+__device__ __forceinline__ void pgs_load_tab(PgsTab<EPL>& t, const uint32_t* bt, int blk, int j) {
+  const uint32_t* e = bt + 8 * blk;  // widened in LDS: no 16-bit extracts on the address path
+  t.a = e[0];
+#pragma unroll
+  for (int d = 0; d < EPL; d++) {
+    const int gi = d * (LPS / 8) + (j >> 3);
+    t.g[d] = gi < 7 ? e[1 + gi] : 0u;
+  }
+}
 
 // f32: two values per v_pk_fma_f32
 typedef float mgx_f2 __attribute__((ext_vector_type(2)));
 
-template <typename T, int EPL>
-__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint32_t* bt, int blk,
-                                               int j) {
+// One block's data at its (prefetched) table entry: A, the lane's B entries and the row scalars.
+// The forces travel with the prefetch: a block's f changes only when the block itself is solved,
+// and the look-ahead never crosses a sweep boundary (each sweep restarts the ring), so the value
+// loaded here is the latest one.
+template <typename T, int EPL, int LPS>
+__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const PgsTab<EPL>& t,
+                                               int blk, int j) {
   // the table entry of a block past the slot's end points at the zero group (A included);
-  // every load is one 16-byte vector load at a table offset
+  // every load is one 16-byte vector load at a table offset (Bsl: the slot's B in the LDS
+  // arena, or in global memory for the global-B launch)
   typedef typename Vec4T<T>::type V4;
-  const uint32_t* t = bt + 8 * blk;  // widened in LDS: no 16-bit extracts on the address path
-  const V4* pa = reinterpret_cast<const V4*>(Bsl + t[0]);
+  const V4* pa = reinterpret_cast<const V4*>(Bsl + t.a);
   k.a0 = pa[0];
   k.a1 = pa[1];
 #pragma unroll
-  for (int d = 0; d < EPL; d++) {
-    // entry d of lane j is dof 8 gi + (j & 7) of 8-dof group gi (16 lanes: the two halves of
-    // the slot take alternate groups)
-    const int gi = MGX_PGS_LPS == 8 ? d : 2 * d + (j >> 3);
-    k.b[d] = *reinterpret_cast<const V4*>(Bsl + (gi < 7 ? t[1 + gi] : 0u) + 4 * (j & 7));
-  }
+  for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t.g[d] + 4 * (j & 7));
   const V4* q = reinterpret_cast<const V4*>(sc + 4 * MGX_SCAL * blk);
   k.qb = q[0];
+  k.qf = q[1];
   k.qR = q[2];
   k.qi = q[3];
   k.qh = q[4];
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
+}
+template <typename T, int EPL, int LPS>
+__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint32_t* bt,
+                                               int blk, int j) {
+  PgsTab<EPL> t;
+  pgs_load_tab<EPL, LPS>(t, bt, blk, j);
+  pgs_load_block<T, EPL, LPS>(k, Bsl, sc, t, blk, j);
 }
 
 template <typename T, int EPL>
@@ -549,23 +589,22 @@ __device__ __forceinline__ void pgs_update(const PgsBlk<T, EPL>& k, T (&v)[EPL],
   }
 }
 
-template <typename T, int EPL>
+template <typename T, int EPL, int LPS>
 __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], T* sc, int r0, bool ok0, T& impr) {
   typedef typename Vec4T<T>::type V4;
   V4* qf = reinterpret_cast<V4*>(sc + r0 * MGX_SCAL + MGX_SQ(1, 0));
-  // forces read here, not with the prefetch: a row's f must be its latest value
-  const V4 f = *qf;
+  const V4 qb = k.qb, f = k.qf, qR = k.qR, qi = k.qi, qh = k.qh;
   T d0, d1, d2, d3;
   pgs_dots(k, v, d0, d1, d2, d3);
   // b + R f off the dependent chain
-  const T t0 = k.qb.x + k.qR.x * f.x, t1 = k.qb.y + k.qR.y * f.y;
-  const T t2 = k.qb.z + k.qR.z * f.z, t3 = k.qb.w + k.qR.w * f.w;
-  oct_sum4(d0, d1, d2, d3);
+  const T t0 = qb.x + qR.x * f.x, t1 = qb.y + qR.y * f.y;
+  const T t2 = qb.z + qR.z * f.z, t3 = qb.w + qR.w * f.w;
+  slot_sum4<LPS>(d0, d1, d2, d3);
   T dl0, dl1, dl2, dl3;
   V4 nfv;
 #define MGX_PGS_ROW(C, I, DOT, DL)                                \
   {                                                               \
-    const T fr = f.C, ai = k.qi.C, hd = k.qh.C;                   \
+    const T fr = f.C, ai = qi.C, hd = qh.C;                       \
     T res = (DOT) + t##I;                                         \
     T fn = fmax(fr - res * ai, (T)0);                             \
     T delta = fn - fr;                                            \
@@ -580,41 +619,82 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
   MGX_PGS_ROW(z, 2, d2 + k.a0.y * dl0 + k.a0.z * dl1, dl2)
   MGX_PGS_ROW(w, 3, d3 + k.a0.w * dl0 + k.a1.x * dl1 + k.a1.y * dl2, dl3)
 #undef MGX_PGS_ROW
-  *qf = nfv;
+  // one lane per slot stores the forces: the slot's lanes hold identical values, and a
+  // same-address LDS store from every lane serialises
+  if ((lane_id() & (LPS - 1)) == 0) *qf = nfv;
   pgs_update(k, v, dl0, dl1, dl2, dl3);
 }
 
-// One group of up to 8 slots (one wave). capE: the rows per slot this launch's LDS holds.
-template <typename T, int EPL>
+// One group of up to 64 / LPS slots (one wave).
+// BLDS (main launch): the wave's slots get an LDS arena of P.arena bytes laid out by their
+// actual sizes — per slot the row scalars and block table for the wave's block count, then the
+// slot's compressed B (P.o_blen reals), copied from global memory once. A wave whose slots do
+// not fit lists them for the global-B launch and returns before touching anything.
+// !BLDS (global-B launch): fixed per-slot capacity of capE rows of scalars and table in LDS, B
+// read from global memory (L2 / MALL) with a register ring RING - 1 blocks ahead.
+// Both run the identical arithmetic on every slot, so which launch solves a slot is invisible.
+template <typename T, int EPL, int LPS, bool BLDS>
 __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* list, int cnt, int base, int capE, int maxit,
                                           T tol, T scale, int spw) {
-  const int l = threadIdx.x, s = l / MGX_PGS_LPS, j = l % MGX_PGS_LPS;
+  constexpr int RING = BLDS ? MGX_PGS_RING_LDS : MGX_PGS_RING;
+  typedef typename Vec4T<T>::type V4;
+  constexpr int SPW = 64 / LPS;
+  const int l = threadIdx.x, s = l / LPS, j = l % LPS;
   const int spn = spw < 0 ? -spw : spw;
   const int idx = base + s;
   const int slot = (s < spn && idx < cnt) ? list[idx] : -1;
   const int ne = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;  // a multiple of 4
   const int nblk = ne >> 2;
-  // LDS capacity in whole ring turns: nbcap3 = capE / 4 rounded up to a multiple of the ring
-  const int nbcap = capE / 4, nbcap3 = (nbcap + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;
-  const int sstride = MGX_SCAL * 4 * nbcap3 + 4;  // 16-byte aligned per slot
-  T* sc = reinterpret_cast<T*>(smem) + s * sstride;
-  uint32_t* bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + MGX_PGS_SPW * sstride) + s * 8 * nbcap3;
-  const size_t sl = (size_t)(slot >= 0 ? slot : 0);
-  const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
-  const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * P.maxE);
-  for (int q = j; q < MGX_SCAL * 4 * nbcap3; q += MGX_PGS_LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
-  // block table: the slot's blocks, then zero-group entries up to the capacity
-  for (int q = j; q < 8 * nbcap3; q += MGX_PGS_LPS) bt[q] = q < 8 * nblk ? (uint32_t)gbt[q] : 0u;
   int nm = nblk;
   nm = max(nm, __shfl_xor(nm, 8));
   nm = max(nm, __shfl_xor(nm, 16));
   nm = max(nm, __shfl_xor(nm, 32));
   int nbMax = __builtin_amdgcn_readfirstlane(nm);
-  if (spw < 0) nbMax = nbcap;  // debug: sweep every block slot
-  // whole ring turns (3 blocks): the sweep has no remainder path; the padding blocks are
-  // zero-table blocks whose rows are masked (their LDS scalars zero-filled below)
-  const int nbRun = (nbMax + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;
-  const T* Bsl = P.at<T>(P.o_B) + sl * P.bcap;
+  if (spw < 0) nbMax = capE / 4;  // debug: sweep every block slot
+  // whole ring turns: the sweep has no remainder path; the padding blocks are zero-table
+  // blocks whose rows are masked (their LDS scalars zero-filled below)
+  const int nbRun = (nbMax + RING - 1) / RING * RING;
+  const size_t sl = (size_t)(slot >= 0 ? slot : 0);
+  const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
+  const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * P.maxE);
+  const T* gB = P.at<T>(P.o_B) + sl * P.bcap;
+  int nbA;  // blocks of scalars / table entries per slot (the look-ahead stays inside)
+  T* sc;
+  uint32_t* bt;
+  const T* Bsl;
+  if constexpr (BLDS) {
+    nbA = nbRun + RING - 1;
+    const int blen = slot >= 0 ? (P.at<int>(P.o_blen)[slot] + 3) & ~3 : 0;
+    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 32) + blen * (int)sizeof(T);  // 16-byte multiple
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < SPW; q++) {
+      const int bq = __shfl(bytes, q * LPS);
+      off += q < s ? bq : 0;
+      tot += bq;
+    }
+    if (__builtin_amdgcn_readfirstlane(tot) > P.arena) {
+      if (j == 0 && slot >= 0) P.at<int>(P.o_k2big)[atomicAdd(P.ctr() + 2, 1)] = slot;
+      return;
+    }
+    sc = reinterpret_cast<T*>(smem + off);
+    bt = reinterpret_cast<uint32_t*>(sc + 4 * MGX_SCAL * nbA);
+    T* Bs = reinterpret_cast<T*>(bt + 8 * nbA);
+    for (int q = 4 * j; q < blen; q += 4 * LPS)
+      *reinterpret_cast<V4*>(Bs + q) = *reinterpret_cast<const V4*>(gB + q);
+    Bsl = Bs;
+  } else {
+    // LDS capacity in whole ring turns: nbA = capE / 4 rounded up to a multiple of the ring
+    const int nbcap = capE / 4;
+    nbA = (nbcap + RING - 1) / RING * RING;
+    const int sstride = MGX_SCAL * 4 * nbA + 4;  // 16-byte aligned per slot
+    sc = reinterpret_cast<T*>(smem) + s * sstride;
+    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * 8 * nbA;
+    Bsl = gB;
+  }
+  for (int q = j; q < MGX_SCAL * 4 * nbA; q += LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
+  // block table: the slot's blocks, then zero-group entries up to the capacity
+  for (int q = j; q < 8 * nbA; q += LPS) bt[q] = q < 8 * nblk ? (uint32_t)gbt[q] : 0u;
   __syncthreads();
   // warmstart: v = B' f, dual cost, reset to zero if the cost is positive
   T v[EPL];
@@ -622,7 +702,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   for (int d = 0; d < EPL; d++) v[d] = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL>(k, Bsl, sc, bt, b, j);
+    pgs_load_block<T, EPL, LPS>(k, Bsl, sc, bt, b, j);
     const T* qf = sc + 4 * b * MGX_SCAL + MGX_SQ(1, 0);
     bool ok = b < nblk;
     T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[1] : (T)0, f2 = ok ? qf[2] : (T)0, f3 = ok ? qf[3] : (T)0;
@@ -631,10 +711,10 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   T cpart = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL>(k, Bsl, sc, bt, b, j);
+    pgs_load_block<T, EPL, LPS>(k, Bsl, sc, bt, b, j);
     T d0, d1, d2, d3;
     pgs_dots(k, v, d0, d1, d2, d3);
-    oct_sum4(d0, d1, d2, d3);
+    slot_sum4<LPS>(d0, d1, d2, d3);
     if (b < nblk) {
       T dd[4] = {d0, d1, d2, d3};
       const T* qq = sc + 4 * b * MGX_SCAL;
@@ -646,7 +726,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     }
   }
   if (cpart > 0) {
-    for (int r = j; r < ne; r += MGX_PGS_LPS) sc[(r >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, r & 3)] = 0;
+    for (int r = j; r < ne; r += LPS) sc[(r >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, r & 3)] = 0;
 #pragma unroll
     for (int d = 0; d < EPL; d++) v[d] = 0;
   }
@@ -664,19 +744,25 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     nsweep++;
 #endif
     T impr = 0;
-    PgsBlk<T, EPL> R[MGX_PGS_RING];
+    PgsBlk<T, EPL> R[RING];
+    PgsTab<EPL> tn;  // the table entry of the next block to load (one ring step ahead of its data)
+    pgs_load_tab<EPL, LPS>(tn, bt, 0, j);
 #pragma unroll
-    for (int k = 0; k < MGX_PGS_RING - 1; k++) pgs_load_block<T, EPL>(R[k], Bsl, sc, bt, k, j);
-    // full groups of 3 blocks (ring of 3, 2 ahead): no early exit inside, so every prefetch is
-    // consumed on every path and the compiler cannot sink the loads next to their use. The
-    // table has zero entries up to its capacity, so the look-ahead past nbMax reads zeros.
-    for (int b0 = 0; b0 < nbRun; b0 += MGX_PGS_RING) {
+    for (int k = 0; k < RING - 1; k++) {
+      pgs_load_block<T, EPL, LPS>(R[k], Bsl, sc, tn, k, j);
+      pgs_load_tab<EPL, LPS>(tn, bt, k + 1, j);
+    }
+    // full ring turns, no early exit inside, so every prefetch is consumed on every path and
+    // the compiler cannot sink the loads next to their use. The table has zero entries up to
+    // nbA, so the look-ahead past nbMax reads zeros.
+    for (int b0 = 0; b0 < nbRun; b0 += RING) {
 #pragma unroll
-      for (int k = 0; k < MGX_PGS_RING; k++) {
+      for (int k = 0; k < RING; k++) {
         // the slot consumed last lands the block RING - 1 ahead, then block b0 + k is solved
-        pgs_load_block<T, EPL>(R[(k + MGX_PGS_RING - 1) % MGX_PGS_RING], Bsl, sc, bt,
-                               min(b0 + k + MGX_PGS_RING - 1, nbcap3 - 1), j);
-        pgs_block<T, EPL>(R[k], v, sc, 4 * (b0 + k), act && b0 + k < nblk, impr);
+        const int bn = min(b0 + k + RING - 1, nbA - 1);
+        pgs_load_block<T, EPL, LPS>(R[(k + RING - 1) % RING], Bsl, sc, tn, bn, j);
+        pgs_load_tab<EPL, LPS>(tn, bt, min(bn + 1, nbA - 1), j);
+        pgs_block<T, EPL, LPS>(R[k], v, sc, 4 * (b0 + k), act && b0 + k < nblk, impr);
       }
     }
     if (act) {
@@ -700,16 +786,18 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
 #pragma unroll
     for (int d = 0; d < EPL; d++)
       {
-        const int dof = 8 * (MGX_PGS_LPS == 8 ? d : 2 * d + (j >> 3)) + (j & 7);
+        const int dof = 8 * (d * (LPS / 8) + (j >> 3)) + (j & 7);
         if (dof < P.nv) vo[dof] = v[d];
       }
     if (j == 0) P.at<int>(P.o_niter)[slot] = it;
   }
 }
 
-// big = 0: the main launch (one wave per 8 listed slots, rows <= capE in LDS); big = 1: the
-// slots with capE < nefc <= maxE, grid-stride over a small grid with maxE rows of LDS per slot
-template <typename T, int EPL>
+// big = 0: the main launch over the solver list (one wave per 64 / LPS listed slots); big = 1:
+// the slots with capE < nefc <= maxE and those of LDS-arena waves that did not fit, grid-stride
+// over a small grid with maxE rows of scalars per slot in LDS. BLDS (main launch only): B in
+// the wave's LDS arena; otherwise B is read from global memory (L2 / MALL).
+template <typename T, int EPL, int LPS, bool BLDS>
 __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw, int big) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (!big && blockIdx.x == 0 && threadIdx.x == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
@@ -717,7 +805,7 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   const int* list = P.at<int>(big ? P.o_k2big : P.o_k2list);
   const int spn = spw < 0 ? -spw : spw;
   for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
-    pgs_group<T, EPL>(P, smem, list, cnt, base, big ? P.maxE : P.capE, maxit, tol, scale, spw);
+    pgs_group<T, EPL, LPS, BLDS && true>(P, smem, list, cnt, base, big ? P.maxE : P.capE, maxit, tol, scale, spw);
     __syncthreads();  // the next group reuses the LDS
   }
 }

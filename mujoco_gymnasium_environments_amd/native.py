@@ -107,6 +107,7 @@ _SIGS = {
     "mgx_soccer_logic_test": ([_VP, C.POINTER(cabi.MgxSoccerLogicIO), C.c_int, _VP], C.c_int),
     "mgx_soccer_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
     "mgx_soccer_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
+    "mgx_soccer_workspace_layout": ([_VP, C.c_int, C.c_int, C.POINTER(C.c_int64), C.c_int], C.c_int),
     "mgx_parkour_configure": ([_VP, C.POINTER(cabi.MgxParkourIds)], C.c_int),
     "mgx_parkour_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxParkourEnv), _VP, _VP, _VP, _VP, _VP,
                           _VP, C.c_int, C.c_uint64, C.c_int, C.c_int, _VP, _VP], C.c_int),

@@ -65,6 +65,46 @@ def test_wide_solver_launch_bit_identical(soccer_model, prec):
     assert EFC_CAPACITY == 384
 
 
+class _Env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_lds_arena_solver_bit_identical(soccer_model, prec):
+    """The main solver launch with B copied into an LDS arena (MGX_PGS_LDS_B=1; a small arena so
+    that some waves do not fit and go to the global-B launch) runs the identical arithmetic as
+    the default global-B launch: the same states, bit for bit."""
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    n, steps = 64, 25
+    a = SoccerVectorEnv(n, precision=prec, seed=33)
+    b = SoccerVectorEnv(n, precision=prec, seed=33)
+    a.reset()
+    b.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(7)
+    for t in range(steps):
+        act = torch.rand(n, soccer_model.nu, device="cuda:0", generator=g) * 300 - 150
+        ra = a.step(act)
+        with _Env(MGX_PGS_LDS_B="1", MGX_PGS_ARENA="24576"):
+            rb = b.step(act)
+        torch.cuda.synchronize()
+        for x, y, name in zip(ra[:4], rb[:4], ("obs", "reward", "terminated", "truncated")):
+            assert torch.equal(x, y), (t, name)
+        assert torch.equal(a.batch.qpos, b.batch.qpos) and torch.equal(a.batch.qvel, b.batch.qvel), t
+
+
 def test_rows_over_main_launch_match_oracle(soccer_model, soccer_packed):
     """fp64 end to end (reset draws + 25 random-action steps, obs 1e-5, reward 1e-6 relative,
     flags exact) with every slot over the lowered LDS threshold."""

@@ -127,7 +127,7 @@ def main():
     n = int(os.environ.get("N", "4096"))
     steps = int(os.environ.get("K", "20"))
     staged = os.environ.get("MODE", "staged") == "staged"
-    env = SoccerVectorEnv(n, seed=3, staged=staged)
+    env = SoccerVectorEnv(n, seed=3, staged=staged, precision=os.environ.get("PREC", "f64"))
     env.reset()
     nslot = n * 5 if staged else n
     buf = torch.zeros(nslot * 32, dtype=torch.int64, device="cuda:0")
