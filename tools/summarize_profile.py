@@ -1,9 +1,9 @@
 """Summarise a tools/profile_round.sh run into small committed files under profiles/.
 
-One env step is several launches (staged: k_soccer_rows, k_pgs_groups, k_soccer_finish,
-k_soccer_fixup; monolithic: k_soccer<.., 0>), each called once per step: the step's kernel
-time is the sum of their rocprof averages, and its HBM traffic the sum of their per-dispatch
-counter means. HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
+One env step is several launches (staged: k_soccer_rows, k_pgs_groups twice — main and global-B
+launch —, k_soccer_finish, k_soccer_fixup; monolithic: k_soccer<.., 0>): the step's kernel time
+is the sum of their rocprof averages times their calls per step, and its HBM traffic the same
+sum over their per-dispatch counter means. HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB, collected in separate passes; on gfx950 FETCH_SIZE counts half the bytes of a wide
 coalesced read, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (raw values kept too).
 """
@@ -61,7 +61,12 @@ def main(out, tag):
             if k:
                 res["kernels"][k] = {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"]),
                                      "pct": float(r["Percentage"])}
-        res["rocprof_step_ms"] = sum(v["avg_ms"] for v in res["kernels"].values())
+        # a kernel may run more than once per step (the staged solver: main launch + global-B
+        # launch); the step count is the fewest calls of any step kernel
+        nstep = min(v["calls"] for v in res["kernels"].values()) if res["kernels"] else 1
+        for v in res["kernels"].values():
+            v["per_step"] = v["calls"] / nstep
+        res["rocprof_step_ms"] = sum(v["avg_ms"] * v["per_step"] for v in res["kernels"].values())
     bj = os.path.join(out, "bench_under_rocprof.json")
     if os.path.exists(bj):
         line = [x for x in open(bj).read().splitlines() if x.startswith("{")]
@@ -81,7 +86,7 @@ def main(out, tag):
             kk["fetch_kib_raw"] = fetch.get(k, 0.0)
             kk["write_kib_raw"] = write.get(k, 0.0)
             kk["hbm_bytes"] = (2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024
-        res["hbm_bytes_per_step"] = sum(v.get("hbm_bytes", 0.0) for v in res["kernels"].values())
+        res["hbm_bytes_per_step"] = sum(v.get("hbm_bytes", 0.0) * v.get("per_step", 1.0) for v in res["kernels"].values())
         res["correction"] = "(2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md §HBM"
     with open(os.path.join(summ, f"{tag}_pmc.json"), "w") as f:
         json.dump(res, f, indent=1)
