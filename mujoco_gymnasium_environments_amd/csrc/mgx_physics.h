@@ -652,13 +652,70 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
   wsync();
 }
 
+#ifndef MGX_TRANSFORM_LANE_ROW
+#define MGX_TRANSFORM_LANE_ROW 0  // 1: the lane-per-row transform for narrow models too (A/B builds)
+#endif
 // B_r = D^-1/2 L'^-1 J_r' in place (lane per row), sqrtdi in vec0. Rows in global scratch
 // (Layout.gB) are staged through LDS in chunks of L.tchunk rows (the phase-A union is dead once
 // the rows exist): coalesced row copies in and out (lane = dof), the lane-per-row transform on
 // LDS, instead of lane-strided global read-modify-writes along every row.
+//
+// Narrow models (nv <= 64) instead go four rows at a time, row-major (lane = dof): the rows are
+// loaded coalesced (the next four in flight), and L'^-1 runs as a readlane sweep over the
+// rows' dof support only — highest dof first, each dof's ancestors joining the support as it is
+// reached — with x_anc -= L[k][anc] x_k as one FMA per row per step (the same operations in the
+// same order as transform_row), then the D^-1/2 scale and one coalesced store per row. A
+// contact row's support is two body chains (~10-20 of nv dofs), so a block costs tens of
+// steps, where the lane-per-row walk visits all nv dofs of every row.
+template <typename T>
+__device__ __forceinline__ void transform_rows_rm(const DevModel<T>& m, Env<T>& e) {
+  const int l = lane_id(), nv = m.nv;
+  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+  const bool dl = l < nv;
+  const int lc = dl ? l : 0;
+  T* Bm = e.Bm;
+  const int Bs = e.Bs;
+  const T dinvs = dl ? e.vec0[l] : (T)0;
+  auto ld4 = [&](int r0, T& a, T& b, T& c, T& d) {
+    a = (dl && r0 < ne) ? Bm[r0 * Bs + lc] : (T)0;
+    b = (dl && r0 + 1 < ne) ? Bm[(r0 + 1) * Bs + lc] : (T)0;
+    c = (dl && r0 + 2 < ne) ? Bm[(r0 + 2) * Bs + lc] : (T)0;
+    d = (dl && r0 + 3 < ne) ? Bm[(r0 + 3) * Bs + lc] : (T)0;
+  };
+  T n0, n1, n2, n3;
+  ld4(0, n0, n1, n2, n3);
+  for (int r0 = 0; r0 < ne; r0 += 4) {
+    T x0 = n0, x1 = n1, x2 = n2, x3 = n3;
+    if (r0 + 4 < ne) ld4(r0 + 4, n0, n1, n2, n3);
+    uint64_t sp = ballot(x0 != (T)0 || x1 != (T)0 || x2 != (T)0 || x3 != (T)0);
+    while (sp) {
+      const int k = 63 - __clzll(sp);
+      const uint64_t am = readlane_u64(e.ancmask, k);
+      sp = (sp & ~(1ull << k)) | am;  // ancestors have lower indices: visited later in the sweep
+      const int base = readlane(e.madr, k) + readlane(e.chainlen, k) - e.chainlen;
+      const T coef = (dl && ((am >> l) & 1ull)) ? e.qLD[base > 0 ? base : 0] : (T)0;
+      const T k0 = readlane(x0, k), k1 = readlane(x1, k), k2 = readlane(x2, k), k3 = readlane(x3, k);
+      x0 -= coef * k0; x1 -= coef * k1; x2 -= coef * k2; x3 -= coef * k3;
+    }
+    if (dl) {
+      if (r0 < ne) Bm[r0 * Bs + l] = x0 * dinvs;
+      if (r0 + 1 < ne) Bm[(r0 + 1) * Bs + l] = x1 * dinvs;
+      if (r0 + 2 < ne) Bm[(r0 + 2) * Bs + l] = x2 * dinvs;
+      if (r0 + 3 < ne) Bm[(r0 + 3) * Bs + l] = x3 * dinvs;
+    }
+  }
+  wsync();
+}
+
 template <typename T, bool WIDE = false>
 __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
+  if constexpr (!WIDE) {
+    if (!(MGX_TRANSFORM_LANE_ROW)) {
+      transform_rows_rm(m, e);
+      return;
+    }
+  }
   const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
   const int C = m.L.tchunk;
   if (m.L.gB && C > 0) {
