@@ -185,7 +185,8 @@ __global__ void __launch_bounds__(64) k_wide_debug(DevModel<T> m, mgx_state s, i
     if (d < m.nv) e.vec0[d] = sqrt(w.diaginv[k]);
   }
   wsync();
-  transform_rows<T, true>(m, e);
+  if (MGX_TRANSFORM_LANE_ROW) transform_rows<T, true>(m, e);
+  else wtransform_rows(m, w);  // as wforward
   wsync();
   for (int r = l; r < e.nefc; r += 64)
     for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];

@@ -571,6 +571,55 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
 }
 
 // ---------------------------------------------------------------- forward + step
+// B_r = D^-1/2 L'^-1 J_r' in place, four rows at a time, row-major with two dofs per lane (the
+// narrow transform_rows_rm with two-word rows): a readlane sweep over the rows' dof support
+// (128-bit, ancestors joining as their descendants are reached), highest dof first.
+template <typename T>
+__device__ __forceinline__ void wtransform_rows(const DevModel<T>& m, WEnv<T>& w) {
+  Env<T>& e = w.e;
+  const int l = lane_id(), nv = m.nv;
+  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+  const bool v0 = l < nv, v1 = 64 + l < nv;
+  T* Bm = e.Bm;
+  const int Bs = e.Bs;
+  const T s0 = v0 ? e.vec0[l] : (T)0, s1 = v1 ? e.vec0[64 + l] : (T)0;
+  for (int r0 = 0; r0 < ne; r0 += 4) {
+    T x[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const bool ok = r0 + i < ne;
+      x[i][0] = (ok && v0) ? Bm[(r0 + i) * Bs + l] : (T)0;
+      x[i][1] = (ok && v1) ? Bm[(r0 + i) * Bs + 64 + l] : (T)0;
+    }
+    uint64_t sp_lo = ballot(x[0][0] != (T)0 || x[1][0] != (T)0 || x[2][0] != (T)0 || x[3][0] != (T)0);
+    uint64_t sp_hi = ballot(x[0][1] != (T)0 || x[1][1] != (T)0 || x[2][1] != (T)0 || x[3][1] != (T)0);
+    while (sp_lo | sp_hi) {
+      const int k = sp_hi ? 127 - __clzll(sp_hi) : 63 - __clzll(sp_lo);
+      if (k >= 64) sp_hi &= ~(1ull << (k - 64)); else sp_lo &= ~(1ull << k);
+      const uint64_t alo = m.dof_ancmask[k], ahi = m.dof_ancmask_hi[k];
+      sp_lo |= alo;  // ancestors have lower indices: visited later in the sweep
+      sp_hi |= ahi;
+      const int base = m.dof_Madr[k] + m.dof_chainlen[k];
+      const T c0 = (v0 && ((alo >> l) & 1ull)) ? e.qLD[base - w.chainlen[0]] : (T)0;
+      const T c1 = (v1 && ((ahi >> l) & 1ull)) ? e.qLD[base - w.chainlen[1]] : (T)0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const T xk = wread(x[i], k);
+        x[i][0] -= c0 * xk;
+        x[i][1] -= c1 * xk;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (r0 + i < ne) {
+        if (v0) Bm[(r0 + i) * Bs + l] = x[i][0] * s0;
+        if (v1) Bm[(r0 + i) * Bs + 64 + l] = x[i][1] * s1;
+      }
+    }
+  }
+  wsync();
+}
+
 template <typename T>
 __device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
   Env<T>& e = w.e;
@@ -606,7 +655,8 @@ __device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
     if (d < m.nv) e.vec0[d] = sqrt(w.diaginv[k]);
   }
   wsync();
-  transform_rows<T, true>(m, e);
+  if (MGX_TRANSFORM_LANE_ROW) transform_rows<T, true>(m, e);
+  else wtransform_rows(m, w);
   MGX_STAMP(7);
   wnewton(m, w);
   MGX_STAMP(8);
