@@ -248,87 +248,6 @@ __device__ __forceinline__ void whessian(const T* Bm, int Bs, const T* efc, int 
   whess_pass<T, 7, 8>(Bm, Bs, efc, ne, nv, H);  // 8 tiles
 }
 
-// ---------------------------------------------------------------- blocked Cholesky
-// H = L L' in place (lower triangle of the row-major nv x nv H, nv <= 128), right-looking in
-// 16-wide block columns: factor the diagonal block (lanes = its rows, one wave barrier per
-// column, <= 15-term dots), solve the panel below it against L_kk' (lane = row, L_kk read as LDS
-// broadcasts), then subtract L_I L_J' from every trailing lower tile on MFMA (16x16x4: four
-// per tile, accumulators initialised from the tile). Entries past nv read as 0 and are never
-// stored. Same pivot clamp as the unblocked factor (d = sqrt(max(dkk, minval))).
-template <typename T>
-__device__ __forceinline__ void wchol_blocked(T* H, int nv) {
-  typedef T V4 __attribute__((ext_vector_type(4)));
-  const int l = lane_id();
-  const int nb = (nv + 15) >> 4;
-  for (int kb = 0; kb < nb; kb++) {
-    const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
-    // 1. diagonal block, left-looking within the block: lane i < bk owns row k0 + i
-    for (int c = 0; c < bk; c++) {
-      const bool act = l < bk && l >= c;
-      const int r = k0 + (act ? l : c);
-      const T* Lr = H + r * nv + k0;
-      const T* Lc = H + (k0 + c) * nv + k0;
-      T s = Lr[c];
-      for (int j = 0; j < c; j++) s -= Lr[j] * Lc[j];
-      const T dkk = readlane(s, c);
-      const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
-      if (act) H[r * nv + k0 + c] = l == c ? d : s / d;
-      wsync();
-    }
-    // 2. panel: rows below the block, x = a L_kk^-T by forward substitution (lane = row)
-    const T* Lkk = H + k0 * nv + k0;
-    for (int r = k0 + bk + l; r < nv + 64 && r - l < nv; r += 64) {
-      if (r < nv) {
-        T* Ar = H + r * nv + k0;
-        T x[16];
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-          if (c < bk) {
-            T t = Ar[c];
-#pragma unroll
-            for (int j = 0; j < c; j++) t -= x[j] * Lkk[c * nv + j];
-            x[c] = t / Lkk[c * nv + c];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 16; c++)
-          if (c < bk) Ar[c] = x[c];
-      }
-    }
-    wsync();
-    // 3. trailing lower tiles (I, J), kb < J <= I < nb: A_IJ -= L_Ik L_Jk' on MFMA
-    const int i = l & 15, kq = l >> 4;
-    auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
-    for (int I = kb + 1; I < nb; I++) {
-      for (int J = kb + 1; J <= I; J++) {
-        V4 acc;
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-          const int row = 16 * I + row_of(v), col = 16 * J + i;
-          acc[v] = (row < nv && col < nv) ? H[row * nv + col] : (T)0;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int kk = k0 + 4 * q + kq;  // this lane's k in the 16-wide block column
-          const int ra = 16 * I + i, rb = 16 * J + i;
-          const T a = (ra < nv && kk < k0 + bk) ? -H[ra * nv + kk] : (T)0;
-          const T b = (rb < nv && kk < k0 + bk) ? H[rb * nv + kk] : (T)0;
-          if constexpr (sizeof(T) == 8)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-          else
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-          const int row = 16 * I + row_of(v), col = 16 * J + i;
-          if (row < nv && col <= row) H[row * nv + col] = acc[v];
-        }
-      }
-    }
-    wsync();
-  }
-}
-
 // ---------------------------------------------------------------- Newton (mj_solNewton)
 // newton() of mgx_physics.h with two-word dof vectors; same whitened coordinates, row scalars
 // (q[0] b, q[1] x / force, q[2] R, q[3] B_r.p, q[4] D, q[5] aref, q[6] B damping), the same line
@@ -431,7 +350,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     whessian(Bm, Bs, efc, ne, nv, H);
     wsync();
     MGX_STAMP(11);  // Hessian
-    wchol_blocked(H, nv);
+    chol_blocked(H, nv);
     MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y
     T rdiag[2];
