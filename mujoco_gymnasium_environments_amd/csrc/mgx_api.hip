@@ -400,8 +400,16 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   const int union_tail = align_up(3 * ng, al) + align_up(9 * ng, al) + align_up(d->nu, al);
   const bool staged_overlay = staged && nb12 + cf9 + cp3 <= union_dead &&
                               nb12 + cf9 + cp3 + align_up(4 * max_nefc, al) <= union_dead + union_tail;
-  if (!hess_union && !staged_overlay) { L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon); }
-  L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged ? 1 : max_nefc);
+  // monolithic PGS models with rows in global scratch: the contact points / frames, the row
+  // margins (make_constraint only) and the broadphase survivor list (collision only) overlay
+  // xmat .. xanchor of the union, dead once the velocity stage is done (bipedal: 62.4 -> 51.4 KiB,
+  // three envs per CU instead of two)
+  const int cvel_sz = align_up(6 * nb, al);
+  const int act_r = align_up((max_active * 4 + real_bytes - 1) / real_bytes, al);
+  const bool mono_overlay = gB && !staged && !hess_union && !(d->layout_flags & MGX_KEEP_CVEL) &&
+                            cp3 + cf9 + align_up(max_nefc, al) + act_r <= union_dead + cvel_sz;
+  if (!hess_union && !staged_overlay && !mono_overlay) { L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon); }
+  L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged || mono_overlay ? 1 : max_nefc);
   L.efc_blk = take(staged || hess_union ? 1 : 2 * max_nefc);
   L.hess = (!staged && d->solver == 2 && !hess_union) ? take(nv * nv) : 0;
   // env logic that reads cvel after the step (martial arts, martial_arts_env.py:536-589) keeps
@@ -423,6 +431,14 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   // stage, over xmat .. crb (dead by then; cvel, read with it, lies beyond them)
   L.cacc = L.xmat;
   int endA = p;
+  L.act_union = 0;
+  if (mono_overlay) {
+    int o = u0;
+    L.con_pos = o; o += cp3;
+    L.con_frame = o; o += cf9;
+    L.efc_margin = o; o += align_up(max_nefc, al);
+    L.act_union = o;
+  }
   if (staged_overlay) {
     // xmat .. xanchor are dead once the velocity stage is done: the contact frames and points
     // (written by collision, read by the row blocks) follow cacc there; the row constants

@@ -48,6 +48,9 @@ struct Layout {
   int tchunk;
   // Newton solver (solver == mjSOL_NEWTON, monolithic kernels only): nv x nv Hessian
   int hess;
+  // > 0: the broadphase survivor list lives at this real offset (inside the dead phase-A
+  // union) instead of the int region (monolithic rows-in-scratch PGS models)
+  int act_union;
 };
 
 // Device-resident model: pointers into one device allocation.

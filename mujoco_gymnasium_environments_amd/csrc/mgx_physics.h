@@ -56,7 +56,8 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.rk = R + L.rk;
   e.hess = R + L.hess;
   int* I = reinterpret_cast<int*>(R + L.reals);
-  e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair; e.act_list = I + L.act_list;
+  e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair;
+  e.act_list = L.act_union > 0 ? reinterpret_cast<int*>(R + L.act_union) : I + L.act_list;
   e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id; e.con_efcadr = I + L.con_efcadr;
   int l = lane_id();
   e.chainlen = l < m.nv ? m.dof_chainlen[l] : 0;

@@ -81,12 +81,16 @@ __global__ void __launch_bounds__(64) k_debug_forward(DevModel<T> m, mgx_state s
   for (int k = l; k < m.nM; k += 64) D[o.qLD + k] = e.qLD[k];
   velocity(m, e);
   e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
-  collision(m, e);
+  // the phase-A arrays before collision: with rows in global scratch the contact arrays overlay
+  // them from collision on (make_layout, mono_overlay)
   wsync();
   for (int k = l; k < 3 * m.nbody; k += 64) D[o.xipos + k] = e.xipos[k];
   for (int k = l; k < 10 * m.nbody; k += 64) D[o.cinert + k] = e.cinert[k];
   for (int k = l; k < 6 * m.nv; k += 64) D[o.cdof_dot + k] = e.cdof_dot[k];
   for (int k = l; k < 6 * m.nbody; k += 64) D[o.cvel + k] = e.cvel[k];
+  wsync();
+  collision(m, e);
+  wsync();
   for (int k = l; k < 3 * m.ngeom; k += 64) D[o.geom_xpos + k] = e.geom_xpos[k];
   for (int k = l; k < 9 * m.ngeom; k += 64) D[o.geom_xmat + k] = e.geom_xmat[k];
   // contacts before the solve: with a Newton model in gB mode their frames share LDS with the
