@@ -502,7 +502,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
-    ap.add_argument("--banks", type=int, default=4)
+    ap.add_argument("--banks", type=int, default=3, help="reset banks per env (3: measured fastest, DESIGN.md §4)")
     ap.add_argument("--full-capacity", action="store_true",
                     help="soccer: 96 contacts / 384 rows per env instead of 64 / 192 (no overflow, slower)")
     ap.add_argument("--streams", type=int, default=1,

@@ -133,7 +133,7 @@ class SoccerVectorEnv:
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
-                 staged: bool = True, banks: int = 4, full_capacity: bool = False):
+                 staged: bool = True, banks: int = 3, full_capacity: bool = False):
         """``staged`` selects the row-builder / lane-group PGS / finisher kernels
         with ``banks`` precomputed resets per env; ``staged=False`` runs one monolithic wave per
         env. Both compute the same step (parity-tested against each other and the oracle).
@@ -271,7 +271,7 @@ class StreamShardedSoccerEnv:
 
     def __init__(self, num_envs: int, n_streams: int = 2, device: str = "cuda:0", precision: str = "f32",
                  seed: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True,
-                 env_offset: int = 0, staged: bool = True, banks: int = 4):
+                 env_offset: int = 0, staged: bool = True, banks: int = 3):
         if n_streams < 1 or n_streams > num_envs:
             raise ValueError("need 1 <= n_streams <= num_envs")
         self.num_envs = num_envs

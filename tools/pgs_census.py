@@ -35,7 +35,7 @@ def main():
     env = SoccerVectorEnv(a.envs, device=str(dev), precision=a.precision, seed=1234)
     env.reset(seed=1234)
     lay = (C.c_int64 * 10)()
-    assert lib().mgx_soccer_workspace_layout(env.native.handle, a.envs, 4, lay, 10) == 0
+    assert lib().mgx_soccer_workspace_layout(env.native.handle, a.envs, int(env._env.banks), lay, 10) == 0
     o_ctr, o_ne, o_list, o_blk, o_B, bcap, maxE, capE, S, rb = list(lay)
     g = torch.Generator(device=dev)
     g.manual_seed(1000)
