@@ -31,7 +31,7 @@ namespace mgx {
 #define MGX_SQ(k, i) (4 * (k) + (i))
 #define MGX_PGS_LPS 16         // solver: lanes per slot (16 or 64; MGX_PGS_LPS env overrides per process)
 #define MGX_PGS_LDS_B 0        // main solver launch: 1 = B in an LDS arena, 0 = B from global memory
-#define MGX_PGS_RING 3         // global-B solver: register ring of 4-row blocks (RING - 1 in flight; 4 measured no faster)
+#define MGX_PGS_RING 2         // global-B solver: register ring of 4-row blocks (RING - 1 in flight; 3 and 4 measured no faster)
 #define MGX_PGS_RING_LDS 2     // LDS-B solver: one block in flight covers the LDS latency
 #define MGX_PGS_LDS_ROWS 192   // rows per slot the main solver launch keeps in LDS (2 waves / CU in fp64)
 #define MGX_PGS_WIDE_GRID 256  // waves of the global-B launch (slots over MGX_PGS_LDS_ROWS, waves over their arena)
