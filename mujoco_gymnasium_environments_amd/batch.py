@@ -33,7 +33,7 @@ def stream_handle(stream: Optional[torch.cuda.Stream] = None):
 class NativeModel:
     """Device-resident model constants (mgx_model_create)."""
 
-    def __init__(self, model: mjcf.Model, precision: str = "f32", device: int = 0):
+    def __init__(self, model: mjcf.Model, precision: str = "f64", device: int = 0):
         self.model = model
         self.packed = cabi.pack_model(model)
         self.precision = precision
@@ -57,7 +57,7 @@ class NativeModel:
 
 
 class PhysicsBatch:
-    def __init__(self, model: mjcf.Model, n_env: int, precision: str = "f32", device: str = "cuda:0",
+    def __init__(self, model: mjcf.Model, n_env: int, precision: str = "f64", device: str = "cuda:0",
                  native: Optional[NativeModel] = None):
         self.model = model
         self.n = n_env

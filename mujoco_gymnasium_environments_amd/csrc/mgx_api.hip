@@ -758,7 +758,8 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // up to 768 for large ones (bipedal 3185 pairs)
   int max_active = d->npair <= 256 ? 128 : (d->npair < 768 ? d->npair : 768);
   // the staged soccer pipeline handles Euler + PGS models up to 64 * MGX_EFC_SLOTS rows
-  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS && condim13;
+  m->staged_ok = d->integrator == 0 && d->solver == 0 && max_nefc <= 64 * MGX_EFC_SLOTS && condim13 &&
+                 d->nv <= 56;  // the solver's block table holds 7 dof groups of 8 (pgs_load_tab)
   // the monolithic layout of a staged model (its reset settle steps, the rare fixup resets,
   // --mono, mgx_debug_forward) keeps rows in LDS at the default 192 rows / 64 contacts; the
   // staged step itself carries the model's full capacity

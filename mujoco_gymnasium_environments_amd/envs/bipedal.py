@@ -109,7 +109,7 @@ class BipedalVectorEnv:
 
     metadata = {'render_modes': [], 'render_fps': 50}
 
-    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
+    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
         self.num_envs = num_envs
         self.device = torch.device(device)
@@ -218,7 +218,7 @@ class BipedalRescueEnv(EnvBase):
 
     metadata = {'render_modes': ['human', 'rgb_array', 'depth_array'], 'render_fps': 50}
 
-    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f32", **kwargs):
+    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f64", **kwargs):
         super().__init__()
         self.render_mode = render_mode
         self.dt = 0.02

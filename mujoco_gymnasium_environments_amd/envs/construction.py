@@ -164,8 +164,15 @@ class ConstructionVectorEnv:
 
 class HumanoidConstructionEnv(EnvBase):
     """Drop-in for humanoid_construction_env.construction_env.HumanoidConstructionEnv on libmgx.
-    Actions are taken as float32 (the reference clips them against its float32 action_space
-    bounds, so the clipped action and its energy term are float32)."""
+    Actions are taken as float32. For float32 input (``action_space.sample()``, float32 policies)
+    this is exactly the reference, which clips against its float32 action_space bounds. A float64
+    action stays float64 in the reference's clip, so its ``ctrl`` and energy term then differ from
+    this env's at the rounding of the float32 cast (documented quirk).
+
+    ``info['episode_stats']['total_reward']`` is the running total *before* this step's reward:
+    the reference copies ``episode_stats`` into ``info`` (construction_env.py:613-614, :746) and
+    only then adds the reward (:617). It is a Python 0.0 until the first reward has been added,
+    np.float32 after (NEP 50: Python float + np.float32 stays float32)."""
 
     metadata = {'render_modes': ['human', 'rgb_array'], 'render_fps': 50}
 
@@ -199,6 +206,7 @@ class HumanoidConstructionEnv(EnvBase):
         obs, _ = self._vec.reset(draws=draws)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = 0
+        self._total_before = 0.0
         return obs[0].cpu().numpy().copy(), self._info()
 
     def step(self, action: np.ndarray):
@@ -206,14 +214,16 @@ class HumanoidConstructionEnv(EnvBase):
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = int(self._vec.ints[0, 1])
-        return obs[0].cpu().numpy().copy(), np.float32(rew[0].item()), bool(term[0]), bool(trunc[0]), self._info()
+        info = self._info()  # the total as it was before this step's reward (construction_env.py:614-617)
+        self._total_before = np.float32(self._vec.total_reward[0].item())
+        return obs[0].cpu().numpy().copy(), np.float32(rew[0].item()), bool(term[0]), bool(trunc[0]), info
 
     def _info(self) -> Dict[str, Any]:
         v = self._vec
         sc = v.scal[0].cpu().numpy()
         it = v.ints[0].cpu().numpy()
         self.current_task = TASKS[int(it[0])]
-        stats = dict(zip(STAT_KEYS, [0, 0, 0, 0, int(it[4]), np.float32(v.total_reward[0].item())]))
+        stats = dict(zip(STAT_KEYS, [0, 0, 0, 0, int(it[4]), getattr(self, '_total_before', 0.0)]))
         return {'task': self.current_task, 'task_progress': float(sc[0]), 'blocks_placed': int(it[2]),
                 'safety_violations': int(it[3]), 'episode_stats': stats,
                 'weather': {'wind': float(sc[1]), 'rain': float(sc[2]), 'temperature': float(sc[3])}}

@@ -105,7 +105,7 @@ class ParkourVectorEnv:
 
     metadata = {'render_modes': [], 'render_fps': 100}
 
-    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
+    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
                  rows_in_scratch: Optional[bool] = None):
         self.num_envs = num_envs
@@ -208,7 +208,7 @@ class QuadrupedParkourEnv(EnvBase):
 
     metadata = {'render_modes': ['human', 'rgb_array'], 'render_fps': 100}
 
-    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f32", **kwargs):
+    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f64", **kwargs):
         super().__init__()
         self.render_mode = render_mode
         self.dt = 0.01

@@ -131,7 +131,7 @@ class SoccerVectorEnv:
 
     metadata = {'render_modes': [], 'render_fps': 50}
 
-    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f32", seed: int = 0,
+    def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
                  staged: bool = True, banks: int = 3, full_capacity: bool = False):
         """``staged`` selects the row-builder / lane-group PGS / finisher kernels
@@ -139,6 +139,9 @@ class SoccerVectorEnv:
         env. Both compute the same step (parity-tested against each other and the oracle).
         ``full_capacity`` raises the staged step's capacity from 64 contacts / 192 rows to
         96 / 384 (see soccer_model)."""
+        if full_capacity and not staged:
+            # the monolithic layout holds 64 contacts / 192 rows whatever the model's capacity
+            raise ValueError("full_capacity needs the staged pipeline (staged=True)")
         self.num_envs = num_envs
         self.device = torch.device(device)
         self.model = soccer_model(full_capacity)
@@ -269,7 +272,7 @@ class StreamShardedSoccerEnv:
     ones a single SoccerVectorEnv over all envs produces (tests/test_gpu_f32_staged.py). obs /
     reward / flags / final_obs are one tensor each; the shards write into row slices of it."""
 
-    def __init__(self, num_envs: int, n_streams: int = 2, device: str = "cuda:0", precision: str = "f32",
+    def __init__(self, num_envs: int, n_streams: int = 2, device: str = "cuda:0", precision: str = "f64",
                  seed: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True,
                  env_offset: int = 0, staged: bool = True, banks: int = 3):
         if n_streams < 1 or n_streams > num_envs:
@@ -355,7 +358,7 @@ class HumanoidSoccerEnv(EnvBase):
 
     metadata = {'render_modes': ['human', 'rgb_array', 'depth_array'], 'render_fps': 50}
 
-    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f32", **kwargs):
+    def __init__(self, render_mode: Optional[str] = None, device: str = "cuda:0", precision: str = "f64", **kwargs):
         super().__init__()
         self.dt = 0.02
         self.max_episode_steps = MAX_EPISODE_STEPS

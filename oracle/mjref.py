@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libmjref.so")
+# MJREF_LIB selects another build of the same source (the sanitizer build, `make asan`)
+LIB_PATH = os.environ.get("MJREF_LIB") or os.path.join(HERE, "_build", "libmjref.so")
 _INT_FIELDS = {"warning", "ncon", "con_geom", "con_dim", "con_pair", "nefc", "efc_type", "efc_id",
                "solver_niter"}
 _lib = None
@@ -26,7 +27,7 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if os.path.exists(os.path.join(HERE, "Makefile")):
+        if os.path.exists(os.path.join(HERE, "Makefile")) and not os.environ.get("MJREF_LIB"):
             build()  # make: rebuilds when mjref.c / mjref.h / include/mgx.h changed
         elif not os.path.exists(LIB_PATH):
             raise FileNotFoundError(LIB_PATH)

@@ -146,7 +146,7 @@ def test_vector_env_end_to_end_f64(soccer_model, soccer_packed):
 
 def test_vector_env_autoreset_and_sharding_invariance(soccer_model):
     """Device reset draws are keyed by global env index: env k of a 2-env shard at offset 2
-    reproduces env 2+k of a 4-env run, bit for bit (fp32), including autoresets."""
+    reproduces env 2+k of a 4-env run, bit for bit (the default fp64), including autoresets."""
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     full = SoccerVectorEnv(4, seed=11)
     part = SoccerVectorEnv(2, seed=11, env_offset=2)
