@@ -114,8 +114,8 @@ __device__ __forceinline__ void soccer_step_mono(const DevModel<T>& m, Env<T>& e
   }
 }
 
-// soccer: MODE 0 = step (+ optional same-step autoreset), MODE 1 = reset. With a workspace
-// (P), MODE 1 also settles the env's R banks (episodes E+1 .. E+R) in the same wave.
+// soccer, monolithic (one wave per env): MODE 0 = step (+ optional same-step autoreset), MODE 1 =
+// reset. A staged batch (workspace) resets through k_soccer_settle instead (mgx_staged.h).
 template <typename T, int MODE>
 __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
                                                const float* action, const T* draws, float* obs, double* reward,
@@ -136,21 +136,6 @@ __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, 
   }
   if (!draws) {
     soccer_reset_philox(m, e, ids, s, ev, obs, seed, env_offset, env, nullptr);
-    if (P) {
-      // prefill: bank for episode E' settles now, so the first R terminations never wait
-      int E1 = ev.episode[env];
-      for (int k = 0; k < P->R; k++) {
-        int Ep = E1 + k;
-        int bi = env * P->R + Ep % P->R;
-        bank_init(m, e, ids, *P, env, Ep % P->R, Ep, seed, env_offset);
-        int warn = 0;
-        for (int t = 0; t < 10; t++) warn += mj_step_env(m, e);
-        bank_store_state(m, e, *P, bi, warn);
-        bank_finalize(m, e, ids, *P, bi);
-        wsync();
-        if (lane_id() == 0) P->at<int>(P->o_bk)[bi] = 10;
-      }
-    }
     return;
   }
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
@@ -164,115 +149,6 @@ __global__ void __launch_bounds__(64) k_soccer(DevModel<T> m, SoccerIds<T> ids, 
   store_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   if (lane_id() == 0 && s.warning) s.warning[env] += warn;
   if (lane_id() == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
-}
-
-// ---- staged step kernels (mgx_staged.h)
-template <typename T>
-__global__ void __launch_bounds__(64) k_soccer_rows(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
-                                                    const float* action, int n_env, const uint8_t* mask, Pipe P,
-                                                    int banks) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int b = blockIdx.x;
-  int slot;
-  Env<T> e;
-  if (b < n_env) {
-    if (mask && !mask[b]) return;
-    env_bind(m, e, smem);
-    load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
-               (T*)s.time, b);
-    soccer_pre(m, e, ids, action + (size_t)b * m.nu, (T*)ev.prev_ball_pos + 3 * (size_t)b, (T*)ev.wind + 3 * (size_t)b);
-    slot = b;
-  } else {
-    int bi = b - n_env;
-    if (!banks || bi >= n_env * P.R) return;
-    int k = P.at<int>(P.o_bk)[bi];
-    if (k < 0 || k >= 10) return;
-    env_bind(m, e, smem);
-    bank_load_state(m, e, P, bi);
-    slot = b;
-  }
-  int warn = 0;  // mj_checkPos / mj_checkVel
-  if (any_bad(e.qpos, m.nq)) { reset_env(m, e); warn++; }
-  if (any_bad(e.qvel, m.nv)) { reset_env(m, e); warn++; }
-  stage_rows(m, e, P, slot, warn);
-}
-
-template <typename T>
-__global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
-                                                      const float* action, float* obs, double* reward,
-                                                      uint8_t* terminated, uint8_t* truncated, float* final_obs,
-                                                      int autoreset, uint64_t seed, int env_offset, int n_env,
-                                                      const uint8_t* mask, Pipe P, int banks) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int env = blockIdx.x;
-  if (env >= n_env) return;
-  int l = lane_id();
-  if (env == 0 && l == 0) {  // the solver lists are consumed; their sizes stay for diagnostics
-    P.ctr()[3] = P.ctr()[1];
-    P.ctr()[4] = P.ctr()[2];
-    P.ctr()[1] = 0;
-    P.ctr()[2] = 0;
-  }
-  Env<T> e;
-  env_bind(m, e, smem);
-  if (banks) {
-    for (int b = 0; b < P.R; b++) {
-      int bi = env * P.R + b;
-      int k = P.at<int>(P.o_bk)[bi];
-      if (k < 0 || k >= 10) continue;
-      int slot = n_env + bi;
-      int warn = load_carry(m, e, P, slot);
-      if (!finish_physics(m, e, P, slot)) {
-        load_template(m, e, P);
-        warn++;
-      }
-      bank_store_state(m, e, P, bi, warn);
-      k++;
-      if (k == 10) bank_finalize(m, e, ids, P, bi);
-      if (l == 0) P.at<int>(P.o_bk)[bi] = k;
-      wsync();
-    }
-    __threadfence();
-    wsync();
-  }
-  if (mask && !mask[env]) return;
-  int warn = load_carry(m, e, P, env);
-  if (!finish_physics(m, e, P, env)) {
-    load_template(m, e, P);
-    warn++;
-  }
-  store_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
-              (T*)s.time, env);
-  if (l == 0 && s.warning) s.warning[env] += warn;
-  if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
-  const float* a = action + (size_t)env * m.nu;
-  float* o = obs + (size_t)env * 80;
-  bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, (T*)ev.prev_ball_pos + 3 * (size_t)env,
-                          (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, o, reward + env,
-                          terminated + env, truncated + env, ev.flags ? ev.flags + 2 * (size_t)env : nullptr);
-  if (ev.rollout && l == 0) {
-    double* ro = (double*)ev.rollout + 8 * (size_t)env;
-    const double ne = e.nefc, it = e.nefc > 0 ? P.at<int>(P.o_niter)[env] : 0;
-    ro[0] += reward[env];
-    ro[1] += terminated[env];
-    ro[2] += truncated[env];
-    ro[3] += 1.0;
-    ro[4] += ne;
-    ro[5] += it;
-    ro[6] += ne * ne;
-    ro[7] += it * ne * ne;
-  }
-  if (done && autoreset) {
-    if (final_obs)
-      for (int i = l; i < 80; i += 64) final_obs[(size_t)env * 80 + i] = o[i];
-    __threadfence();
-    wsync();
-    bool ok = banks && bank_install(m, e, ids, P, s, ev, obs, seed, env_offset, env);
-    if (!ok && l == 0) {
-      int i = atomicAdd(P.ctr(), 1);
-      P.at<int>(P.o_fix)[i] = env * 4 + FIX_RESET;
-    }
-  }
 }
 
 // mj_step from mj_resetData'd state (the checkAcc template, see load_template)
@@ -299,24 +175,6 @@ __global__ void __launch_bounds__(64) k_soccer_template(DevModel<T> m, Pipe P) {
     P.at<T>(P.o_tcm)[k] = e.con_mu[k];
   }
   if (l == 0) { P.at<int>(P.o_tn)[0] = nc; P.at<T>(P.o_tt)[0] = e.time; }
-}
-
-// S4: resets whose bank was not ready (listed by the finisher), monolithic: one wave per
-// env with the full LDS layout, grid-stride over the list
-template <typename T>
-__global__ void __launch_bounds__(64) k_soccer_fixup(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
-                                                     float* obs, uint64_t seed, int env_offset, Pipe P, int banks) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int cnt = P.ctr()[0];
-  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
-    int env = P.at<int>(P.o_fix)[i] >> 2;
-    Env<T> e;
-    env_bind(m, e, smem);
-    load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied,
-               (T*)s.xfrc_applied, (T*)s.time, env);
-    soccer_reset_philox(m, e, ids, s, ev, obs, seed, env_offset, env, banks ? &P : nullptr);
-    wsync();
-  }
 }
 
 // Env-logic-only test hook: frames/contacts come from the caller (golden vectors generated
@@ -675,6 +533,15 @@ static int pgs_lds_bytes(const mgx_model* m, int rows) {
   return spw * (MGX_SCAL * 4 * nb3 + 4) * rb + spw * nb3 * 32 + 64;
 }
 
+// LDS of the one-wave settle: the row builder's layout, then one solver wave with maxE rows per
+// slot, then the finisher's layout, in turn
+static int settle_lds_bytes(const mgx_model* m, const Pipe& P) {
+  int b = pgs_lds_bytes(m, P.maxE);
+  if (m->Ls.bytes > b) b = m->Ls.bytes;
+  if (m->Lf.bytes > b) b = m->Lf.bytes;
+  return b;
+}
+
 template <typename T>
 static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms, const DevModel<T>& Mf,
                               const SoccerIds<T>& ids, const mgx_state* s, const mgx_soccer_env* e, const float* action,
@@ -686,19 +553,37 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   size_t need = make_pipe(m, e->workspace, n_env, e->banks, &P);
   if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
   int slots = n_env * (1 + banks);
-  hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, *e, action, n_env, mask, P,
-                     banks);
+  launch_soccer_rows<T>(Ms, ids, *s, *e, action, n_env, mask, P, banks, slots, m->Ls.bytes, st);
   T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
   launch_pgs<T>(P, slots, pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE), st, M.iterations, M.tolerance, scale, 0);
   // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped)
   // and those of main-launch waves that did not fit their arena: a small grid-stride global-B
   // launch that exits at once when the list is empty
   launch_pgs<T>(P, 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, pgs_lds_bytes(m, P.maxE), st, M.iterations, M.tolerance, scale, 1);
-  hipLaunchKernelGGL(k_soccer_finish<T>, dim3(n_env), dim3(64), m->Lf.bytes, st, Mf, ids, *s, *e, action, obs, reward,
-                     terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks);
+  launch_soccer_finish<T>(Mf, ids, *s, *e, action, obs, reward, terminated, truncated, final_obs, autoreset, seed,
+                          env_offset, n_env, mask, P, banks, m->Lf.bytes, st);
+  // resets whose bank was not ready: settled in one wave each by the pipeline's own stages
+  // (k_soccer_settle), a small grid-stride launch that exits at once when the list is empty
   int fgrid = n_env < 256 ? n_env : 256;
-  hipLaunchKernelGGL(k_soccer_fixup<T>, dim3(fgrid), dim3(64), m->L.bytes, st, M, ids, *s, *e, obs, seed, env_offset, P,
-                     banks);
+  launch_soccer_settle<T>(Ms, Mf, ids, *s, *e, (const T*)nullptr, obs, seed, env_offset, n_env, nullptr, P, SETTLE_FIXUP,
+                          fgrid, settle_lds_bytes(m, P), st, M.iterations, M.tolerance, scale);
+  HIPCHK(hipGetLastError());
+  return MGX_OK;
+}
+
+// reset() of a staged batch: every env's reset (and, with Philox draws, its R banks) settled by
+// the pipeline's stages in one wave (k_soccer_settle), so the staged batch has one arithmetic for
+// every reset, whatever the bank count
+template <typename T>
+static int soccer_reset_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms, const DevModel<T>& Mf,
+                               const SoccerIds<T>& ids, const mgx_state* s, const mgx_soccer_env* e, const T* draws,
+                               float* obs, uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st) {
+  Pipe P;
+  size_t need = make_pipe(m, e->workspace, n_env, e->banks, &P);
+  if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
+  T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
+  launch_soccer_settle<T>(Ms, Mf, ids, *s, *e, draws, obs, seed, env_offset, n_env, mask, P, SETTLE_RESET, n_env,
+                          settle_lds_bytes(m, P), st, M.iterations, M.tolerance, scale);
   HIPCHK(hipGetLastError());
   return MGX_OK;
 }
@@ -789,13 +674,16 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   }
   r2 = precision == MGX_F32
                ? (set_lds(k_soccer<float, 0>, m->L.bytes) | set_lds(k_soccer<float, 1>, m->L.bytes) |
-                  set_lds(k_soccer_logic<float>, m->L.bytes) | set_lds(k_soccer_fixup<float>, m->L.bytes) | set_lds(k_soccer_template<float>, m->L.bytes) |
-                  set_lds(k_soccer_rows<float>, m->Ls.bytes) | set_lds(k_soccer_finish<float>, m->Lf.bytes))
+                  set_lds(k_soccer_logic<float>, m->L.bytes) | set_lds(k_soccer_template<float>, m->L.bytes))
                : (set_lds(k_soccer<double, 0>, m->L.bytes) | set_lds(k_soccer<double, 1>, m->L.bytes) |
-                  set_lds(k_soccer_logic<double>, m->L.bytes) | set_lds(k_soccer_fixup<double>, m->L.bytes) | set_lds(k_soccer_template<double>, m->L.bytes) |
-                  set_lds(k_soccer_rows<double>, m->Ls.bytes) | set_lds(k_soccer_finish<double>, m->Lf.bytes));
+                  set_lds(k_soccer_logic<double>, m->L.bytes) | set_lds(k_soccer_template<double>, m->L.bytes));
   if (r2 != MGX_OK) { delete m; return r2; }
   if (m->staged_ok) {
+    int sl = pgs_lds_bytes(m, m->Ls.max_nefc);  // the settle kernel's (settle_lds_bytes)
+    if (m->Ls.bytes > sl) sl = m->Ls.bytes;
+    if (m->Lf.bytes > sl) sl = m->Lf.bytes;
+    r2 = staged_kernels_configure(precision, m->Ls.bytes, m->Lf.bytes, sl);
+    if (r2 != MGX_OK) { delete m; return r2; }
     int pl = pgs_lds_bytes(m, m->Ls.max_nefc);  // the global-B launch's
     if (pl < 96 * 1024) pl = 96 * 1024;  // the arena (MGX_PGS_ARENA tuning up to 96 KiB)
     if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
@@ -899,22 +787,24 @@ int mgx_soccer_reset(const mgx_model* m, const mgx_state* s, const mgx_soccer_en
   if (rc) return rc;
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
-  Pipe P{};
-  int use_pipe = 0;
-  if (e->workspace && !draws && e->banks > 0) {
-    if (e->banks > 16) return fail(MGX_E_ARG, "banks must be in [0, 16]");
-    size_t need = make_pipe(m, e->workspace, n_env, e->banks, &P);
-    if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
-    use_pipe = 1;
+  if (e->workspace) {
+    if (!m->staged_ok) return fail(MGX_E_UNSUPPORTED, "staged step: model exceeds the staged solver's capacity");
+    if (e->banks < 0 || e->banks > 16) return fail(MGX_E_ARG, "banks must be in [0, 16]");
+    if (m->precision == MGX_F32)
+      return soccer_reset_staged<float>(m, m->mf, m->mfs, m->mff, m->sf, s, e, (const float*)draws, obs, seed,
+                                        env_offset, n_env, mask, st);
+    return soccer_reset_staged<double>(m, m->md, m->mds, m->mdf, m->sd, s, e, (const double*)draws, obs, seed,
+                                       env_offset, n_env, mask, st);
   }
+  Pipe none{};
   if (m->precision == MGX_F32)
     hipLaunchKernelGGL((k_soccer<float, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->sf, *s, *e,
                        (const float*)nullptr, (const float*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
-                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask, P, use_pipe);
+                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask, none, 0);
   else
     hipLaunchKernelGGL((k_soccer<double, 1>), dim3(n_env), dim3(64), m->L.bytes, st, m->md, m->sd, *s, *e,
                        (const float*)nullptr, (const double*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
-                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask, P, use_pipe);
+                       (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask, none, 0);
   HIPCHK(hipGetLastError());
   return MGX_OK;
 }

@@ -79,6 +79,22 @@ int step_kernels_configure(const mgx_model* m);
 template <typename T>
 void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big);
 int pgs_configure_lds(int precision, int bytes);
+// S1 / S3 and the one-wave settle (mgx_pgs.hip, the staged TU)
+template <typename T>
+void launch_soccer_rows(const DevModel<T>& Ms, const SoccerIds<T>& ids, const mgx_state& s, const mgx_soccer_env& ev,
+                        const float* action, int n_env, const uint8_t* mask, const Pipe& P, int banks, int slots, int lds,
+                        hipStream_t st);
+template <typename T>
+void launch_soccer_finish(const DevModel<T>& Mf, const SoccerIds<T>& ids, const mgx_state& s, const mgx_soccer_env& ev,
+                          const float* action, float* obs, double* reward, uint8_t* terminated, uint8_t* truncated,
+                          float* final_obs, int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t* mask,
+                          const Pipe& P, int banks, int lds, hipStream_t st);
+template <typename T>
+void launch_soccer_settle(const DevModel<T>& Ms, const DevModel<T>& Mf, const SoccerIds<T>& ids, const mgx_state& s,
+                          const mgx_soccer_env& ev, const T* draws, float* obs, uint64_t seed, int env_offset, int n_env,
+                          const uint8_t* mask, const Pipe& P, int mode, int grid, int lds, hipStream_t st, int maxit, T tol,
+                          T scale);
+int staged_kernels_configure(int precision, int ls, int lf, int settle);
 int pgs_lanes();
 int pgs_lds_b();
 }  // namespace mgx

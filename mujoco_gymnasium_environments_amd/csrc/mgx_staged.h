@@ -355,8 +355,11 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
 }
 
 // S1 body: forward up to the constraint rows, rows -> pipe, carry -> pipe
+// list_slot: enter the slot in the solver launches' lists (the pipeline); the one-wave settle
+// (settle_step) solves the slot itself.
 template <typename T>
-__device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot, int warn) {
+__device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot, int warn,
+                                           bool list_slot = true) {
   int l = lane_id();
   const int nv = m.nv;
   MGX_STAMP_DECL
@@ -433,7 +436,8 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
       g_mgx_prof[slot * 32 + 25] += e.overflow != 0;
     }
 #endif
-    if (ne > P.capE) {  // rare: more rows than the main solver launch keeps in LDS
+    if (!list_slot) {
+    } else if (ne > P.capE) {  // rare: more rows than the main solver launch keeps in LDS
       int idx = atomicAdd(P.ctr() + 2, 1);
       P.at<int>(P.o_k2big)[idx] = slot;
     } else if (ne > 0) {
@@ -890,13 +894,11 @@ __device__ __forceinline__ void copy_g(T* dst, const T* src, int n) {
 
 // bank (env, b) restarts for `episode`: Philox draws -> mj_resetData + randomised qpos
 // (soccer_apply_reset), settle counter 0. Clobbers the Env's state arrays.
+// bank record bi restarts for `episode` from the 36 draws in e.vec1 (LDS)
 template <typename T>
-__device__ __forceinline__ void bank_init(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const Pipe& P, int env,
-                                          int b, int episode, uint64_t seed, int env_offset) {
+__device__ __forceinline__ void bank_init_draws(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const Pipe& P,
+                                                int bi, int episode, uint64_t seed) {
   int l = lane_id();
-  int bi = env * P.R + b;
-  soccer_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)episode, ids.n_noise, e.vec1);
-  wsync();
   soccer_apply_reset(m, e, ids, e.vec1, P.at<T>(P.o_bwind) + 3 * (size_t)bi);
   copy_g(P.at<T>(P.o_bq) + (size_t)bi * m.nq, e.qpos, m.nq);
   if (l < m.nv) {
@@ -911,6 +913,13 @@ __device__ __forceinline__ void bank_init(const DevModel<T>& m, Env<T>& e, const
     P.at<int>(P.o_bk)[bi] = 0;
   }
   wsync();
+}
+template <typename T>
+__device__ __forceinline__ void bank_init(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const Pipe& P, int env,
+                                          int b, int episode, uint64_t seed, int env_offset) {
+  soccer_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)episode, ids.n_noise, e.vec1);
+  wsync();
+  bank_init_draws(m, e, ids, P, env * P.R + b, episode, seed);
 }
 
 // settle finished: the reset's observation and prev snapshots (soccer_env.py:381-396)
@@ -952,18 +961,12 @@ __device__ __forceinline__ void bank_load_state(const DevModel<T>& m, Env<T>& e,
   wsync();
 }
 
-// Install the ready bank of env `env` into its live state and restart the bank for
-// episode + R. Returns false if the bank is not ready (caller falls back).
+// the settled reset of bank record bi becomes env's live state for episode E (soccer_env.py:
+// 347-396 outcome: state, obs, prev snapshots, wind, zero stats / step / goal); episode E + 1
 template <typename T>
-__device__ __forceinline__ bool bank_install(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const Pipe& P,
-                                             mgx_state s, mgx_soccer_env ev, float* obs, uint64_t seed, int env_offset,
-                                             int env) {
+__device__ __forceinline__ void bank_copy_live(const DevModel<T>& m, const Pipe& P, mgx_state s, mgx_soccer_env ev,
+                                               float* obs, int env, int bi, int E) {
   int l = lane_id();
-  int E = ev.episode[env];
-  int b = E % P.R;
-  int bi = env * P.R + b;
-  bool ready = P.at<int>(P.o_bk)[bi] == 10 && P.at<int>(P.o_bep)[bi] == E && P.at<uint64_t>(P.o_bseed)[bi] == seed;
-  if (!ready) return false;
   copy_g((T*)s.qpos + (size_t)env * m.nq, P.at<T>(P.o_bq) + (size_t)bi * m.nq, m.nq);
   copy_g((T*)s.qvel + (size_t)env * m.nv, P.at<T>(P.o_bv) + (size_t)bi * m.nv, m.nv);
   copy_g((T*)s.qacc_warmstart + (size_t)env * m.nv, P.at<T>(P.o_ba) + (size_t)bi * m.nv, m.nv);
@@ -983,11 +986,129 @@ __device__ __forceinline__ bool bank_install(const DevModel<T>& m, Env<T>& e, co
     if (s.warning) s.warning[env] += P.at<int>(P.o_bwarn)[bi];
     ev.step[env] = 0;
     ev.goal_scored[env] = 0;
-    ev.episode[env] = E + 1;
+    if (ev.episode) ev.episode[env] = E + 1;
   }
   wsync();
+}
+
+// Install the ready bank of env `env` into its live state and restart the bank for
+// episode + R. Returns false if the bank is not ready (caller falls back).
+template <typename T>
+__device__ __forceinline__ bool bank_install(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const Pipe& P,
+                                             mgx_state s, mgx_soccer_env ev, float* obs, uint64_t seed, int env_offset,
+                                             int env) {
+  int E = ev.episode[env];
+  int b = E % P.R;
+  int bi = env * P.R + b;
+  bool ready = P.at<int>(P.o_bk)[bi] == 10 && P.at<int>(P.o_bep)[bi] == E && P.at<uint64_t>(P.o_bseed)[bi] == seed;
+  if (!ready) return false;
+  bank_copy_live(m, P, s, ev, obs, env, bi, E);
   bank_init(m, e, ids, P, env, b, E + P.R, seed, env_offset);
   return true;
+}
+
+// ------------------------------------------------------------------ one-wave settle
+// One settle step of bank record bi in one wave, through pipe slot `slot`: the pipeline's own
+// stages in sequence — stage_rows, the PGS of the one slot (pgs_group, lane group 0 of the
+// wave), the finisher's finish_physics / checkAcc template / bank store. A reset settled here is
+// bit-identical to one settled as extra slots of the pipeline launches, so the fallback for a
+// bank that is not ready (and reset()) produces exactly what a ready bank would have: the bank
+// count is a performance knob only. Returns with the finisher's Env (layout Mf) in `smem`.
+template <typename T, int EPL, int LPS>
+__device__ __forceinline__ void settle_step(const DevModel<T>& Ms, const DevModel<T>& Mf, const SoccerIds<T>& ids,
+                                            const Pipe& P, char* smem, int* lst, Env<T>& f, int bi, int slot,
+                                            int maxit, T tol, T scale, bool last) {
+  {
+    Env<T> e;
+    env_bind(Ms, e, smem);
+    bank_load_state(Ms, e, P, bi);
+    int warn = 0;  // mj_checkPos / mj_checkVel
+    if (any_bad(e.qpos, Ms.nq)) { reset_env(Ms, e); warn++; }
+    if (any_bad(e.qvel, Ms.nv)) { reset_env(Ms, e); warn++; }
+    stage_rows(Ms, e, P, slot, warn, false);
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) lst[0] = slot;
+  __syncthreads();
+  pgs_group<T, EPL, LPS, false>(P, smem, lst, 1, 0, P.maxE, maxit, tol, scale, 64 / LPS);
+  __threadfence();
+  __syncthreads();
+  env_bind(Mf, f, smem);
+  int warn = load_carry(Mf, f, P, slot);
+  if (!finish_physics(Mf, f, P, slot)) {
+    load_template(Mf, f, P);
+    warn++;
+  }
+  bank_store_state(Mf, f, P, bi, warn);
+  if (last) bank_finalize(Mf, f, ids, P, bi);
+  __threadfence();
+  __syncthreads();
+}
+
+// Restart record bi for `episode` (draws: host [36] or nullptr for Philox) and settle it
+// (soccer_env.py:378-379: 10 mj_steps from the randomised pose); bk = 10 at the end.
+template <typename T, int EPL, int LPS>
+__device__ __forceinline__ void settle_reset(const DevModel<T>& Ms, const DevModel<T>& Mf, const SoccerIds<T>& ids,
+                                             const Pipe& P, char* smem, int* lst, int env, int bi, int episode,
+                                             const T* draws, uint64_t seed, int env_offset, int maxit, T tol, T scale) {
+  {
+    Env<T> e;
+    env_bind(Ms, e, smem);
+    if (draws) {
+      if (lane_id() < 36) e.vec1[lane_id()] = draws[lane_id()];
+    } else {
+      soccer_philox_draws(seed, (uint32_t)(env_offset + env), (uint32_t)episode, ids.n_noise, e.vec1);
+    }
+    wsync();
+    bank_init_draws(Ms, e, ids, P, bi, episode, seed);
+  }
+  __threadfence();
+  __syncthreads();
+  Env<T> f;
+  for (int t = 0; t < 10; t++) settle_step<T, EPL, LPS>(Ms, Mf, ids, P, smem, lst, f, bi, env, maxit, tol, scale, t == 9);
+  if (lane_id() == 0) P.at<int>(P.o_bk)[bi] = 10;
+  __threadfence();
+  __syncthreads();
+}
+
+enum { SETTLE_RESET = 0, SETTLE_FIXUP = 1 };
+// reset() of a staged batch (SETTLE_RESET: one workgroup per env; with Philox draws and banks it
+// also prefills the env's R banks) and the step's fallback for banks that were not ready
+// (SETTLE_FIXUP: grid-stride over the finisher's list). Every reset goes through settle_reset,
+// the pipeline's arithmetic.
+template <typename T, int EPL, int LPS>
+__global__ void __launch_bounds__(64) k_soccer_settle(DevModel<T> Ms, DevModel<T> Mf, SoccerIds<T> ids, mgx_state s,
+                                                      mgx_soccer_env ev, const T* draws, float* obs, uint64_t seed,
+                                                      int env_offset, int n_env, const uint8_t* mask, Pipe P, int mode,
+                                                      int maxit, T tol, T scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int lst[4];
+  const int cnt = mode == SETTLE_FIXUP ? P.ctr()[0] : n_env;
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const int env = mode == SETTLE_FIXUP ? P.at<int>(P.o_fix)[i] >> 2 : i;
+    if (mode == SETTLE_RESET && mask && !mask[env]) continue;
+    const int E = ev.episode ? ev.episode[env] : 0;
+    const int bi = P.R > 0 ? env * P.R + E % P.R : env;  // R = 0: one scratch record per env
+    const T* d = draws ? draws + (size_t)env * 36 : nullptr;
+    settle_reset<T, EPL, LPS>(Ms, Mf, ids, P, smem, lst, env, bi, E, d, seed, env_offset, maxit, tol, scale);
+    bank_copy_live(Mf, P, s, ev, obs, env, bi, E);
+    if (P.R > 0 && mode == SETTLE_FIXUP) {
+      // as bank_install: the consumed bank restarts for episode E + R (the pipeline settles it)
+      Env<T> e;
+      env_bind(Ms, e, smem);
+      bank_init(Ms, e, ids, P, env, E % P.R, E + P.R, seed, env_offset);
+    } else if (P.R > 0 && !draws) {
+      // reset(): prefill the banks of episodes E + 1 .. E + R, so the first R terminations never wait
+      for (int k = 1; k <= P.R; k++)
+        settle_reset<T, EPL, LPS>(Ms, Mf, ids, P, smem, lst, env, env * P.R + (E + k) % P.R, E + k, nullptr, seed,
+                                  env_offset, maxit, tol, scale);
+    } else if (lane_id() == 0) {
+      P.at<int>(P.o_bk)[bi] = -1;  // a scratch record (R = 0, or host draws): nothing to settle
+    }
+    __threadfence();
+    __syncthreads();
+  }
 }
 
 }  // namespace mgx
