@@ -7,6 +7,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -255,9 +257,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   const int nb12 = align_up(12 * nb, al), cf9 = align_up(9 * max_ncon, al), cp3 = align_up(3 * max_ncon, al);
   const int union_dead = align_up(9 * nb, al) + align_up(3 * nb, al) + align_up(9 * nb, al) + align_up(10 * nb, al) +
                          align_up(10 * nb, al) + align_up(6 * nb, al) + align_up(6 * nv, al) + 2 * align_up(3 * nj, al);
-  const int union_tail = align_up(3 * ng, al) + align_up(9 * ng, al) + align_up(d->nu, al);
-  const bool staged_overlay = staged && nb12 + cf9 + cp3 <= union_dead &&
-                              nb12 + cf9 + cp3 + align_up(4 * max_nefc, al) <= union_dead + union_tail;
+  const bool staged_overlay = staged && nb12 + cf9 + cp3 <= union_dead;
   // monolithic PGS models with rows in global scratch: the contact points / frames, the row
   // margins (make_constraint only) and the broadphase survivor list (collision only) overlay
   // xmat .. xanchor of the union, dead once the velocity stage is done (bipedal: 62.4 -> 51.4 KiB,
@@ -299,18 +299,14 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   }
   if (staged_overlay) {
     // xmat .. xanchor are dead once the velocity stage is done: the contact frames and points
-    // (written by collision, read by the row blocks) follow cacc there; the row constants
-    // (written after collision) follow them, over the geom frames collision has consumed
-    // (fp64 soccer: 38.6 -> 32.4 KB per row-builder wave, five waves per CU)
+    // (written by collision, read by the row blocks) follow cacc there (fp64 soccer: 38.6 ->
+    // 32.4 KB per row-builder wave). The per-row impedance constants live in the slot's row-scalar
+    // area of the pipe (rows_impedance), so the full capacity (96 contacts / 384 rows) fits the
+    // same budget: 31.7 / 32.6 KB, five waves per CU either way.
     L.con_frame = u0 + nb12;
     L.con_pos = L.con_frame + cf9;
-    L.rowc = L.con_pos + cp3;
-  } else {
-    // staged: per-row impedance constants (4 per row) over cfrc .. (dead after velocity and
-    // collision), or their own space when that tail is too short
-    L.rowc = staged ? (endA - L.cfrc >= 4 * max_nefc ? L.cfrc : take(4 * max_nefc)) : 0;
-    if (staged && L.rowc != L.cfrc) endA = p;
   }
+  L.rowc = 0;
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
   L.Bmat = u0;
   L.chunk_rows = staged ? 0 : max_nefc;  // the staged row builder keeps rows in registers
@@ -333,8 +329,19 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   auto takei = [&](int n) { int r = q; q = align_up(q + (n > 0 ? n : 1), 4); return r; };
   L.con_geom = takei(2 * max_ncon);
   L.carry_ints = q;
-  L.con_pair = takei(max_ncon); L.act_list = takei(max_active);
-  L.efc_type = takei(staged ? 1 : max_nefc); L.efc_id = takei(max_nefc); L.con_efcadr = takei(1);
+  L.con_pair = takei(max_ncon);
+  if (staged) {
+    // the staged row builder lists only the joint-limit rows in efc_id (<= 2 per joint), after
+    // collision: it shares the space of the broadphase survivor list (collision only)
+    const int ecap = std::min(max_nefc, align_up(2 * nj, 4));
+    L.act_list = takei(std::max(max_active, ecap));
+    L.efc_id = L.act_list;
+    L.efc_type = takei(1);
+  } else {
+    L.act_list = takei(max_active);
+    L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
+  }
+  L.con_efcadr = takei(1);
   L.ints = q;
   L.bytes = L.reals * real_bytes + L.ints * 4;
   (void)vec_end;
@@ -533,6 +540,32 @@ static int pgs_lds_bytes(const mgx_model* m, int rows) {
   return spw * (MGX_SCAL * 4 * nb3 + 4) * rb + spw * nb3 * 32 + 64;
 }
 
+// A side stream and two events per caller stream (created once, kept for the process): the wide
+// solver launch runs beside the main one. nullptr if the runtime refuses (then both run in order).
+struct SideStream {
+  hipStream_t s;
+  hipEvent_t rows, big;
+};
+static SideStream* side_stream(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<hipStream_t, int>, SideStream*> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_pair(st, dev);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  SideStream* x = new SideStream{};
+  if (hipStreamCreateWithFlags(&x->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&x->rows, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&x->big, hipEventDisableTiming) != hipSuccess) {
+    delete x;
+    x = nullptr;
+  }
+  cache[key] = x;
+  return x;
+}
+
 // LDS of the one-wave settle: the row builder's layout, then one solver wave with maxE rows per
 // slot, then the finisher's layout, in turn
 static int settle_lds_bytes(const mgx_model* m, const Pipe& P) {
@@ -555,11 +588,26 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   int slots = n_env * (1 + banks);
   launch_soccer_rows<T>(Ms, ids, *s, *e, action, n_env, mask, P, banks, slots, m->Ls.bytes, st);
   T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
-  launch_pgs<T>(P, slots, pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE), st, M.iterations, M.tolerance, scale, 0);
-  // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped)
-  // and those of main-launch waves that did not fit their arena: a small grid-stride global-B
-  // launch that exits at once when the list is empty
-  launch_pgs<T>(P, 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, pgs_lds_bytes(m, P.maxE), st, M.iterations, M.tolerance, scale, 1);
+  // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped):
+  // a small grid-stride global-B launch with maxE rows of LDS per slot, which exits at once when
+  // the list is empty. It runs on a side stream beside the main launch (a slot of ~300 rows is
+  // one wave's 50-sweep chain, which would otherwise trail the main launch). With the LDS-arena
+  // main launch (MGX_PGS_LDS_B) it also takes the waves that did not fit their arena, so it
+  // follows the main launch there.
+  const int wgrid = 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, wlds = pgs_lds_bytes(m, P.maxE);
+  const int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE);
+  SideStream* side = pgs_lds_b() ? nullptr : side_stream(st);
+  if (side) {
+    HIPCHK(hipEventRecord(side->rows, st));
+    HIPCHK(hipStreamWaitEvent(side->s, side->rows, 0));
+    launch_pgs<T>(P, wgrid, wlds, side->s, M.iterations, M.tolerance, scale, 1);
+    HIPCHK(hipEventRecord(side->big, side->s));
+    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
+    HIPCHK(hipStreamWaitEvent(st, side->big, 0));
+  } else {
+    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
+    launch_pgs<T>(P, wgrid, wlds, st, M.iterations, M.tolerance, scale, 1);
+  }
   launch_soccer_finish<T>(Mf, ids, *s, *e, action, obs, reward, terminated, truncated, final_obs, autoreset, seed,
                           env_offset, n_env, mask, P, banks, m->Lf.bytes, st);
   // resets whose bank was not ready: settled in one wave each by the pipeline's own stages

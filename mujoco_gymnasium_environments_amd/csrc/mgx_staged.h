@@ -95,10 +95,13 @@ __device__ __forceinline__ int rows_plan(const DevModel<T>& m, Env<T>& e, int* n
   return nlim4 + 4 * ncf;
 }
 
-// Per-row constants of mj_makeImpedance [ext], lane per row, into e.rowc (4 per row):
-// R, B (damping of aref), K*imp*(pos - margin), 1 for a real row / 0 for padding.
+// Per-row constants of mj_makeImpedance [ext], lane per row: R, B (damping of aref),
+// K*imp*(pos - margin), 1 for a real row / 0 for padding. They go to the slot's own row-scalar
+// area in the pipe (the b, f, R, 1/AR places of the row, overwritten by build_block with the
+// final scalars), not to LDS: 4 reals per row would cost the row builder 12 KB of LDS at full
+// capacity (384 rows, fp64).
 template <typename T>
-__device__ __forceinline__ void rows_impedance(const DevModel<T>& m, Env<T>& e, int ne, int nlim, int nlim4) {
+__device__ __forceinline__ void rows_impedance(const DevModel<T>& m, Env<T>& e, int ne, int nlim, int nlim4, T* scal) {
   const int l = lane_id();
   for (int r = l; r < ne; r += 64) {
     const T *solref = nullptr, *solimp = nullptr;
@@ -127,9 +130,9 @@ __device__ __forceinline__ void rows_impedance(const DevModel<T>& m, Env<T>& e, 
         solimp = m.pair_solimp + 5 * p;
       }
     }
-    T* o = e.rowc + 4 * r;
+    T* o = scal + (size_t)(r >> 2) * (4 * MGX_SCAL) + (r & 3);
     if (!solref) {
-      o[0] = 1; o[1] = 0; o[2] = 0; o[3] = 0;
+      o[MGX_SQ(0, 0)] = 1; o[MGX_SQ(1, 0)] = 0; o[MGX_SQ(2, 0)] = 0; o[MGX_SQ(3, 0)] = 0;
       continue;
     }
     T imp = impedance(solimp, pos, margin);
@@ -144,10 +147,10 @@ __device__ __forceinline__ void rows_impedance(const DevModel<T>& m, Env<T>& e, 
       B = -solref[1] / dmax;
     }
     T R = ((T)1 - imp) * diag / imp;
-    o[0] = R > minval<T>() ? R : minval<T>();
-    o[1] = B;
-    o[2] = K * imp * (pos - margin);
-    o[3] = 1;
+    o[MGX_SQ(0, 0)] = R > minval<T>() ? R : minval<T>();
+    o[MGX_SQ(1, 0)] = B;
+    o[MGX_SQ(2, 0)] = K * imp * (pos - margin);
+    o[MGX_SQ(3, 0)] = 1;
   }
 }
 
@@ -207,6 +210,12 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
 #ifdef MGX_PROFILE
   unsigned long long _bt = __builtin_amdgcn_s_memtime();
 #endif
+  // the block's row constants (rows_impedance), lane i < 4 row r0 + i, loaded now and used last
+  T rc0 = 0, rc1 = 0, rc2 = 0, rc3 = 0;
+  if (l < 4) {
+    const T* q = scal + (size_t)(r0 >> 2) * (4 * MGX_SCAL) + l;
+    rc0 = q[MGX_SQ(0, 0)]; rc1 = q[MGX_SQ(1, 0)]; rc2 = q[MGX_SQ(2, 0)]; rc3 = q[MGX_SQ(3, 0)];
+  }
   T j0 = 0, j1 = 0, j2 = 0, j3 = 0;
   uint64_t sup = 0;
   T dv = 0, ds = 0, dw = 0;
@@ -312,11 +321,10 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
   MGX_BSTAMP(10);
   if (l < 4) {
     T* o = scal + (size_t)(r0 >> 2) * (4 * MGX_SCAL) + l;
-    const T* rc = e.rowc + 4 * (r0 + l);
     T nn = l == 0 ? n0 : l == 1 ? n1 : l == 2 ? n2 : n3;
-    if (rc[3] != 0) {
-      T R = rc[0];
-      T aref = -rc[1] * dv - rc[2];   // mj_referenceConstraint
+    if (rc3 != 0) {
+      T R = rc0;
+      T aref = -rc1 * dv - rc2;   // mj_referenceConstraint
       T jar = dw - aref;
       T ad = nn + R;
       o[MGX_SQ(0, 0)] = ds - aref;                 // b = J qacc_smooth - aref
@@ -407,9 +415,10 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
       }
       wsync();
     }
-    rows_impedance(m, e, ne, nlim, nlim4);
+    rows_impedance(m, e, ne, nlim, nlim4, scal);
     ContactMeta<T> cm;
     contact_meta(m, e, ncf, cm);
+    __threadfence();  // the row constants are read back by other lanes of this wave (build_block)
     wsync();
     for (int r0 = 0; r0 < ne; r0 += 4) build_block(m, e, P, r0, nlim, nlim4, cm, dinvs, scal, blk, Bo, boff);
   }

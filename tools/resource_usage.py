@@ -5,9 +5,15 @@ import sys
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src = os.path.join(ROOT, "mujoco_gymnasium_environments_amd", "csrc", "mgx_api.hip")
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", "/tmp/_ru.so", src,
-       "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
+# usage: resource_usage.py [source.hip] [extra hipcc flags]; default mgx_api.hip; mgx_pgs.hip gets
+# its own per-TU flags (native.SOURCE_FLAGS)
+args = sys.argv[1:]
+name = args.pop(0) if args and args[0].endswith(".hip") else "mgx_api.hip"
+src = os.path.join(ROOT, "mujoco_gymnasium_environments_amd", "csrc", name)
+sys.path.insert(0, ROOT)
+from mujoco_gymnasium_environments_amd.native import SOURCE_FLAGS  # noqa: E402
+cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", "-o", "/tmp/_ru.o", src,
+       "-Rpass-analysis=kernel-resource-usage"] + SOURCE_FLAGS.get(name, []) + args
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur = None
 rows = {}
