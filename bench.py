@@ -66,6 +66,8 @@ PARKOUR_METRIC = "env steps/sec (whole node), quadruped_parkour 4096 envs/GPU (B
 # prev_sz, distance, prev_robot_pos[3] (fp64), read ttfr (fp64), write obs 102 (fp32), reward
 # (fp64), flags (u8)
 BIPEDAL_ALG_BYTES = 4 * (2 * 189 + 2 * 26 + 26 + 2 * 9 + 2 * 2 + 102) + 2 + 8 * (2 * 6 + 1 + 1) + 2
+# fp64 (the parity precision): the same state / task I/O with the physics reals in 8 bytes
+BIPEDAL_ALG_BYTES_F64 = 8 * (2 * 189 + 2 * 26) + 4 * (26 + 2 * 9 + 2 * 2 + 102) + 2 + 8 * (2 * 6 + 1 + 1) + 2
 BIPEDAL_METRIC = "env steps/sec (whole node), bipedal_rescue 8192 envs/GPU (BASELINE configs[3])"
 # dancing: r/w qpos/qvel/qacc_warmstart 29 each and ctrl 29 (fp32), action 29, r/w 18 fp64 + 8
 # int32 task scalars + 3 hist, prev_jvel 23 (fp64), read the 20-move sequence (int32 + fp64),
@@ -460,6 +462,32 @@ def soccer_flops(ro: torch.Tensor, nv: int) -> dict:
             "pgs_sweeps_mean": float(ro[5]) / max(steps, 1.0)}
 
 
+def bipedal_other_line(args, dev, N, g, precision: str) -> dict:
+    """configs[3] in the other precision (a short timed run after the headline's timed region).
+    fp64 is the parity precision; fp32 is compared with it by distribution
+    (tests/test_gpu_bipedal.py::test_bipedal_f32_distribution_matches_f64)."""
+    from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+    env = BipedalVectorEnv(N, device=str(dev), precision=precision, seed=1234, staged=not args.mono,
+                           banks=min(args.banks, 1) if args.banks > 0 else 0)
+    pool = [((torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0).contiguous() for _ in range(4)]
+    env.reset()
+    for k in range(3):
+        env.step(pool[k % 4])
+    torch.cuda.synchronize(dev)
+    steps = 10
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record()
+    for k in range(steps):
+        env.step(pool[k % 4])
+    b.record()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return {"value": round(N * steps / el, 1), "unit": "env_steps/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "launch_ms": round(a.elapsed_time(b) / steps, 4), "steps": steps, "dtype": precision,
+            "step_kernels": "mono" if args.mono else "staged"}
+
+
 def other_precision_line(args, dev, N, g, precision: str) -> dict:
     """The same staged step in the other precision (SURVEY §7 'report both'): a short timed run
     after the headline's timed region. fp64 is the parity precision (tests/test_gpu_f32_staged.py:
@@ -497,7 +525,7 @@ def main():
     # soccer's headline precision is fp64: the precision that meets the north_star accuracy bar
     # (qpos drift < 1e-4 over 1000 steps vs the fp64 oracle); fp32 rides along as an extra key
     ap.add_argument("--precision", default=None, choices=["f32", "f64"],
-                    help="default: f64 for soccer (the headline), f32 for the other tasks")
+                    help="default: f64 (MuJoCo's mjtNum, the parity precision) for every task")
     ap.add_argument("--cpu-envs", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -512,10 +540,10 @@ def main():
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
                                                           "construction"])
     args = ap.parse_args()
-    if args.task != "soccer":
+    if args.task not in ("soccer", "bipedal"):
         args.mono = True  # one fused wave-per-env launch per step
     if args.precision is None:
-        args.precision = "f64" if args.task == "soccer" else "f32"
+        args.precision = "f64"
     if args.envs <= 0:
         args.envs = {"bipedal": 8192, "mixed": 1024, "assembly": 1024, "construction": 1024}.get(args.task, 4096)
 
@@ -542,7 +570,8 @@ def main():
         pool = [((torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * lim).contiguous() for _ in range(16)]
     elif args.task == "bipedal":
         from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
-        env = BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
+        env = BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
+                               staged=not args.mono, banks=min(args.banks, 1) if args.banks > 0 else 0)
         pool = [((torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0).contiguous() for _ in range(16)]
     elif args.task == "assembly":
         from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
@@ -595,7 +624,8 @@ def main():
     acc, elapsed, value = whole_job_value(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
     if rank == 0 and args.task == "bipedal":
-        bytes_per_launch = BIPEDAL_ALG_BYTES * N
+        bytes_per_launch = (BIPEDAL_ALG_BYTES_F64 if args.precision == "f64" else BIPEDAL_ALG_BYTES) * N
+        bmode = "mono" if args.mono else "staged"
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         out = {
             "metric": BIPEDAL_METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
@@ -604,16 +634,20 @@ def main():
             "data": "synthetic (U(-100,100) actions, Philox reset draws)",
             "config": {"workload": "bipedal_rescue_env, 8192 envs/GPU (BASELINE configs[3])", "envs_per_gpu": N,
                        "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
-                       "integrator": "RK4", "step_kernels": "mono", "episodes_started": int(acc[1].item()),
+                       "integrator": "RK4", "step_kernels": bmode, "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "capacity_overflow_steps": overflow_steps,
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(PMC_PROFILE_BIPEDAL, N, args.precision,
-                                                                                  "mono"),
-                         "kernel": "mgx_bipedal_step = k_bipedal<float,0,GB>", "alg_bytes_per_step": bytes_per_launch,
-                         "launch_ms": round(launch_ms, 4)},
+                                                                                  bmode),
+                         "kernel": ("mgx_bipedal_step = 4 x (k_rk_rows + k_pgs_groups + k_rk_finish) + k_rk_settle"
+                                    if bmode == "staged" else "mgx_bipedal_step = k_bipedal<T,0,GB>"),
+                         "alg_bytes_per_step": bytes_per_launch, "launch_ms": round(launch_ms, 4)},
         }
+        if not args.no_f64_line:
+            other = "f32" if args.precision == "f64" else "f64"
+            out[f"{other}_line"] = bipedal_other_line(args, dev, N, g, other)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_bipedal(max(1, args.cpu_envs // 8), args.cpu_steps // 10)
         print(json.dumps(out))

@@ -332,9 +332,21 @@ typedef struct mgx_bipedal_env {
   double *prev_robot_pos;    /* [N][3] */
   int32_t *episode;          /* [N] episodes started (keys device reset draws); nullable with host draws */
   void *rollout;             /* [N][4] reward, terminated, truncated, env steps (nullable) */
+  void *workspace;           /* nullable: staged RK4 step workspace (mgx_bipedal_workspace_bytes), bound to
+                                (model, N, banks); NULL = one wave per env for the whole step */
+  uint64_t workspace_bytes;
+  int32_t banks;             /* reset banks per env of the staged step (0 = every reset settles in place) */
 } mgx_bipedal_env;
 
 int mgx_bipedal_configure(mgx_model *m, const mgx_bipedal_ids *ids);
+
+/* Staged RK4 step (configs[3]): per RK4 stage a row builder (one wave per slot), the lane-group
+ * PGS (mgx_soccer_step's solver) and a stage finisher, with reset banks settled as extra slots
+ * and every reset settled by the same stages. Workspace bytes for (model, N, banks) and its
+ * initialisation (zeroes it, computes the checkAcc template); bound to the model, N and banks. */
+int64_t mgx_bipedal_workspace_bytes(const mgx_model *m, int n_env, int banks);
+int mgx_bipedal_workspace_init(const mgx_model *m, void *workspace, uint64_t bytes, int n_env, int banks,
+                               void *stream);
 
 /* One env step for N envs (rescue_env.py:416-471): clip to +-100, ctrl[:26], float32 energy,
  * one RK4 mj_step, victim pickup / rescue, observation [N][102] float32, reward [N] float64,

@@ -163,7 +163,8 @@ class MgxBipedalEnv(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ["step", "energy", "energy_used", "rescued", "carried", "carrying", "closest", "prev_rescued",
                  "prev_carried", "prev_sz", "fall_timer", "victims_rescued", "distance", "ttfr", "falls", "collisions",
-                 "prev_robot_pos", "episode", "rollout"]]
+                 "prev_robot_pos", "episode", "rollout"]] + \
+               [("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32)]
 
 
 class MgxBipedalLogicIO(C.Structure):

@@ -484,8 +484,9 @@ static int pgs_arena_bytes(int precision) {
   return pgs_lanes() == 64 ? a / 2 : a;
 }
 
-// Staged-step workspace layout for (model, n_env, banks); offsets in bytes, 256-aligned.
-static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P) {
+// Staged-step workspace layout for (model, n_env, banks); offsets in bytes, 256-aligned. rk: the
+// RK4 staged step's extra arrays (stage carry, template scratch); nobs: floats per bank observation.
+size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P, bool rk, int nobs) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nq = m->precision == MGX_F32 ? m->mf.nq : m->md.nq;
   int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
@@ -498,6 +499,12 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   const char* cap_env = getenv("MGX_PGS_LDS_ROWS");
   int capE = cap_env ? (atoi(cap_env) + 3) / 4 * 4 : MGX_PGS_LDS_ROWS;
   if (capE < 4 || capE > MGX_PGS_LDS_ROWS) capE = MGX_PGS_LDS_ROWS;
+  if (rk) {
+    // the RK4 pipeline's rows (bipedal: ~150 per forward, up to 512): MGX_RK_LDS_ROWS, default 256
+    const char* rk_env = getenv("MGX_RK_LDS_ROWS");
+    capE = rk_env ? (atoi(rk_env) + 3) / 4 * 4 : 256;
+    if (capE < 4) capE = 256;
+  }
   p.capE = p.maxE < capE ? p.maxE : capE;
   // LDS arena of one main-launch solver wave (scalars + block table + B of its slots); the
   // test / tuning hook MGX_PGS_ARENA overrides it (read per call; a small arena sends waves to
@@ -508,6 +515,8 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
+  p.tw = nv > 56 ? 16 : 8;
+  p.nobs = nobs;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t r = off; off = (off + bytes + 255) / 256 * 256; return r; };
   size_t S = (size_t)p.S, NB = (size_t)n_env * (banks > 0 ? banks : 1);
@@ -516,28 +525,42 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
   p.o_carryi = take(S * p.carryi_stride * 4);
   p.o_ne = take(S * 4); p.o_blen = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_k2big = take(S * 4); p.o_fix = take((size_t)n_env * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
-  p.o_blk = take(S * p.maxE * 4);  // 8 uint16 per 4-row block
+  p.o_blk = take(S * p.maxE * p.tw / 2);  // tw uint16 per 4-row block
   p.o_B = take(S * (size_t)p.bcap * rb);
   p.o_vout = take(S * 64 * rb);
   p.o_bq = take(NB * nq * rb); p.o_bv = take(NB * nv * rb); p.o_ba = take(NB * nv * rb); p.o_btime = take(NB * rb);
-  p.o_bobs = take(NB * 80 * 4); p.o_bprev = take(NB * 6 * rb); p.o_bwind = take(NB * 3 * rb);
+  p.o_bobs = take(NB * nobs * 4); p.o_bprev = take(NB * 6 * rb); p.o_bwind = take(NB * 3 * rb);
   p.o_bk = take(NB * 4); p.o_bep = take(NB * 4); p.o_bwarn = take(NB * 4); p.o_bseed = take(NB * 8);
   int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
   p.maxC = m->Ls.max_ncon;
   p.o_tq = take(nq * rb); p.o_tv = take(nv * rb); p.o_ta = take(64 * rb); p.o_tt = take(rb);
   p.o_tx = take(3 * nb * rb); p.o_txq = take(4 * nb * rb); p.o_tsc = take(3 * nb * rb); p.o_tn = take(4);
   p.o_tcg = take(2 * p.maxC * 4); p.o_tcd = take(p.maxC * rb); p.o_tcm = take(p.maxC * rb);
+  if (rk) {
+    const int nq4 = (nq + 3) & ~3;
+    p.rk_stride = 2 * nq4 + 8 * 64 + 4;
+    p.o_rk = take(S * p.rk_stride * rb);
+    p.o_rks = take(S * 4);
+    p.o_rkw = take(S * 4);
+    p.o_tscr = take(m->L.gB ? (size_t)m->L.gB_stride * rb : 64);
+  }
   if (P) *P = p;
   return off;
+}
+static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P) {
+  return make_staged_pipe(m, ws, n_env, banks, P, false, 80);
 }
 
 // LDS of one solver wave holding `rows` rows per slot (main launch: min(max_nefc,
 // MGX_PGS_LDS_ROWS); wide launch: max_nefc)
-static int pgs_lds_bytes(const mgx_model* m, int rows) {
+int mgx::staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int tw) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nb3 = (rows / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
-  const int spw = 64 / pgs_lanes();
-  return spw * (MGX_SCAL * 4 * nb3 + 4) * rb + spw * nb3 * 32 + 64;
+  const int spw = 64 / lps;
+  return spw * (MGX_SCAL * 4 * nb3 + 4) * rb + spw * nb3 * 4 * tw + 64;
+}
+static int pgs_lds_bytes(const mgx_model* m, int rows) {
+  return staged_pgs_lds_bytes(m, rows, pgs_lanes(), 8);
 }
 
 // A side stream and two events per caller stream (created once, kept for the process): the wide
@@ -702,7 +725,12 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024 || (d->layout_flags & MGX_ROWS_IN_SCRATCH))
     m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, false, true);
-  m->Ls = make_layout(d, rb, max_ncon, m->staged_ok ? max_nefc : 4, 128, true);
+  // the staged RK4 step (mgx_rk_staged.h, bipedal_rescue): RK4 + PGS, nv 49..64 (four register
+  // entries per solver lane, a 16-word block table)
+  m->staged_rk_ok = d->integrator == 1 && d->solver == 0 && condim13 && d->nv > 48 && d->nv <= 64 &&
+                    max_nefc <= 1024 && max_ncon <= 128;
+  const bool any_staged = m->staged_ok || m->staged_rk_ok;
+  m->Ls = make_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active, true);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;
   if (precision == MGX_F32) {

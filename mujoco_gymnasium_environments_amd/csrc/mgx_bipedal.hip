@@ -166,6 +166,8 @@ int mgx_bipedal_configure(mgx_model* m, const mgx_bipedal_ids* ids) {
     return fail(MGX_E_ARG, "root joint address out of range");
   int rc = f32 ? configure_lds<float>(m) : configure_lds<double>(m);
   if (rc != MGX_OK) return rc;
+  rc = bipedal_staged_configure(m);
+  if (rc != MGX_OK) return rc;
   BipedalIds& o = m->bp;
   o.torso = ids->torso;
   for (int i = 0; i < 5; i++) {
@@ -190,9 +192,12 @@ int mgx_bipedal_step(const mgx_model* m, const mgx_state* s, const mgx_bipedal_e
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
-  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (e->workspace)  // the staged RK4 step (mgx_rk_staged.hip)
+    return bipedal_step_staged(m, s, e, action, obs, reward, terminated, truncated, final_obs, autoreset, seed,
+                               env_offset, n_env, mask, st);
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (m->precision == MGX_F32)
     launch<float, 0>(m, m->mf, s, e, action, nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
                      env_offset, n_env, mask, st);
@@ -211,9 +216,11 @@ int mgx_bipedal_reset(const mgx_model* m, const mgx_state* s, const mgx_bipedal_
   if (!draws && !e->episode) return fail(MGX_E_ARG, "device draws need the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
-  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (e->workspace)
+    return bipedal_reset_staged(m, s, e, draws, obs, seed, env_offset, n_env, mask, st);
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (m->precision == MGX_F32)
     launch<float, 1>(m, m->mf, s, e, nullptr, (const float*)draws, obs, nullptr, nullptr, nullptr, nullptr, 0, seed,
                      env_offset, n_env, mask, st);

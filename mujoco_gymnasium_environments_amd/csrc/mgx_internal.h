@@ -41,6 +41,7 @@ struct mgx_model {
   int npair;
   bool wide = false;       // nv > 64: only the wide kernels (mgx_wide.h) run this model
   bool staged_ok = false;  // the staged soccer pipeline supports this model's capacities
+  bool staged_rk_ok = false;  // the staged RK4 pipeline (bipedal) supports this model
 };
 
 namespace mgx {
@@ -95,6 +96,19 @@ void launch_soccer_settle(const DevModel<T>& Ms, const DevModel<T>& Mf, const So
                           const uint8_t* mask, const Pipe& P, int mode, int grid, int lds, hipStream_t st, int maxit, T tol,
                           T scale);
 int staged_kernels_configure(int precision, int ls, int lf, int settle);
+// staged-step workspace layout (mgx_api.hip) and the LDS of one solver wave holding `rows` rows
+// per slot with `lps` lanes per slot and `tw` table words per block
+size_t make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P, bool rk, int nobs);
+int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int tw);
+// the staged RK4 bipedal step (mgx_rk_staged.hip)
+int bipedal_staged_configure(const mgx_model* m);
+int bipedal_step_staged(const mgx_model* m, const mgx_state* s, const mgx_bipedal_env* e, const float* action, float* obs,
+                        double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
+                        uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st);
+int bipedal_reset_staged(const mgx_model* m, const mgx_state* s, const mgx_bipedal_env* e, const void* draws,
+                         float* obs, uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st);
+int64_t bipedal_workspace_bytes(const mgx_model* m, int n_env, int banks);
+int bipedal_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, hipStream_t st);
 int pgs_lanes();
 int pgs_lds_b();
 }  // namespace mgx

@@ -54,8 +54,17 @@ struct Pipe {
   // the checkAcc template: mj_step's outcome after mj_resetData (state + forward frames)
   size_t o_tq, o_tv, o_ta, o_tt, o_tx, o_txq, o_tsc, o_tn, o_tcg, o_tcd, o_tcm;
   int maxC;
+  int tw;              // block-table words per 4-row block (8: nv <= 56, 16: nv <= 64)
+  int nobs;            // floats of a bank's reset observation
+  // RK4 staged step (mgx_rk_staged.h): per slot the stage carry (rk_stride reals: X0 positions,
+  // the stage's positions, stage velocities / accelerations, t0 / t_k), its state in the step
+  // (o_rks) and the warnings / overflow gathered over its stages (o_rkw); o_tscr: the template
+  // kernel's row scratch (monolithic layout with rows in global memory)
+  int rk_stride;
+  size_t o_rk, o_rks, o_rkw, o_tscr;
   template <typename X> __device__ __forceinline__ X* at(size_t off) const { return reinterpret_cast<X*>(base + off); }
-  // [0] fixup count, [1] solver-list count, [2] wide-solver-list count
+  // [0] fixup count, [1] solver-list count, [2] wide-solver-list count, [3] / [4] the last
+  // step's list sizes, [5] RK4 step: fixup count (k_pgs_groups clears [0] at every launch)
   __device__ __forceinline__ int* ctr() const { return at<int>(o_ctr); }
 };
 
@@ -162,8 +171,9 @@ struct ContactMeta {
   T mu0, mu1;
 };
 template <typename T>
-__device__ __forceinline__ void contact_meta(const DevModel<T>& m, const Env<T>& e, int ncf, ContactMeta<T>& cm) {
-  const int c = lane_id();
+__device__ __forceinline__ void contact_meta(const DevModel<T>& m, const Env<T>& e, int ncf, ContactMeta<T>& cm,
+                                             int c0 = 0) {
+  const int c = c0 + lane_id();
   cm.dim = 3; cm.b1 = 0; cm.b2 = 0; cm.rt1 = 0; cm.rt2 = 0; cm.m1 = 0; cm.m2 = 0; cm.mu0 = 0; cm.mu1 = 0;
   if (c < ncf) {
     int p = e.con_pair[c];
@@ -201,9 +211,12 @@ __device__ __forceinline__ double readlane_t(double x, int l) { return readlane(
 // B = D^-1/2 L'^-1 J' by a readlane sweep over the block's dof support only (the two bodies'
 // chains, closed under ancestors, highest dof first); then B.B and the block couplings A_ij,
 // the row scalars and B -> pipe.
-template <typename T>
+// TW: block-table words per 4-row block (the A offset, then one per 8-dof group): 8 for nv <= 56,
+// 16 for nv <= 64. C2: contacts 64..127 read their metadata from cm2 (lane c - 64).
+template <typename T, int TW = 8, bool C2 = false>
 __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, const Pipe& P, int r0, int nlim, int nlim4,
-                                            const ContactMeta<T>& cm, T dinvs, T* scal, int* blk, T* Bo, int& boff) {
+                                            const ContactMeta<T>& cm, const ContactMeta<T>& cm2, T dinvs, T* scal,
+                                            int* blk, T* Bo, int& boff) {
   const int l = lane_id();
   const int nv = m.nv;
   const bool dl = l < nv;
@@ -235,10 +248,12 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
     }
   } else {
     const int c = (r0 - nlim4) >> 2;
-    const int dim = readlane(cm.dim, c), b1 = readlane(cm.b1, c), b2 = readlane(cm.b2, c);
-    const int rt1 = readlane(cm.rt1, c), rt2 = readlane(cm.rt2, c);
-    const uint64_t m1 = readlane_u64(cm.m1, c), m2 = readlane_u64(cm.m2, c);
-    const T mu0 = readlane_t(cm.mu0, c), mu1 = readlane_t(cm.mu1, c);
+    const ContactMeta<T>& cs = (C2 && c >= 64) ? cm2 : cm;
+    const int cl = C2 ? (c & 63) : c;
+    const int dim = readlane(cs.dim, cl), b1 = readlane(cs.b1, cl), b2 = readlane(cs.b2, cl);
+    const int rt1 = readlane(cs.rt1, cl), rt2 = readlane(cs.rt2, cl);
+    const uint64_t m1 = readlane_u64(cs.m1, cl), m2 = readlane_u64(cs.m2, cl);
+    const T mu0 = readlane_t(cs.mu0, cl), mu1 = readlane_t(cs.mu1, cl);
     const T* fr = e.con_frame + 9 * c;
     const T* cp = e.con_pos + 3 * c;
     sup = m1 | m2;
@@ -352,8 +367,8 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
       T* og = o + 8 + 32 * __popc(gm & ((1u << g) - 1u)) + 4 * jj;
       og[0] = j0; og[1] = j1; og[2] = j2; og[3] = j3;
     }
-    if (l < 8) {
-      uint16_t* bt = reinterpret_cast<uint16_t*>(blk) + 8 * (r0 >> 2);
+    if (l < TW) {
+      uint16_t* bt = reinterpret_cast<uint16_t*>(blk) + TW * (r0 >> 2);
       int v = l == 0 ? boff : (((gm >> (l - 1)) & 1u) ? boff + 8 + 32 * __popc(gm & ((1u << (l - 1)) - 1u)) : 0);
       bt[l] = (uint16_t)v;
     }
@@ -365,7 +380,7 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
 // S1 body: forward up to the constraint rows, rows -> pipe, carry -> pipe
 // list_slot: enter the slot in the solver launches' lists (the pipeline); the one-wave settle
 // (settle_step) solves the slot itself.
-template <typename T>
+template <typename T, int TW = 8, bool C2 = false>
 __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot, int warn,
                                            bool list_slot = true) {
   int l = lane_id();
@@ -393,7 +408,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
     const T dinvs = dl ? sqrt(e.diaginv) : (T)0;
     T* scal = P.at<T>(P.o_scal) + (size_t)slot * P.maxE * MGX_SCAL;
     T* Bo = P.at<T>(P.o_B) + (size_t)slot * P.bcap;
-    int* blk = P.at<int>(P.o_blk) + (size_t)slot * P.maxE;  // 8 uint16 per 4-row block
+    int* blk = P.at<int>(P.o_blk) + (size_t)slot * (P.maxE * TW / 8);  // TW uint16 per 4-row block
     const int nlim4 = (nlim + 3) & ~3;
     // qacc_smooth / qacc_warmstart into LDS (limit rows) and their per-body chain sums
     if (dl) { e.vec1[l] = e.qacc_smooth; e.vec2[l] = e.qacc_ws; }
@@ -416,11 +431,13 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
       wsync();
     }
     rows_impedance(m, e, ne, nlim, nlim4, scal);
-    ContactMeta<T> cm;
+    ContactMeta<T> cm, cm2;
     contact_meta(m, e, ncf, cm);
+    if constexpr (C2) contact_meta(m, e, ncf, cm2, 64);
     __threadfence();  // the row constants are read back by other lanes of this wave (build_block)
     wsync();
-    for (int r0 = 0; r0 < ne; r0 += 4) build_block(m, e, P, r0, nlim, nlim4, cm, dinvs, scal, blk, Bo, boff);
+    for (int r0 = 0; r0 < ne; r0 += 4)
+      build_block<T, TW, C2>(m, e, P, r0, nlim, nlim4, cm, cm2, dinvs, scal, blk, Bo, boff);
   }
   MGX_STAMP(7);
   // carry + registers + ints
@@ -523,14 +540,14 @@ struct PgsTab {
   uint32_t a, g[EPL];
 };
 
-template <int EPL, int LPS>
+template <int EPL, int LPS, int TW = 8>
 __device__ __forceinline__ void pgs_load_tab(PgsTab<EPL>& t, const uint32_t* bt, int blk, int j) {
-  const uint32_t* e = bt + 8 * blk;  // widened in LDS: no 16-bit extracts on the address path
+  const uint32_t* e = bt + TW * blk;  // widened in LDS: no 16-bit extracts on the address path
   t.a = e[0];
 #pragma unroll
   for (int d = 0; d < EPL; d++) {
     const int gi = d * (LPS / 8) + (j >> 3);
-    t.g[d] = gi < 7 ? e[1 + gi] : 0u;
+    t.g[d] = gi < TW - 1 ? e[1 + gi] : 0u;
   }
 }
 
@@ -561,11 +578,11 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.qh = q[4];
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
 }
-template <typename T, int EPL, int LPS>
+template <typename T, int EPL, int LPS, int TW = 8>
 __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint32_t* bt,
                                                int blk, int j) {
   PgsTab<EPL> t;
-  pgs_load_tab<EPL, LPS>(t, bt, blk, j);
+  pgs_load_tab<EPL, LPS, TW>(t, bt, blk, j);
   pgs_load_block<T, EPL, LPS>(k, Bsl, sc, t, blk, j);
 }
 
@@ -646,7 +663,7 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
 // !BLDS (global-B launch): fixed per-slot capacity of capE rows of scalars and table in LDS, B
 // read from global memory (L2 / MALL) with a register ring RING - 1 blocks ahead.
 // Both run the identical arithmetic on every slot, so which launch solves a slot is invisible.
-template <typename T, int EPL, int LPS, bool BLDS>
+template <typename T, int EPL, int LPS, bool BLDS, int TW = 8>
 __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* list, int cnt, int base, int capE, int maxit,
                                           T tol, T scale, int spw) {
   constexpr int RING = BLDS ? MGX_PGS_RING_LDS : MGX_PGS_RING;
@@ -669,7 +686,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   const int nbRun = (nbMax + RING - 1) / RING * RING;
   const size_t sl = (size_t)(slot >= 0 ? slot : 0);
   const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
-  const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * P.maxE);
+  const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * (P.maxE * TW / 8));
   const T* gB = P.at<T>(P.o_B) + sl * P.bcap;
   int nbA;  // blocks of scalars / table entries per slot (the look-ahead stays inside)
   T* sc;
@@ -678,7 +695,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   if constexpr (BLDS) {
     nbA = nbRun + RING - 1;
     const int blen = slot >= 0 ? (P.at<int>(P.o_blen)[slot] + 3) & ~3 : 0;
-    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 32) + blen * (int)sizeof(T);  // 16-byte multiple
+    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 4 * TW) + blen * (int)sizeof(T);  // 16-byte multiple
     int off = 0, tot = 0;
 #pragma unroll
     for (int q = 0; q < SPW; q++) {
@@ -692,7 +709,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     }
     sc = reinterpret_cast<T*>(smem + off);
     bt = reinterpret_cast<uint32_t*>(sc + 4 * MGX_SCAL * nbA);
-    T* Bs = reinterpret_cast<T*>(bt + 8 * nbA);
+    T* Bs = reinterpret_cast<T*>(bt + TW * nbA);
     for (int q = 4 * j; q < blen; q += 4 * LPS)
       *reinterpret_cast<V4*>(Bs + q) = *reinterpret_cast<const V4*>(gB + q);
     Bsl = Bs;
@@ -702,12 +719,12 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     nbA = (nbcap + RING - 1) / RING * RING;
     const int sstride = MGX_SCAL * 4 * nbA + 4;  // 16-byte aligned per slot
     sc = reinterpret_cast<T*>(smem) + s * sstride;
-    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * 8 * nbA;
+    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * TW * nbA;
     Bsl = gB;
   }
   for (int q = j; q < MGX_SCAL * 4 * nbA; q += LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
   // block table: the slot's blocks, then zero-group entries up to the capacity
-  for (int q = j; q < 8 * nbA; q += LPS) bt[q] = q < 8 * nblk ? (uint32_t)gbt[q] : 0u;
+  for (int q = j; q < TW * nbA; q += LPS) bt[q] = q < TW * nblk ? (uint32_t)gbt[q] : 0u;
   __syncthreads();
   // warmstart: v = B' f, dual cost, reset to zero if the cost is positive
   T v[EPL];
@@ -715,7 +732,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   for (int d = 0; d < EPL; d++) v[d] = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS>(k, Bsl, sc, bt, b, j);
+    pgs_load_block<T, EPL, LPS, TW>(k, Bsl, sc, bt, b, j);
     const T* qf = sc + 4 * b * MGX_SCAL + MGX_SQ(1, 0);
     bool ok = b < nblk;
     T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[1] : (T)0, f2 = ok ? qf[2] : (T)0, f3 = ok ? qf[3] : (T)0;
@@ -724,7 +741,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
   T cpart = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS>(k, Bsl, sc, bt, b, j);
+    pgs_load_block<T, EPL, LPS, TW>(k, Bsl, sc, bt, b, j);
     T d0, d1, d2, d3;
     pgs_dots(k, v, d0, d1, d2, d3);
     slot_sum4<LPS>(d0, d1, d2, d3);
@@ -759,11 +776,11 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
     T impr = 0;
     PgsBlk<T, EPL> R[RING];
     PgsTab<EPL> tn;  // the table entry of the next block to load (one ring step ahead of its data)
-    pgs_load_tab<EPL, LPS>(tn, bt, 0, j);
+    pgs_load_tab<EPL, LPS, TW>(tn, bt, 0, j);
 #pragma unroll
     for (int k = 0; k < RING - 1; k++) {
       pgs_load_block<T, EPL, LPS>(R[k], Bsl, sc, tn, k, j);
-      pgs_load_tab<EPL, LPS>(tn, bt, k + 1, j);
+      pgs_load_tab<EPL, LPS, TW>(tn, bt, k + 1, j);
     }
     // full ring turns, no early exit inside, so every prefetch is consumed on every path and
     // the compiler cannot sink the loads next to their use. The table has zero entries up to
@@ -774,7 +791,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
         // the slot consumed last lands the block RING - 1 ahead, then block b0 + k is solved
         const int bn = min(b0 + k + RING - 1, nbA - 1);
         pgs_load_block<T, EPL, LPS>(R[(k + RING - 1) % RING], Bsl, sc, tn, bn, j);
-        pgs_load_tab<EPL, LPS>(tn, bt, min(bn + 1, nbA - 1), j);
+        pgs_load_tab<EPL, LPS, TW>(tn, bt, min(bn + 1, nbA - 1), j);
         pgs_block<T, EPL, LPS>(R[k], v, sc, 4 * (b0 + k), act && b0 + k < nblk, impr);
       }
     }
@@ -810,7 +827,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
 // the slots with capE < nefc <= maxE and those of LDS-arena waves that did not fit, grid-stride
 // over a small grid with maxE rows of scalars per slot in LDS. BLDS (main launch only): B in
 // the wave's LDS arena; otherwise B is read from global memory (L2 / MALL).
-template <typename T, int EPL, int LPS, bool BLDS>
+template <typename T, int EPL, int LPS, bool BLDS, int TW = 8>
 __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw, int big) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (!big && blockIdx.x == 0 && threadIdx.x == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
@@ -818,7 +835,7 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   const int* list = P.at<int>(big ? P.o_k2big : P.o_k2list);
   const int spn = spw < 0 ? -spw : spw;
   for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
-    pgs_group<T, EPL, LPS, BLDS && true>(P, smem, list, cnt, base, big ? P.maxE : P.capE, maxit, tol, scale, spw);
+    pgs_group<T, EPL, LPS, BLDS && true, TW>(P, smem, list, cnt, base, big ? P.maxE : P.capE, maxit, tol, scale, spw);
     __syncthreads();  // the next group reuses the LDS
   }
 }

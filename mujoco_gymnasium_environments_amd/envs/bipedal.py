@@ -29,7 +29,7 @@ import torch
 
 from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
-from ..native import check, lib
+from ..native import NativeError, check, lib
 from ..seeding import np_random
 from ..spaces import Box, EnvBase
 
@@ -110,7 +110,13 @@ class BipedalVectorEnv:
     metadata = {'render_modes': [], 'render_fps': 50}
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64", seed: int = 0,
-                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0):
+                 max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
+                 staged: bool = True, banks: int = 1):
+        """``staged`` selects the staged RK4 step (csrc/mgx_rk_staged.hip: per RK4 stage a row
+        builder, the lane-group PGS and a stage finisher, with ``banks`` reset states settled ahead
+        per env); ``staged=False`` runs one wave per env for the whole step. An episode lasts at
+        least 101 steps unless truncated earlier (the fall timer, rescue_env.py:670-697), so one
+        bank, ready 10 steps after it restarts, covers every autoreset."""
         self.num_envs = num_envs
         self.device = torch.device(device)
         self.model = bipedal_model()
@@ -154,6 +160,18 @@ class BipedalVectorEnv:
             self.ttfr, self.falls, self.collisions, self.prev_robot_pos, self.episode, self.rollout)])
         ids = self.tables.ids_struct()
         check(lib().mgx_bipedal_configure(self.native.handle, C.byref(ids)), "mgx_bipedal_configure")
+        self.staged = staged
+        self.workspace = None
+        if staged:
+            nb = int(lib().mgx_bipedal_workspace_bytes(self.native.handle, N, banks))
+            if nb <= 0:
+                raise NativeError(f"mgx_bipedal_workspace_bytes: {lib().mgx_last_error().decode()}")
+            self.workspace = torch.empty(nb, dtype=torch.uint8, device=dev)
+            check(lib().mgx_bipedal_workspace_init(self.native.handle, _ptr(self.workspace), nb, N, banks, None),
+                  "mgx_bipedal_workspace_init")
+            self._env.workspace = self.workspace.data_ptr()
+            self._env.workspace_bytes = nb
+            self._env.banks = banks
         self.action_space = Box(low=-ACTION_LIMIT, high=ACTION_LIMIT, shape=(N_ACT,), dtype=np.float32)
 
     def reset(self, seed: Optional[int] = None, env_mask: Optional[torch.Tensor] = None,
@@ -234,8 +252,9 @@ class BipedalRescueEnv(EnvBase):
         self.victim_priorities = [0.8, 1.0, 0.7, 0.9, 1.0]
         self.fire_zones = [{'pos': np.array([-5.0, -3.0, 0.0]), 'radius': 1.5},
                            {'pos': np.array([8.0, 6.0, 0.0]), 'radius': 1.2}]
+        # one env: the single-launch monolithic kernel has the lowest step latency
         self._vec = BipedalVectorEnv(1, device=device, precision=precision, autoreset=False,
-                                     max_episode_steps=self.max_episode_steps)
+                                     max_episode_steps=self.max_episode_steps, staged=False)
         self.model = self._vec.model
         self.num_actuators = N_ACT
         self.action_space = Box(low=-ACTION_LIMIT, high=ACTION_LIMIT, shape=(N_ACT,), dtype=np.float32)
