@@ -347,6 +347,12 @@ int mgx_bipedal_configure(mgx_model *m, const mgx_bipedal_ids *ids);
 int64_t mgx_bipedal_workspace_bytes(const mgx_model *m, int n_env, int banks);
 int mgx_bipedal_workspace_init(const mgx_model *m, void *workspace, uint64_t bytes, int n_env, int banks,
                                void *stream);
+/* Diagnostics (n_out >= 6; up to 12 values): byte offset of the per-slot RK4 stage carry, its
+ * stride (reals), the offsets of the per-slot step state and row counts, the slot count, bytes
+ * per real, the offset of the row scalars, rows per slot, the offset of the solver sweep counts,
+ * the offset and per-slot capacity (reals) of the compressed rows B, the offset of the block
+ * tables (16 uint16 per 4-row block). */
+int mgx_bipedal_workspace_layout(const mgx_model *m, int n_env, int banks, int64_t *out, int n_out);
 
 /* One env step for N envs (rescue_env.py:416-471): clip to +-100, ctrl[:26], float32 energy,
  * one RK4 mj_step, victim pickup / rescue, observation [N][102] float32, reward [N] float64,

@@ -704,6 +704,17 @@ int bipedal_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, 
 }  // namespace mgx
 
 extern "C" {
+int mgx_bipedal_workspace_layout(const mgx_model* m, int n_env, int banks, int64_t* out, int n_out) {
+  if (!m || !out || n_env <= 0 || banks < 0 || banks > 16 || n_out < 6) return fail(MGX_E_ARG, "bad argument");
+  if (!m->staged_rk_ok) return fail(MGX_E_UNSUPPORTED, "staged RK4 step: model outside the staged pipeline's range");
+  Pipe P;
+  make_staged_pipe(m, nullptr, n_env, banks, &P, true, RK_OBS);
+  const int64_t v[12] = {(int64_t)P.o_rk, P.rk_stride, (int64_t)P.o_rks, (int64_t)P.o_ne, P.S,
+                         m->precision == MGX_F32 ? 4 : 8, (int64_t)P.o_scal, P.maxE, (int64_t)P.o_niter,
+                         (int64_t)P.o_B, P.bcap, (int64_t)P.o_blk};
+  for (int i = 0; i < (n_out < 12 ? n_out : 12); i++) out[i] = v[i];
+  return MGX_OK;
+}
 int64_t mgx_bipedal_workspace_bytes(const mgx_model* m, int n_env, int banks) {
   return bipedal_workspace_bytes(m, n_env, banks);
 }

@@ -362,8 +362,10 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
     for (int g = 0; g < 8; g++) gm |= ((sup >> (8 * g)) & 0xffull) ? (1u << g) : 0u;
     T* o = Bo + boff;
     if (l < 8) o[l] = l == 0 ? a10 : l == 1 ? a20 : l == 2 ? a21 : l == 3 ? a30 : l == 4 ? a31 : l == 5 ? a32 : (T)0;
+    // every lane of a touched group stores, so a group that runs past nv (bipedal: dofs 56..62 and
+    // the phantom 63) carries zeros there, not the slot's stale data (j* are 0 on lanes >= nv)
     const int g = l >> 3, jj = l & 7;
-    if (dl && ((gm >> g) & 1u)) {
+    if ((gm >> g) & 1u) {
       T* og = o + 8 + 32 * __popc(gm & ((1u << g) - 1u)) + 4 * jj;
       og[0] = j0; og[1] = j1; og[2] = j2; og[3] = j3;
     }

@@ -108,6 +108,7 @@ _SIGS = {
     "mgx_soccer_logic_test": ([_VP, C.POINTER(cabi.MgxSoccerLogicIO), C.c_int, _VP], C.c_int),
     "mgx_bipedal_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
     "mgx_bipedal_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
+    "mgx_bipedal_workspace_layout": ([_VP, C.c_int, C.c_int, C.POINTER(C.c_int64), C.c_int], C.c_int),
     "mgx_soccer_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
     "mgx_soccer_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
     "mgx_soccer_workspace_layout": ([_VP, C.c_int, C.c_int, C.POINTER(C.c_int64), C.c_int], C.c_int),

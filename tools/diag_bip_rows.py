@@ -1,0 +1,66 @@
+"""Diagnostic: the staged RK4 step's stage-3 constraint rows, decompressed from the pipe (B per
+4-row block: A couplings, then 32 reals per touched 8-dof group; a 16-word block table), against
+the CPU oracle at the same stage state: A = B B' vs the oracle's efc_AR - diag(R), row by row."""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from mujoco_gymnasium_environments_amd import cabi
+from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+from mujoco_gymnasium_environments_amd.native import lib
+from mujoco_gymnasium_environments_amd.seeding import np_random
+from oracle.mjref import RefSim
+
+n = 6
+a = BipedalVectorEnv(n, precision="f64", autoreset=False, staged=True)
+m = a.model
+packed = cabi.pack_model(m)
+lay = (C.c_int64 * 12)()
+lib().mgx_bipedal_workspace_layout(a.native.handle, n, 1, lay, 12)
+o_rk, stride, o_rks, o_ne, S, rb, o_scal, maxE, o_niter, o_B, bcap, o_blk = list(lay)
+nq4 = (m.nq + 3) & ~3
+draws = np.stack([a.tables.reset_draws(np_random(200 + i)[0]) for i in range(n)])
+a.reset(draws=draws)
+rng = np.random.default_rng(11)
+sim = RefSim(packed)
+for k in range(4):
+    ws = a.batch.qacc_warmstart.cpu().numpy().copy()
+    act = torch.from_numpy((rng.uniform(-1, 1, (n, 26)) * 10.0).astype(np.float32)).cuda()
+    a.step(act)
+    torch.cuda.synchronize()
+    W = a.workspace
+    rk = W[o_rk:o_rk + S * stride * rb].view(torch.float64).reshape(S, stride).cpu().numpy()
+    Bw = W[o_B:o_B + S * bcap * rb].view(torch.float64).reshape(S, bcap).cpu().numpy()
+    tab = W[o_blk:o_blk + S * maxE * 8].view(torch.int16).reshape(S, maxE // 4, 16).cpu().numpy().astype(np.int64) & 0xFFFF
+    ne_s = W[o_ne:o_ne + 4 * S].view(torch.int32).cpu().numpy()
+    ctrl = a.batch.ctrl.cpu().numpy()
+    for i in range(n):
+        x3 = rk[i, nq4:nq4 + m.nq]
+        v = rk[i, 2 * nq4:2 * nq4 + 256].reshape(4, 64)[:, :m.nv]
+        f = rk[i, 2 * nq4 + 256:2 * nq4 + 512].reshape(4, 64)[:, :m.nv]
+        sim.reset()
+        sim.qpos[:] = x3
+        sim.qvel[:] = v[3]
+        sim.ctrl[:] = ctrl[i]
+        sim.qacc_warmstart[:] = ws[i]
+        sim.forward()
+        err = float(np.max(np.abs(sim.qacc - f[3])))
+        ne = int(sim.nefc[0])
+        ncon = int(sim.ncon[0])
+        nlim = ne - 4 * ncon
+        nlim4 = (nlim + 3) // 4 * 4
+        ns = int(ne_s[i])
+        Bs = np.zeros((ns, 64))
+        for blk in range(ns // 4):
+            t = tab[i, blk]
+            for g in range(8):
+                off = t[1 + g]
+                Bs[4 * blk:4 * blk + 4, 8 * g:8 * g + 8] = Bw[i, off:off + 32].reshape(8, 4).T
+        # staged row index of each oracle row
+        idx = list(range(nlim)) + [nlim4 + q for q in range(4 * ncon)]
+        A_s = (Bs @ Bs.T)[np.ix_(idx, idx)]
+        A_o = sim.efc_AR[:ne * ne].reshape(ne, ne) - np.diag(sim.efc_R[:ne])
+        dA = np.abs(A_s - A_o)
+        r_bad = np.unique(np.nonzero(dA > 1e-6 * (1 + np.abs(A_o)))[0])
+        print(f"step {k} env {i}: err {err:.3g} nlim {nlim} ncon {ncon} max|dA| {dA.max():.3g} bad rows {list(r_bad[:12])}")
