@@ -563,6 +563,14 @@ static int pgs_lds_bytes(const mgx_model* m, int rows) {
   return staged_pgs_lds_bytes(m, rows, pgs_lanes(), 8);
 }
 
+// MGX_SIDE_STREAM=0 (read per call) runs the wide solver launch after the main one on the caller's
+// stream: with more streams than hardware queues (several tasks on one GPU, each on its own stream)
+// a side stream can queue behind another task's long kernels.
+int mgx::side_streams() {
+  const char* v = getenv("MGX_SIDE_STREAM");
+  return v ? atoi(v) != 0 : 1;
+}
+
 // A side stream and two events per caller stream (created once, kept for the process): the wide
 // solver launch runs beside the main one. nullptr if the runtime refuses (then both run in order).
 struct SideStream {
@@ -619,8 +627,10 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   // follows the main launch there.
   const int wgrid = 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, wlds = pgs_lds_bytes(m, P.maxE);
   const int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE);
-  SideStream* side = pgs_lds_b() ? nullptr : side_stream(st);
-  if (side) {
+  if (!pgs_lds_b() && P.maxE <= P.capE) {
+    // every slot fits the main launch (the default capacity): no wide launch at all
+    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
+  } else if (SideStream* side = (!pgs_lds_b() && side_streams()) ? side_stream(st) : nullptr) {
     HIPCHK(hipEventRecord(side->rows, st));
     HIPCHK(hipStreamWaitEvent(side->s, side->rows, 0));
     launch_pgs<T>(P, wgrid, wlds, side->s, M.iterations, M.tolerance, scale, 1);

@@ -100,6 +100,8 @@ int staged_kernels_configure(int precision, int ls, int lf, int settle);
 // per slot with `lps` lanes per slot and `tw` table words per block
 size_t make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P, bool rk, int nobs);
 int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int tw);
+// the wide solver launch beside the main one on a side stream (MGX_SIDE_STREAM, default 1)
+int side_streams();
 // the staged RK4 bipedal step (mgx_rk_staged.hip)
 int bipedal_staged_configure(const mgx_model* m);
 int bipedal_step_staged(const mgx_model* m, const mgx_state* s, const mgx_bipedal_env* e, const float* action, float* obs,

@@ -593,7 +593,7 @@ int step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms,
   const T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
   const int mlds = staged_pgs_lds_bytes(m, P.capE, RK_LPS, RK_TW), wlds = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, RK_TW);
   const int wgrid = 64 / RK_LPS * MGX_PGS_WIDE_GRID;
-  RkSide* side = rk_side(st);
+  RkSide* side = side_streams() ? rk_side(st) : nullptr;
   for (int k = 0; k < 4; k++) {
     hipLaunchKernelGGL(k_rk_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, m->bp, *s, *e, action, n_env, mask, P,
                        banks, k);

@@ -14,7 +14,8 @@ import os
 import shutil
 import sys
 
-STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_finish", "k_soccer_fixup", "k_soccer<float, 0>",
+STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_finish", "k_soccer_fixup", "k_soccer_settle",
+                "k_rk_rows", "k_rk_finish", "k_rk_settle", "k_soccer<float, 0>",
                 "k_soccer<double, 0>", "k_bipedal<float, 0, true>", "k_bipedal<float, 0, false>",
                 "k_parkour<float, 0>", "k_parkour<float, 0, true>", "k_parkour<float, 0, false>",
                 "k_martial<float, 0, true>", "k_martial<float, 0, false>",
@@ -46,7 +47,10 @@ def counter_means(d, counter):
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
         per.setdefault(k, {})
         per[k][key] = per[k].get(key, 0.0) + float(r["Counter_Value"])
-    return {k: sum(v.values()) / len(v) for k, v in per.items() if v}
+    # the settle kernel's reset() dispatch (outside the timed steps) moves the whole batch's
+    # settle traffic: its per-step value is the median dispatch
+    return {k: (sorted(v.values())[len(v) // 2] if "settle" in k else sum(v.values()) / len(v))
+            for k, v in per.items() if v}
 
 
 def main(out, tag):
@@ -59,10 +63,17 @@ def main(out, tag):
         for r in csv.DictReader(open(stats)):
             k = step_kernel(r["Name"])
             if k:
-                res["kernels"][k] = {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"]),
-                                     "pct": float(r["Percentage"])}
+                calls, tot, mx = int(r["Calls"]), float(r["TotalDurationNs"]), float(r["MaxNs"])
+                avg = tot / calls
+                if "settle" in k and calls > 1:
+                    # the settle kernel's longest call is reset() (every env settled, banks
+                    # prefilled), outside the timed steps; the per-step calls are the fallback
+                    avg = (tot - mx) / (calls - 1)
+                    calls -= 1
+                res["kernels"][k] = {"avg_ms": avg / 1e6, "calls": calls, "pct": float(r["Percentage"])}
         # a kernel may run more than once per step (the staged solver: main launch + global-B
-        # launch); the step count is the fewest calls of any step kernel
+        # launch; the RK4 pipeline: four of each stage kernel); the step count is the fewest calls
+        # of any step kernel
         nstep = min(v["calls"] for v in res["kernels"].values()) if res["kernels"] else 1
         for v in res["kernels"].values():
             v["per_step"] = v["calls"] / nstep
