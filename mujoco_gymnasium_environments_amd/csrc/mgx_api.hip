@@ -226,7 +226,7 @@ namespace {
 
 int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
-Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active, bool staged,
+Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active,
                    bool gB = false) {
   Layout L{};
   int p = 0;
@@ -234,60 +234,52 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   auto take = [&](int n) { int r = p; p = align_up(p + (n > 0 ? n : 1), al); return r; };
   int nb = d->nbody, nv = d->nv, nj = d->njnt, ng = d->ngeom;
   L.max_ncon = max_ncon; L.max_nefc = max_nefc; L.max_active = max_active;
-  L.staged = staged ? 1 : 0;
   // carry: state + frames read by env logic + factors + contacts (the finisher's inputs)
   L.qpos = take(d->nq); L.qvel = take(nv); L.ctrl = take(d->nu); L.xfrc = take(6 * nb);
   L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb);
   L.qLD = take(d->nM); L.qMH = take(d->nM); L.con_dist = take(max_ncon); L.con_mu = take(max_ncon);
   L.carry_reals = p;
+  L.carry_lds = p;
+  L.cfs = 9;
   const int nvw = nv > 64 ? 128 : 64;  // dof-indexed scratch vectors: one or two dofs per lane
   L.vec0 = take(nvw); L.vec1 = take(nvw); L.vec2 = take(nvw); L.vec3 = take(nvw);
   int vec_end = p;
-  L.rk = (!staged && d->integrator == 1) ? take(((d->nq + 3) & ~3) + nvw) : 0;
+  L.rk = d->integrator == 1 ? take(((d->nq + 3) & ~3) + nvw) : 0;
   // persistent for the rest of the forward pass
   // Newton with rows in global scratch (gB): the Hessian / its factor overlay the phase-A union,
   // dead from the row transform on (newton() is its only user; no env logic reads a union array
   // after the solve), and the contact frames sit in the Hessian's tail beyond the phase-A arrays
   // (live from collision to make_constraint only). The PGS block table is not allocated.
   // Assembly (fp64, 384 rows, 96 contacts): 113 -> 80 KiB per env, two envs per CU.
-  const bool hess_union = gB && !staged && d->solver == 2;
+  const bool hess_union = gB && d->solver == 2;
   L.cdof = take(6 * nv);
-  // staged row builder: the contact frames / points and the row constants overlay the union
-  // (below) when they fit there, else they get their own space here
-  const int nb12 = align_up(12 * nb, al), cf9 = align_up(9 * max_ncon, al), cp3 = align_up(3 * max_ncon, al);
+  const int cf9 = align_up(9 * max_ncon, al), cp3 = align_up(3 * max_ncon, al);
   const int union_dead = align_up(9 * nb, al) + align_up(3 * nb, al) + align_up(9 * nb, al) + align_up(10 * nb, al) +
                          align_up(10 * nb, al) + align_up(6 * nb, al) + align_up(6 * nv, al) + 2 * align_up(3 * nj, al);
-  const bool staged_overlay = staged && nb12 + cf9 + cp3 <= union_dead;
   // monolithic PGS models with rows in global scratch: the contact points / frames, the row
   // margins (make_constraint only) and the broadphase survivor list (collision only) overlay
   // xmat .. xanchor of the union, dead once the velocity stage is done (bipedal: 62.4 -> 51.4 KiB,
   // three envs per CU instead of two)
   const int cvel_sz = align_up(6 * nb, al);
   const int act_r = align_up((max_active * 4 + real_bytes - 1) / real_bytes, al);
-  const bool mono_overlay = gB && !staged && !hess_union && !(d->layout_flags & MGX_KEEP_CVEL) &&
+  const bool mono_overlay = gB && !hess_union && !(d->layout_flags & MGX_KEEP_CVEL) &&
                             cp3 + cf9 + align_up(max_nefc, al) + act_r <= union_dead + cvel_sz;
-  if (!hess_union && !staged_overlay && !mono_overlay) { L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon); }
-  L.efc = take(staged ? 1 : 8 * max_nefc); L.efc_margin = take(staged || mono_overlay ? 1 : max_nefc);
-  L.efc_blk = take(staged || hess_union ? 1 : 2 * max_nefc);
-  L.hess = (!staged && d->solver == 2 && !hess_union) ? take(nv * nv) : 0;
+  if (!hess_union && !mono_overlay) { L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon); }
+  L.efc = take(8 * max_nefc); L.efc_margin = take(mono_overlay ? 1 : max_nefc);
+  L.efc_blk = take(hess_union ? 1 : 2 * max_nefc);
+  L.hess = (d->solver == 2 && !hess_union) ? take(nv * nv) : 0;
   // env logic that reads cvel after the step (martial arts, martial_arts_env.py:536-589) keeps
   // it out of the union the constraint rows overwrite
-  const bool keep_cvel = !staged && (d->layout_flags & MGX_KEEP_CVEL);
+  const bool keep_cvel = (d->layout_flags & MGX_KEEP_CVEL) != 0;
   if (keep_cvel) L.cvel = take(6 * nb);
-  // union: phase A (kinematics .. collision) arrays, then B rows on top (all rows for the
-  // monolithic kernel, one chunk of rows for the staged row builder)
+  // union: phase A (kinematics .. collision) arrays, then B rows on top
   int u0 = p;
   L.xmat = take(9 * nb); L.xipos = take(3 * nb); L.ximat = take(9 * nb); L.cinert = take(10 * nb);
   L.crb = take(10 * nb);
-  if (!keep_cvel && !staged_overlay) L.cvel = take(6 * nb);
+  if (!keep_cvel) L.cvel = take(6 * nb);
   L.cfrc = take(6 * nb); L.cdof_dot = take(6 * nv);
   L.xaxis = take(3 * nj); L.xanchor = take(3 * nj); L.geom_xpos = take(3 * ng); L.geom_xmat = take(9 * ng);
   L.act_force = take(d->nu);
-  // staged overlay: cvel (read by the row blocks) after everything the overlay covers
-  if (staged_overlay) L.cvel = take(6 * nb);
-  // staged: per-body sums of cdof * (qacc_smooth | qacc_warmstart), built after the velocity
-  // stage, over xmat .. crb (dead by then; cvel, read with it, lies beyond them)
-  L.cacc = L.xmat;
   int endA = p;
   L.act_union = 0;
   if (mono_overlay) {
@@ -297,20 +289,11 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
     L.efc_margin = o; o += align_up(max_nefc, al);
     L.act_union = o;
   }
-  if (staged_overlay) {
-    // xmat .. xanchor are dead once the velocity stage is done: the contact frames and points
-    // (written by collision, read by the row blocks) follow cacc there (fp64 soccer: 38.6 ->
-    // 32.4 KB per row-builder wave). The per-row impedance constants live in the slot's row-scalar
-    // area of the pipe (rows_impedance), so the full capacity (96 contacts / 384 rows) fits the
-    // same budget: 31.7 / 32.6 KB, five waves per CU either way.
-    L.con_frame = u0 + nb12;
-    L.con_pos = L.con_frame + cf9;
-  }
   L.rowc = 0;
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
   L.Bmat = u0;
-  L.chunk_rows = staged ? 0 : max_nefc;  // the staged row builder keeps rows in registers
-  if (gB && !staged) {  // rows in per-env global scratch
+  L.chunk_rows = max_nefc;
+  if (gB) {  // rows in per-env global scratch
     L.gB = 1;
     L.gB_stride = align_up(max_nefc * L.Bstride, al);
     L.chunk_rows = 0;
@@ -330,17 +313,8 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.con_geom = takei(2 * max_ncon);
   L.carry_ints = q;
   L.con_pair = takei(max_ncon);
-  if (staged) {
-    // the staged row builder lists only the joint-limit rows in efc_id (<= 2 per joint), after
-    // collision: it shares the space of the broadphase survivor list (collision only)
-    const int ecap = std::min(max_nefc, align_up(2 * nj, 4));
-    L.act_list = takei(std::max(max_active, ecap));
-    L.efc_id = L.act_list;
-    L.efc_type = takei(1);
-  } else {
-    L.act_list = takei(max_active);
-    L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
-  }
+  L.act_list = takei(max_active);
+  L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
   L.con_efcadr = takei(1);
   L.ints = q;
   L.bytes = L.reals * real_bytes + L.ints * 4;
@@ -348,10 +322,83 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   return L;
 }
 
-// The finisher binds the staged layout but only owns the carry + scratch vectors.
+// The staged row builder (k_soccer_rows, k_rk_rows, the row stage of the settle kernels): the
+// per-slot working set by liveness, so more row-builder waves share a CU (LDS-bound: 160 KiB / CU).
+//   carry: the finisher's inputs; xfrc_applied and qMH (written once, read by the finisher or
+//          once per step) sit in the slot's pipe carry in global memory, not in LDS (carry_lds);
+//   cvel:  velocity stage -> row blocks;
+//   region R, three lives: phase A (kinematics .. velocity) xipos / cinert / crb live throughout,
+//          xmat / ximat / xaxis / xanchor until com_crb, then cdof_dot / cfrc / act_force and an
+//          LDS copy of xfrc_applied over them; phase C (collision): the geom poses (computed from xquat just before collision,
+//          geom_poses) + contact normals / points + the broadphase list (later efc_id);
+//          phase D (row blocks): cacc over the geom poses.
+// fp64 soccer, default capacity (64 contacts, 192 rows): 31.7 -> 19.7 KB per row-builder wave,
+// eight waves per CU instead of five (the VGPR limit of the row builder is also eight).
+Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active) {
+  Layout L{};
+  int p = 0;
+  const int al = 16 / real_bytes;
+  auto a = [&](int n) { return align_up(n > 0 ? n : 1, al); };
+  auto take = [&](int n) { int r = p; p += a(n); return r; };
+  const int nb = d->nbody, nv = d->nv, nj = d->njnt, ng = d->ngeom;
+  L.max_ncon = max_ncon; L.max_nefc = max_nefc; L.max_active = max_active;
+  L.staged = 1;
+  L.late_geom = 1;
+  L.cfs = 3;
+  L.qpos = take(d->nq); L.qvel = take(nv); L.ctrl = take(d->nu);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb);
+  L.qLD = take(d->nM); L.con_dist = take(max_ncon); L.con_mu = take(max_ncon);
+  L.carry_lds = p;
+  L.xfrc = take(6 * nb); L.qMH = take(d->nM);
+  L.carry_reals = p;
+  p = L.carry_lds;  // the row builder's LDS continues after the LDS part of the carry
+  const int nvw = nv > 64 ? 128 : 64;
+  L.vec0 = take(nvw); L.vec1 = take(nvw); L.vec2 = take(nvw); L.vec3 = take(nvw);
+  L.cdof = take(6 * nv);
+  L.efc = take(1); L.efc_margin = take(1); L.efc_blk = take(1);
+  L.cvel = take(6 * nb);
+  const int R = p;
+  // phase A
+  L.xipos = R; L.cinert = L.xipos + a(3 * nb); L.crb = L.cinert + a(10 * nb);
+  const int dead = L.crb + a(10 * nb);
+  L.xmat = dead; L.ximat = L.xmat + a(9 * nb); L.xaxis = L.ximat + a(9 * nb); L.xanchor = L.xaxis + a(3 * nj);
+  const int endA1 = L.xanchor + a(3 * nj);
+  L.cdof_dot = dead; L.cfrc = L.cdof_dot + a(6 * nv); L.act_force = L.cfrc + a(6 * nb);
+  L.xfrc_lds = L.act_force + a(d->nu);
+  const int endA2 = L.xfrc_lds + a(6 * nb);
+  // phase C
+  const int ecap = std::min(max_nefc, align_up(2 * nj, 4));  // efc_id: the joint-limit rows only
+  const int nlist = std::max(max_active, ecap);
+  L.geom_xpos = R; L.geom_xmat = L.geom_xpos + a(3 * ng);
+  L.con_frame = L.geom_xmat + a(9 * ng); L.con_pos = L.con_frame + a(3 * max_ncon);
+  L.act_union = L.con_pos + a(3 * max_ncon);
+  const int endC = L.act_union + a((nlist * 4 + real_bytes - 1) / real_bytes);
+  // phase D: cacc (12 per body) over the geom poses when they cover it, else after phase C
+  L.cacc = a(12 * nb) <= L.con_frame - R ? R : endC;
+  const int endD = L.cacc + a(12 * nb);
+  L.reals = std::max(std::max(endA1, endA2), std::max(endC, endD));
+  L.rowc = 0; L.rk = 0; L.hess = 0;
+  L.Bstride = nv | 1; L.Bmat = R; L.chunk_rows = 0; L.gB = 0; L.gB_stride = 0; L.tchunk = 0;
+  int q = 0;
+  auto takei = [&](int n) { int r = q; q = align_up(q + (n > 0 ? n : 1), 4); return r; };
+  L.con_geom = takei(2 * max_ncon);
+  L.carry_ints = q;
+  L.con_pair = takei(max_ncon);
+  L.act_list = 0; L.efc_id = 0;  // both at act_union (env_bind)
+  L.efc_type = takei(1);
+  L.con_efcadr = takei(1);
+  L.ints = q;
+  L.bytes = L.reals * real_bytes + L.ints * 4;
+  return L;
+}
+
+// The finisher binds the staged carry (all of it in LDS) and the four scratch vectors after it.
 Layout finisher_layout(const Layout& S, int real_bytes) {
   Layout L = S;
-  L.reals = S.vec3 + 64;
+  const int nvw = S.vec1 - S.vec0;
+  L.vec0 = S.carry_reals; L.vec1 = L.vec0 + nvw; L.vec2 = L.vec1 + nvw; L.vec3 = L.vec2 + nvw;
+  L.carry_lds = S.carry_reals;
+  L.reals = L.vec3 + nvw;
   L.ints = S.carry_ints;
   L.bytes = L.reals * real_bytes + L.ints * 4;
   return L;
@@ -731,16 +778,16 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // staged step itself carries the model's full capacity
   const int mono_nefc = m->staged_ok && max_nefc > 192 ? 192 : max_nefc;
   const int mono_ncon = m->staged_ok && max_ncon > 64 ? 64 : max_ncon;
-  m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, false);
+  m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active);
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024 || (d->layout_flags & MGX_ROWS_IN_SCRATCH))
-    m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, false, true);
+    m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, true);
   // the staged RK4 step (mgx_rk_staged.h, bipedal_rescue): RK4 + PGS, nv 49..64 (four register
   // entries per solver lane, a 16-word block table)
   m->staged_rk_ok = d->integrator == 1 && d->solver == 0 && condim13 && d->nv > 48 && d->nv <= 64 &&
                     max_nefc <= 1024 && max_ncon <= 128;
   const bool any_staged = m->staged_ok || m->staged_rk_ok;
-  m->Ls = make_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active, true);
+  m->Ls = make_staged_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;
   if (precision == MGX_F32) {

@@ -49,8 +49,20 @@ struct Layout {
   // Newton solver (solver == mjSOL_NEWTON, monolithic kernels only): nv x nv Hessian
   int hess;
   // > 0: the broadphase survivor list lives at this real offset (inside the dead phase-A
-  // union) instead of the int region (monolithic rows-in-scratch PGS models)
+  // union) instead of the int region (monolithic rows-in-scratch PGS models; the staged row
+  // builder, where efc_id shares it)
   int act_union;
+  // staged row builder: carry reals [carry_lds, carry_reals) (xfrc_applied, qMH) live in the
+  // slot's pipe carry in global memory instead of LDS (bind_carry_tail); the finisher's layout
+  // holds the whole carry in LDS
+  int carry_lds;
+  // staged row builder: geom poses are computed right before collision (geom_poses), from xquat,
+  // over the phase-A arrays dead by then; contacts keep their normal only (3 reals, stride
+  // cfs = 3; the frame is rebuilt where it is read) instead of the 9-real frame
+  int late_geom, cfs;
+  // staged row builder: LDS copy of xfrc_applied for the velocity stage (its per-dof force sums
+  // read it nbody times per lane), in the phase-A region
+  int xfrc_lds;
 };
 
 // Device-resident model: pointers into one device allocation.

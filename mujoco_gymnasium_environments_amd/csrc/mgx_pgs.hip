@@ -71,6 +71,7 @@ __global__ void __launch_bounds__(64) k_soccer_rows(DevModel<T> m, SoccerIds<T> 
   if (b < n_env) {
     if (mask && !mask[b]) return;
     env_bind(m, e, smem);
+    bind_carry_tail(m, e, P, b);
     load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
                (T*)s.time, b);
     soccer_pre(m, e, ids, action + (size_t)b * m.nu, (T*)ev.prev_ball_pos + 3 * (size_t)b, (T*)ev.wind + 3 * (size_t)b);
@@ -81,6 +82,7 @@ __global__ void __launch_bounds__(64) k_soccer_rows(DevModel<T> m, SoccerIds<T> 
     int k = P.at<int>(P.o_bk)[bi];
     if (k < 0 || k >= 10) return;
     env_bind(m, e, smem);
+    bind_carry_tail(m, e, P, b);
     bank_load_state(m, e, P, bi);
     slot = b;
   }
@@ -173,6 +175,9 @@ template <typename T>
 void launch_soccer_rows(const DevModel<T>& Ms, const SoccerIds<T>& ids, const mgx_state& s, const mgx_soccer_env& ev,
                         const float* action, int n_env, const uint8_t* mask, const Pipe& P, int banks, int slots, int lds,
                         hipStream_t st) {
+  // occupancy probe: MGX_ROWS_LDS pads the row builder's LDS (fewer waves per CU; up to 64 KiB)
+  static const int pad = getenv("MGX_ROWS_LDS") ? atoi(getenv("MGX_ROWS_LDS")) : 0;
+  if (pad > lds && pad <= 64 * 1024) lds = pad;
   hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), lds, st, Ms, ids, s, ev, action, n_env, mask, P, banks);
 }
 template <typename T>
@@ -226,10 +231,10 @@ int staged_kernels_configure(int precision, int ls, int lf, int settle) {
         mgx_set_lds(k_soccer_settle<T, 3, 16>, settle) | mgx_set_lds(k_soccer_settle<T, 4, 16>, settle) | \
         mgx_set_lds(k_soccer_settle<T, 1, 64>, settle);
   if (precision == MGX_F32) {
-    rc |= mgx_set_lds(k_soccer_rows<float>, ls) | mgx_set_lds(k_soccer_finish<float>, lf);
+    rc |= mgx_set_lds(k_soccer_rows<float>, ls > 64 * 1024 ? ls : 64 * 1024) | mgx_set_lds(k_soccer_finish<float>, lf);
     MGX_SETTLE_SET(float)
   } else {
-    rc |= mgx_set_lds(k_soccer_rows<double>, ls) | mgx_set_lds(k_soccer_finish<double>, lf);
+    rc |= mgx_set_lds(k_soccer_rows<double>, ls > 64 * 1024 ? ls : 64 * 1024) | mgx_set_lds(k_soccer_finish<double>, lf);
     MGX_SETTLE_SET(double)
   }
 #undef MGX_SETTLE_SET

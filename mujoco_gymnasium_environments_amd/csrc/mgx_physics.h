@@ -58,7 +58,11 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   int* I = reinterpret_cast<int*>(R + L.reals);
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair;
   e.act_list = L.act_union > 0 ? reinterpret_cast<int*>(R + L.act_union) : I + L.act_list;
-  e.efc_type = I + L.efc_type; e.efc_id = I + L.efc_id; e.con_efcadr = I + L.con_efcadr;
+  e.efc_type = I + L.efc_type; e.con_efcadr = I + L.con_efcadr;
+  // the staged row builder lists only its joint-limit rows, after collision, in the broadphase list
+  e.efc_id = L.staged ? e.act_list : I + L.efc_id;
+  // the staged row builder's carry tail lives in global memory (bind_carry_tail)
+  if (L.carry_lds < L.carry_reals) { e.xfrc = nullptr; e.qMH = nullptr; }
   int l = lane_id();
   e.chainlen = l < m.nv ? m.dof_chainlen[l] : 0;
   e.madr = l < m.nv ? m.dof_Madr[l] : 0;
@@ -161,6 +165,9 @@ __device__ __forceinline__ void body_pose_step(const DevModel<T>& m, Env<T>& e, 
   quat2mat(mat, quat);
 }
 
+template <typename T, bool FROMQ>
+__device__ __forceinline__ void geom_poses(const DevModel<T>& m, Env<T>& e);
+
 template <typename T>
 __device__ __forceinline__ void kinematics(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
@@ -182,10 +189,25 @@ __device__ __forceinline__ void kinematics(const DevModel<T>& m, Env<T>& e) {
     quat2mat(e.ximat + 9 * b, q);
   }
   wsync();
+  if (!m.L.late_geom) geom_poses<T, false>(m, e);
+}
+
+// geom poses (mj_kinematics' geom loop). FROMQ (the staged row builder, Layout.late_geom): the body
+// rotation is rebuilt from xquat — kinematics stores xmat = quat2mat(xquat), so this is the same
+// matrix — and the poses are computed just before collision, over arrays dead by then.
+template <typename T, bool FROMQ>
+__device__ __forceinline__ void geom_poses(const DevModel<T>& m, Env<T>& e) {
+  const int l = lane_id();
   for (int g = l; g < m.ngeom; g += 64) {
     int b = m.geom_bodyid[g];
     T q[4], gp[3];
-    mulmatvec3(gp, e.xmat + 9 * b, m.geom_pos + 3 * g);
+    if constexpr (FROMQ) {
+      T bm[9];
+      quat2mat(bm, e.xquat + 4 * b);
+      mulmatvec3(gp, bm, m.geom_pos + 3 * g);
+    } else {
+      mulmatvec3(gp, e.xmat + 9 * b, m.geom_pos + 3 * g);
+    }
     for (int k = 0; k < 3; k++) e.geom_xpos[3 * g + k] = gp[k] + e.xpos[3 * b + k];
     mulquat(q, e.xquat + 4 * b, m.geom_quat + 4 * g);
     quat2mat(e.geom_xmat + 9 * g, q);
@@ -467,8 +489,8 @@ __device__ __forceinline__ void collision(const DevModel<T>& m, Env<T>& e) {
       int k = ncon + off + c;
       if (k >= L.max_ncon) break;
       e.con_dist[k] = rc[c].dist;
-      for (int q = 0; q < 3; q++) { e.con_pos[3 * k + q] = rc[c].pos[q]; e.con_frame[9 * k + q] = rc[c].n[q]; }
-      make_frame(e.con_frame + 9 * k);
+      for (int q = 0; q < 3; q++) { e.con_pos[3 * k + q] = rc[c].pos[q]; e.con_frame[L.cfs * k + q] = rc[c].n[q]; }
+      if (L.cfs == 9) make_frame(e.con_frame + 9 * k);  // else the normal only (Layout.cfs)
       e.con_pair[k] = p;
       e.con_mu[k] = sqrt(m.pair_friction[5 * p] * m.pair_friction[5 * p] + m.pair_friction[5 * p + 1] * m.pair_friction[5 * p + 1]);
       e.con_geom[2 * k] = m.pair_geom[2 * p];

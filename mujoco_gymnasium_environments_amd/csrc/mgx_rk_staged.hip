@@ -383,6 +383,7 @@ __global__ void __launch_bounds__(64) k_rk_rows(DevModel<T> m, BipedalIds ids, m
   if (stage > 0 && P.at<int>(P.o_rks)[b] != RK_ACTIVE) return;
   Env<T> e;
   env_bind(m, e, smem);
+  bind_carry_tail(m, e, P, b);
   rk_rows_slot(m, e, ids, s, be, action, P, b < n_env ? b : 0, bi, b, stage, true);
 }
 
@@ -431,6 +432,7 @@ __device__ __forceinline__ void rk_settle_step(const DevModel<T>& Ms, const DevM
     {
       Env<T> e;
       env_bind(Ms, e, smem);
+      bind_carry_tail(Ms, e, P, slot);
       rk_rows_slot(Ms, e, ids, s, be, nullptr, P, env, bi, slot, stage, false);
     }
     __threadfence();
@@ -460,6 +462,7 @@ __device__ __forceinline__ void rk_settle_reset(const DevModel<T>& Ms, const Dev
   {
     Env<T> e;
     env_bind(Ms, e, smem);
+    bind_carry_tail(Ms, e, P, env);
     if (draws) {
       if (lane_id() < 12) e.vec3[lane_id()] = draws[lane_id()];
     } else {
@@ -495,6 +498,7 @@ __global__ void __launch_bounds__(64) k_rk_settle(DevModel<T> Ms, DevModel<T> Mf
     if (P.R > 0 && mode == RK_SETTLE_FIXUP) {
       Env<T> e;
       env_bind(Ms, e, smem);
+      bind_carry_tail(Ms, e, P, env);
       rk_bank_init(Ms, e, ids, P, env, bi, E + P.R, seed, env_offset);
     } else if (P.R > 0 && !draws) {
       for (int k = 1; k <= P.R; k++)

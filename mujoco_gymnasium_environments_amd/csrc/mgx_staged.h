@@ -68,6 +68,19 @@ struct Pipe {
   __device__ __forceinline__ int* ctr() const { return at<int>(o_ctr); }
 };
 
+// The row builder's carry tail (Layout.carry_lds): xfrc_applied and qMH of `slot` are read and
+// written in its pipe carry (global memory), where the finisher's load_carry picks them up.
+// Every Env bound with the row-builder layout binds its tail before first use (env_bind leaves
+// the two pointers null).
+template <typename T>
+__device__ __forceinline__ void bind_carry_tail(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot) {
+  if (m.L.carry_lds < m.L.carry_reals) {
+    T* cr = P.at<T>(P.o_carry) + (size_t)slot * P.carry_stride;
+    e.xfrc = cr + (m.L.xfrc - m.L.qpos);
+    e.qMH = cr + (m.L.qMH - m.L.qpos);
+  }
+}
+
 // ------------------------------------------------------------------ S1 helpers
 // Row plan (mj_makeConstraint order [ext]): joint limits (joint order, lower then upper),
 // padded with dummy rows to a multiple of 4, then one 4-row block per contact (the 4 pyramid
@@ -254,7 +267,11 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
     const int rt1 = readlane(cs.rt1, cl), rt2 = readlane(cs.rt2, cl);
     const uint64_t m1 = readlane_u64(cs.m1, cl), m2 = readlane_u64(cs.m2, cl);
     const T mu0 = readlane_t(cs.mu0, cl), mu1 = readlane_t(cs.mu1, cl);
-    const T* fr = e.con_frame + 9 * c;
+    // the contact frame from its normal (make_frame, as collision builds it for the
+    // monolithic layout: the same arithmetic on the same normal)
+    T fr[9];
+    fr[0] = e.con_frame[3 * c]; fr[1] = e.con_frame[3 * c + 1]; fr[2] = e.con_frame[3 * c + 2];
+    make_frame(fr);
     const T* cp = e.con_pos + 3 * c;
     sup = m1 | m2;
     T o1[3] = {cp[0] - e.subtree_com[3 * rt1], cp[1] - e.subtree_com[3 * rt1 + 1], cp[2] - e.subtree_com[3 * rt1 + 2]};
@@ -394,10 +411,20 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   MGX_STAMP(1);
   e.diaginv = factor_ld(m, e, e.qLD);
   MGX_STAMP(2);
-  velocity(m, e);
+  {
+    // the velocity stage reads xfrc_applied from an LDS copy (the carry tail is in global memory)
+    T* const xg = e.xfrc;
+    T* const xl = e.cdof + (m.L.xfrc_lds - m.L.cdof);
+    for (int k = l; k < 6 * m.nbody; k += 64) xl[k] = xg[k];
+    wsync();
+    e.xfrc = xl;
+    velocity(m, e);
+    e.xfrc = xg;
+  }
   MGX_STAMP(3);
   e.qacc_smooth = solve_M(m, e, e.qLD, e.diaginv, e.qfrc_smooth);
   MGX_STAMP(4);
+  if (m.L.late_geom) geom_poses<T, true>(m, e);
   collision(m, e);
   MGX_STAMP(5);
   int nlim, ncf;
@@ -444,7 +471,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   MGX_STAMP(7);
   // carry + registers + ints
   T* cr = P.at<T>(P.o_carry) + (size_t)slot * P.carry_stride;
-  for (int k = l; k < m.L.carry_reals; k += 64) cr[k] = reinterpret_cast<T*>(e.qpos)[k - m.L.qpos];
+  for (int k = l; k < m.L.carry_lds; k += 64) cr[k] = reinterpret_cast<T*>(e.qpos)[k - m.L.qpos];
   T* rg = cr + ((m.L.carry_reals + 63) & ~63);
   rg[l] = e.qacc_ws; rg[64 + l] = e.qfrc_applied; rg[128 + l] = e.qfrc_smooth; rg[192 + l] = e.qacc_smooth;
   if (l == 0) rg[256] = e.time;
@@ -1049,6 +1076,7 @@ __device__ __forceinline__ void settle_step(const DevModel<T>& Ms, const DevMode
   {
     Env<T> e;
     env_bind(Ms, e, smem);
+    bind_carry_tail(Ms, e, P, slot);
     bank_load_state(Ms, e, P, bi);
     int warn = 0;  // mj_checkPos / mj_checkVel
     if (any_bad(e.qpos, Ms.nq)) { reset_env(Ms, e); warn++; }
@@ -1083,6 +1111,7 @@ __device__ __forceinline__ void settle_reset(const DevModel<T>& Ms, const DevMod
   {
     Env<T> e;
     env_bind(Ms, e, smem);
+    bind_carry_tail(Ms, e, P, env);
     if (draws) {
       if (lane_id() < 36) e.vec1[lane_id()] = draws[lane_id()];
     } else {
@@ -1125,6 +1154,7 @@ __global__ void __launch_bounds__(64) k_soccer_settle(DevModel<T> Ms, DevModel<T
       // as bank_install: the consumed bank restarts for episode E + R (the pipeline settles it)
       Env<T> e;
       env_bind(Ms, e, smem);
+      bind_carry_tail(Ms, e, P, env);
       bank_init(Ms, e, ids, P, env, E % P.R, E + P.R, seed, env_offset);
     } else if (P.R > 0 && !draws) {
       // reset(): prefill the banks of episodes E + 1 .. E + R, so the first R terminations never wait

@@ -45,6 +45,7 @@ def build():
 
 
 TASK_TU = {"assembly": "mgx_prof_set_buffer_assembly", "bipedal": "mgx_prof_set_buffer_bipedal",
+           "bipedal_staged": "mgx_prof_set_buffer_rk_staged",
            "martial": "mgx_prof_set_buffer_martial", "construction": "mgx_prof_set_buffer_construction"}
 
 
@@ -62,9 +63,9 @@ def make_task(task, n):
         from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
         env = ConstructionVectorEnv(n, seed=3, precision=os.environ.get("PREC", "f64"))
         acts = [(torch.rand(n, 33, device="cuda:0", generator=g) * 2 - 1) * 200 for _ in range(4)]
-    elif task == "bipedal":
+    elif task.startswith("bipedal"):
         from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
-        env = BipedalVectorEnv(n, seed=3)
+        env = BipedalVectorEnv(n, seed=3, staged=task == "bipedal_staged")
         acts = [(torch.rand(n, 26, device="cuda:0", generator=g) * 2 - 1) * 100 for _ in range(4)]
     else:
         from mujoco_gymnasium_environments_amd.envs.martial import MartialArtsVectorEnv
@@ -137,6 +138,9 @@ def main():
         env.step(acts[k % 4])
     torch.cuda.synchronize()
     assert L.mgx_prof_set_buffer(C.c_void_p(buf.data_ptr())) == 0
+    if staged:  # the staged kernels live in their own translation unit (mgx_pgs.hip)
+        L.mgx_prof_set_buffer_pgs.argtypes = [C.c_void_p]
+        assert L.mgx_prof_set_buffer_pgs(C.c_void_p(buf.data_ptr())) == 0
     for k in range(steps):
         env.step(acts[k % 4])
     torch.cuda.synchronize()
