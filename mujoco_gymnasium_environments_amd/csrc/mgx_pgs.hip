@@ -108,6 +108,8 @@ __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T
     P.ctr()[1] = 0;
     P.ctr()[2] = 0;
   }
+  if (env == 0)
+    for (int b = lane_id(); b < P.nbk; b += 64) P.at<int>(P.o_hist)[b] = 0;
   Env<T> e;
   env_bind(m, e, smem);
   if (banks) {

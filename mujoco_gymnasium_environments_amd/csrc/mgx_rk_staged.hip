@@ -402,6 +402,8 @@ __global__ void __launch_bounds__(64) k_rk_finish(DevModel<T> m, BipedalIds ids,
     P.ctr()[1] = 0;
     P.ctr()[2] = 0;
   }
+  if (env == 0)
+    for (int b = lane_id(); b < P.nbk; b += 64) P.at<int>(P.o_hist)[b] = 0;
   Env<T> f;
   env_bind(m, f, smem);
   const int* rks = P.at<int>(P.o_rks);
@@ -439,7 +441,8 @@ __device__ __forceinline__ void rk_settle_step(const DevModel<T>& Ms, const DevM
     __syncthreads();
     if (threadIdx.x == 0) lst[0] = slot;
     __syncthreads();
-    pgs_group<T, RK_EPL, RK_LPS, false, RK_TW>(P, smem, lst, 1, 0, P.maxE, maxit, tol, scale, 64 / RK_LPS);
+    pgs_group<T, RK_EPL, RK_LPS, false, RK_TW>(P, smem, threadIdx.x < RK_LPS ? slot : -1, P.maxE, maxit, tol, scale,
+                                               64 / RK_LPS);
     __threadfence();
     __syncthreads();
     Env<T> f;

@@ -50,6 +50,12 @@ struct Pipe {
                        // to maxE) go to the second, wide-LDS launch (o_k2big)
   int arena;           // LDS bytes of one main-launch solver wave (scalars + block table + B of its slots)
   size_t o_carry, o_carryi, o_ne, o_blen, o_niter, o_k2list, o_k2big, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
+  // the main solver launch's slots by block count: o_hist[b] slots with b blocks (b = 1 .. nbk - 1),
+  // listed in o_blist[b * S ..]; the launch takes them heaviest first (sorted_slot), so a wave's
+  // four slots have (nearly) equal sweeps and the longest chains start first. The finisher
+  // clears the histogram.
+  int nbk;
+  size_t o_hist, o_blist;
   size_t o_bq, o_bv, o_ba, o_btime, o_bobs, o_bprev, o_bwind, o_bk, o_bep, o_bwarn, o_bseed;
   // the checkAcc template: mj_step's outcome after mj_resetData (state + forward frames)
   size_t o_tq, o_tv, o_ta, o_tt, o_tx, o_txq, o_tsc, o_tn, o_tcg, o_tcd, o_tcm;
@@ -497,7 +503,10 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
       P.at<int>(P.o_k2big)[idx] = slot;
     } else if (ne > 0) {
       int idx = atomicAdd(P.ctr() + 1, 1);
-      P.at<int>(P.o_k2list)[idx] = slot;
+      P.at<int>(P.o_k2list)[idx] = slot;  // arrival order (diagnostics: tools/pgs_census.py)
+      const int nb = ne >> 2;
+      const int r = atomicAdd(P.at<int>(P.o_hist) + nb, 1);
+      P.at<int>(P.o_blist)[(size_t)nb * P.S + r] = slot;
     }
   }
 }
@@ -693,15 +702,13 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
 // read from global memory (L2 / MALL) with a register ring RING - 1 blocks ahead.
 // Both run the identical arithmetic on every slot, so which launch solves a slot is invisible.
 template <typename T, int EPL, int LPS, bool BLDS, int TW = 8>
-__device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* list, int cnt, int base, int capE, int maxit,
-                                          T tol, T scale, int spw) {
+__device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, int capE, int maxit, T tol, T scale,
+                                          int spw) {
   constexpr int RING = BLDS ? MGX_PGS_RING_LDS : MGX_PGS_RING;
   typedef typename Vec4T<T>::type V4;
   constexpr int SPW = 64 / LPS;
   const int l = threadIdx.x, s = l / LPS, j = l % LPS;
-  const int spn = spw < 0 ? -spw : spw;
-  const int idx = base + s;
-  const int slot = (s < spn && idx < cnt) ? list[idx] : -1;
+  (void)spw;
   const int ne = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;  // a multiple of 4
   const int nblk = ne >> 2;
   int nm = nblk;
@@ -856,15 +863,51 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, const int* 
 // the slots with capE < nefc <= maxE and those of LDS-arena waves that did not fit, grid-stride
 // over a small grid with maxE rows of scalars per slot in LDS. BLDS (main launch only): B in
 // the wave's LDS arena; otherwise B is read from global memory (L2 / MALL).
+// The slot at position idx (< 0: none) of the main solver list in heaviest-first order: the
+// block-count buckets from the top down (o_hist / o_blist). Lanes of one slot pass the same idx;
+// the wave's (up to four) positions are resolved together: lane k scans bucket top - k.
+__device__ __forceinline__ int sorted_slot(const Pipe& P, int idx, int LPS) {
+  const int* hist = P.at<int>(P.o_hist);
+  const int* bl = P.at<int>(P.o_blist);
+  const int l = lane_id();
+  int slot = -1, acc = 0;
+  for (int top = P.nbk - 1; top >= 1; top -= 64) {
+    const int b = top - l;
+    const int h = b >= 1 ? hist[b] : 0;
+    int x = h;  // inclusive prefix over the lanes (descending buckets)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (l >= o) x += y;
+    }
+    for (int q = 0; q < 64; q += LPS) {
+      const int iq = __shfl(idx, q);
+      const unsigned long long m = __ballot(iq >= 0 && acc + x > iq);
+      if (m) {
+        const int f = __ffsll((long long)m) - 1;
+        const int xf = __shfl(x, f), hf = __shfl(h, f);
+        const int rank = iq - (acc + xf - hf);
+        const int sq = bl[(size_t)(top - f) * P.S + rank];
+        if (l >= q && l < q + LPS && slot < 0) slot = sq;
+      }
+    }
+    acc += __shfl(x, 63);
+  }
+  return slot;
+}
+
 template <typename T, int EPL, int LPS, bool BLDS, int TW = 8>
 __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw, int big) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (!big && blockIdx.x == 0 && threadIdx.x == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
   const int cnt = P.ctr()[big ? 2 : 1];
-  const int* list = P.at<int>(big ? P.o_k2big : P.o_k2list);
+  const int* list = P.at<int>(P.o_k2big);
   const int spn = spw < 0 ? -spw : spw;
+  const int s = threadIdx.x / LPS;
   for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
-    pgs_group<T, EPL, LPS, BLDS && true, TW>(P, smem, list, cnt, base, big ? P.maxE : P.capE, maxit, tol, scale, spw);
+    const int idx = (s < spn && base + s < cnt) ? base + s : -1;
+    const int slot = big ? (idx >= 0 ? list[idx] : -1) : sorted_slot(P, idx, LPS);
+    pgs_group<T, EPL, LPS, BLDS && true, TW>(P, smem, slot, big ? P.maxE : P.capE, maxit, tol, scale, spw);
     __syncthreads();  // the next group reuses the LDS
   }
 }
@@ -1087,7 +1130,7 @@ __device__ __forceinline__ void settle_step(const DevModel<T>& Ms, const DevMode
   __syncthreads();
   if (threadIdx.x == 0) lst[0] = slot;
   __syncthreads();
-  pgs_group<T, EPL, LPS, false>(P, smem, lst, 1, 0, P.maxE, maxit, tol, scale, 64 / LPS);
+  pgs_group<T, EPL, LPS, false>(P, smem, threadIdx.x < LPS ? slot : -1, P.maxE, maxit, tol, scale, 64 / LPS);
   __threadfence();
   __syncthreads();
   env_bind(Mf, f, smem);
