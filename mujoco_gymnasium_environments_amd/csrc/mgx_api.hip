@@ -607,7 +607,9 @@ int mgx::staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int tw) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nb3 = (rows / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
   const int spw = 64 / lps;
-  return spw * (MGX_SCAL * 4 * nb3 + 4) * rb + spw * nb3 * 4 * tw + 64;
+  // the row scalars (or, SQG: the forces only; pgs_group) + the block table
+  const int sq = tw > 8 ? 4 : 4 * MGX_SCAL;
+  return spw * (sq * nb3 + 4) * rb + spw * nb3 * 4 * tw + 64;
 }
 static int pgs_lds_bytes(const mgx_model* m, int rows) {
   return staged_pgs_lds_bytes(m, rows, pgs_lanes(), 8);
@@ -676,7 +678,10 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   // main launch (MGX_PGS_LDS_B) it also takes the waves that did not fit their arena, so it
   // follows the main launch there.
   const int wgrid = 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, wlds = pgs_lds_bytes(m, P.maxE);
-  const int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE);
+  int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE);
+  // occupancy probe: MGX_PGS_LDS_PAD pads the main solver launch's LDS (fewer waves per CU)
+  if (const char* pad = getenv("MGX_PGS_LDS_PAD"))
+    if (atoi(pad) > mlds && atoi(pad) <= 96 * 1024) mlds = atoi(pad);
   if (!pgs_lds_b() && P.maxE <= P.capE) {
     // every slot fits the main launch (the default capacity): no wide launch at all
     launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);

@@ -596,9 +596,11 @@ typedef float mgx_f2 __attribute__((ext_vector_type(2)));
 // The forces travel with the prefetch: a block's f changes only when the block itself is solved,
 // and the look-ahead never crosses a sweep boundary (each sweep restarts the ring), so the value
 // loaded here is the latest one.
-template <typename T, int EPL, int LPS>
-__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const PgsTab<EPL>& t,
-                                               int blk, int j) {
+// sq: the row scalars ([b][f][R][1/AR][AR/2] x 4 per block; LDS arena or the pipe in global
+// memory), fb: the forces, FS reals per block (the LDS copy the sweeps update)
+template <typename T, int EPL, int LPS, int FS>
+__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sq, const T* fb,
+                                               const PgsTab<EPL>& t, int blk, int sblk, int j) {
   // the table entry of a block past the slot's end points at the zero group (A included);
   // every load is one 16-byte vector load at a table offset (Bsl: the slot's B in the LDS
   // arena, or in global memory for the global-B launch)
@@ -608,20 +610,20 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.a1 = pa[1];
 #pragma unroll
   for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t.g[d] + 4 * (j & 7));
-  const V4* q = reinterpret_cast<const V4*>(sc + 4 * MGX_SCAL * blk);
+  const V4* q = reinterpret_cast<const V4*>(sq + 4 * MGX_SCAL * sblk);
   k.qb = q[0];
-  k.qf = q[1];
+  k.qf = *reinterpret_cast<const V4*>(fb + FS * blk);
   k.qR = q[2];
   k.qi = q[3];
   k.qh = q[4];
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
 }
-template <typename T, int EPL, int LPS, int TW = 8>
-__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sc, const uint32_t* bt,
-                                               int blk, int j) {
+template <typename T, int EPL, int LPS, int FS, int TW = 8>
+__device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sq, const T* fb,
+                                               const uint32_t* bt, int blk, int sblk, int j) {
   PgsTab<EPL> t;
   pgs_load_tab<EPL, LPS, TW>(t, bt, blk, j);
-  pgs_load_block<T, EPL, LPS>(k, Bsl, sc, t, blk, j);
+  pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, t, blk, sblk, j);
 }
 
 template <typename T, int EPL>
@@ -658,9 +660,9 @@ __device__ __forceinline__ void pgs_update(const PgsBlk<T, EPL>& k, T (&v)[EPL],
 }
 
 template <typename T, int EPL, int LPS>
-__device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], T* sc, int r0, bool ok0, T& impr) {
+__device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], T* fblk, bool ok0, T& impr) {
   typedef typename Vec4T<T>::type V4;
-  V4* qf = reinterpret_cast<V4*>(sc + r0 * MGX_SCAL + MGX_SQ(1, 0));
+  V4* qf = reinterpret_cast<V4*>(fblk);
   const V4 qb = k.qb, f = k.qf, qR = k.qR, qi = k.qi, qh = k.qh;
   T d0, d1, d2, d3;
   pgs_dots(k, v, d0, d1, d2, d3);
@@ -701,7 +703,12 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
 // !BLDS (global-B launch): fixed per-slot capacity of capE rows of scalars and table in LDS, B
 // read from global memory (L2 / MALL) with a register ring RING - 1 blocks ahead.
 // Both run the identical arithmetic on every slot, so which launch solves a slot is invisible.
-template <typename T, int EPL, int LPS, bool BLDS, int TW = 8>
+// SQG (global-B only): the row scalars b / R / 1/AR / AR/2 are read from the pipe with the B
+// prefetch and only the forces live in LDS. The RK4 pipeline uses it (its 256-row slots would
+// otherwise hold the launch to two waves per CU; bipedal 175.0k -> 186.6k env-steps/s); the
+// soccer launch keeps all scalars in LDS at four waves per CU, which measured faster than the
+// global scalars at any occupancy (MGX_PGS_LDS_PAD sweep).
+template <typename T, int EPL, int LPS, bool BLDS, int TW = 8, bool SQG = (TW > 8)>
 __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, int capE, int maxit, T tol, T scale,
                                           int spw) {
   constexpr int RING = BLDS ? MGX_PGS_RING_LDS : MGX_PGS_RING;
@@ -728,6 +735,12 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   T* sc;
   uint32_t* bt;
   const T* Bsl;
+  // all row scalars in LDS with the forces in place (FS = 20 reals per block), or (SQG) only the
+  // forces in LDS (FS = 4)
+  constexpr bool SG = SQG && !BLDS;
+  constexpr int FS = SG ? 4 : 4 * MGX_SCAL;
+  const T* sq;
+  T* fb;
   if constexpr (BLDS) {
     nbA = nbRun + RING - 1;
     const int blen = slot >= 0 ? (P.at<int>(P.o_blen)[slot] + 3) & ~3 : 0;
@@ -749,16 +762,29 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     for (int q = 4 * j; q < blen; q += 4 * LPS)
       *reinterpret_cast<V4*>(Bs + q) = *reinterpret_cast<const V4*>(gB + q);
     Bsl = Bs;
+    sq = sc;
+    fb = sc + MGX_SQ(1, 0);
+    for (int q = j; q < MGX_SCAL * 4 * nbA; q += LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
   } else {
     // LDS capacity in whole ring turns: nbA = capE / 4 rounded up to a multiple of the ring
     const int nbcap = capE / 4;
     nbA = (nbcap + RING - 1) / RING * RING;
-    const int sstride = MGX_SCAL * 4 * nbA + 4;  // 16-byte aligned per slot
+    const int sstride = (SG ? 4 : 4 * MGX_SCAL) * nbA + 4;  // 16-byte aligned per slot
     sc = reinterpret_cast<T*>(smem) + s * sstride;
     bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * TW * nbA;
     Bsl = gB;
+    if constexpr (SG) {
+      sq = gsc;
+      fb = sc;
+      for (int q = j; q < 4 * nbA; q += LPS) sc[q] = q < ne ? gsc[(q >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, q & 3)] : (T)0;
+    } else {
+      sq = sc;
+      fb = sc + MGX_SQ(1, 0);
+      for (int q = j; q < MGX_SCAL * 4 * nbA; q += LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
+    }
   }
-  for (int q = j; q < MGX_SCAL * 4 * nbA; q += LPS) sc[q] = q < ne * MGX_SCAL ? gsc[q] : (T)0;
+  // scalar blocks past the slot's capacity are never real (masked); their loads stay inside it
+  const int sbmax = P.maxE / 4 - 1;
   // block table: the slot's blocks, then zero-group entries up to the capacity
   for (int q = j; q < TW * nbA; q += LPS) bt[q] = q < TW * nblk ? (uint32_t)gbt[q] : 0u;
   __syncthreads();
@@ -768,8 +794,8 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   for (int d = 0; d < EPL; d++) v[d] = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS, TW>(k, Bsl, sc, bt, b, j);
-    const T* qf = sc + 4 * b * MGX_SCAL + MGX_SQ(1, 0);
+    pgs_load_block<T, EPL, LPS, FS, TW>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
+    const T* qf = fb + FS * b;
     bool ok = b < nblk;
     T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[1] : (T)0, f2 = ok ? qf[2] : (T)0, f3 = ok ? qf[3] : (T)0;
     pgs_update(k, v, f0, f1, f2, f3);
@@ -777,22 +803,23 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   T cpart = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS, TW>(k, Bsl, sc, bt, b, j);
+    pgs_load_block<T, EPL, LPS, FS, TW>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
     T d0, d1, d2, d3;
     pgs_dots(k, v, d0, d1, d2, d3);
     slot_sum4<LPS>(d0, d1, d2, d3);
     if (b < nblk) {
       T dd[4] = {d0, d1, d2, d3};
-      const T* qq = sc + 4 * b * MGX_SCAL;
+      const T* qq = sq + 4 * b * MGX_SCAL;
+      const T* qf = fb + FS * b;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const T fi = qq[MGX_SQ(1, i)];
+        const T fi = qf[i];
         cpart += fi * (qq[MGX_SQ(0, i)] + (T)0.5 * (dd[i] + qq[MGX_SQ(2, i)] * fi));
       }
     }
   }
   if (cpart > 0) {
-    for (int r = j; r < ne; r += LPS) sc[(r >> 2) * (4 * MGX_SCAL) + MGX_SQ(1, r & 3)] = 0;
+    for (int r = j; r < ne; r += LPS) fb[(r >> 2) * FS + (r & 3)] = 0;
 #pragma unroll
     for (int d = 0; d < EPL; d++) v[d] = 0;
   }
@@ -815,7 +842,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     pgs_load_tab<EPL, LPS, TW>(tn, bt, 0, j);
 #pragma unroll
     for (int k = 0; k < RING - 1; k++) {
-      pgs_load_block<T, EPL, LPS>(R[k], Bsl, sc, tn, k, j);
+      pgs_load_block<T, EPL, LPS, FS>(R[k], Bsl, sq, fb, tn, k, min(k, sbmax), j);
       pgs_load_tab<EPL, LPS, TW>(tn, bt, k + 1, j);
     }
     // full ring turns, no early exit inside, so every prefetch is consumed on every path and
@@ -826,9 +853,9 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
       for (int k = 0; k < RING; k++) {
         // the slot consumed last lands the block RING - 1 ahead, then block b0 + k is solved
         const int bn = min(b0 + k + RING - 1, nbA - 1);
-        pgs_load_block<T, EPL, LPS>(R[(k + RING - 1) % RING], Bsl, sc, tn, bn, j);
+        pgs_load_block<T, EPL, LPS, FS>(R[(k + RING - 1) % RING], Bsl, sq, fb, tn, bn, min(bn, sbmax), j);
         pgs_load_tab<EPL, LPS, TW>(tn, bt, min(bn + 1, nbA - 1), j);
-        pgs_block<T, EPL, LPS>(R[k], v, sc, 4 * (b0 + k), act && b0 + k < nblk, impr);
+        pgs_block<T, EPL, LPS>(R[k], v, fb + FS * (b0 + k), act && b0 + k < nblk, impr);
       }
     }
     if (act) {
