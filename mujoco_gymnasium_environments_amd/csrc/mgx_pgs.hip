@@ -92,6 +92,30 @@ __global__ void __launch_bounds__(64) k_soccer_rows(DevModel<T> m, SoccerIds<T> 
   stage_rows(m, e, P, slot, warn);
 }
 
+// The bank slots' settle steps (S3 of the extra slots), one wave per bank record, launched before
+// the live finisher: a bank that completes its tenth step here is ready for a reset in this
+// step's live finisher, as when one wave finished an env's banks and then the env.
+template <typename T>
+__global__ void __launch_bounds__(64) k_soccer_bank_finish(DevModel<T> m, SoccerIds<T> ids, int n_env, Pipe P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bi = blockIdx.x;
+  if (bi >= n_env * P.R) return;
+  int k = P.at<int>(P.o_bk)[bi];
+  if (k < 0 || k >= 10) return;
+  Env<T> e;
+  env_bind(m, e, smem);
+  const int slot = n_env + bi;
+  int warn = load_carry(m, e, P, slot);
+  if (!finish_physics(m, e, P, slot)) {
+    load_template(m, e, P);
+    warn++;
+  }
+  bank_store_state(m, e, P, bi, warn);
+  k++;
+  if (k == 10) bank_finalize(m, e, ids, P, bi);
+  if (lane_id() == 0) P.at<int>(P.o_bk)[bi] = k;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T> ids, mgx_state s, mgx_soccer_env ev,
                                                       const float* action, float* obs, double* reward,
@@ -112,26 +136,6 @@ __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T
     for (int b = lane_id(); b < P.nbk; b += 64) P.at<int>(P.o_hist)[b] = 0;
   Env<T> e;
   env_bind(m, e, smem);
-  if (banks) {
-    for (int b = 0; b < P.R; b++) {
-      int bi = env * P.R + b;
-      int k = P.at<int>(P.o_bk)[bi];
-      if (k < 0 || k >= 10) continue;
-      int slot = n_env + bi;
-      int warn = load_carry(m, e, P, slot);
-      if (!finish_physics(m, e, P, slot)) {
-        load_template(m, e, P);
-        warn++;
-      }
-      bank_store_state(m, e, P, bi, warn);
-      k++;
-      if (k == 10) bank_finalize(m, e, ids, P, bi);
-      if (l == 0) P.at<int>(P.o_bk)[bi] = k;
-      wsync();
-    }
-    __threadfence();
-    wsync();
-  }
   if (mask && !mask[env]) return;
   int warn = load_carry(m, e, P, env);
   if (!finish_physics(m, e, P, env)) {
@@ -187,6 +191,8 @@ void launch_soccer_finish(const DevModel<T>& Mf, const SoccerIds<T>& ids, const 
                           const float* action, float* obs, double* reward, uint8_t* terminated, uint8_t* truncated,
                           float* final_obs, int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t* mask,
                           const Pipe& P, int banks, int lds, hipStream_t st) {
+  if (banks && P.R > 0)
+    hipLaunchKernelGGL(k_soccer_bank_finish<T>, dim3(n_env * P.R), dim3(64), lds, st, Mf, ids, n_env, P);
   hipLaunchKernelGGL(k_soccer_finish<T>, dim3(n_env), dim3(64), lds, st, Mf, ids, s, ev, action, obs, reward, terminated,
                      truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks);
 }
@@ -233,10 +239,12 @@ int staged_kernels_configure(int precision, int ls, int lf, int settle) {
         mgx_set_lds(k_soccer_settle<T, 3, 16>, settle) | mgx_set_lds(k_soccer_settle<T, 4, 16>, settle) | \
         mgx_set_lds(k_soccer_settle<T, 1, 64>, settle);
   if (precision == MGX_F32) {
-    rc |= mgx_set_lds(k_soccer_rows<float>, ls > 64 * 1024 ? ls : 64 * 1024) | mgx_set_lds(k_soccer_finish<float>, lf);
+    rc |= mgx_set_lds(k_soccer_rows<float>, ls > 64 * 1024 ? ls : 64 * 1024) | mgx_set_lds(k_soccer_finish<float>, lf) |
+          mgx_set_lds(k_soccer_bank_finish<float>, lf);
     MGX_SETTLE_SET(float)
   } else {
-    rc |= mgx_set_lds(k_soccer_rows<double>, ls > 64 * 1024 ? ls : 64 * 1024) | mgx_set_lds(k_soccer_finish<double>, lf);
+    rc |= mgx_set_lds(k_soccer_rows<double>, ls > 64 * 1024 ? ls : 64 * 1024) | mgx_set_lds(k_soccer_finish<double>, lf) |
+          mgx_set_lds(k_soccer_bank_finish<double>, lf);
     MGX_SETTLE_SET(double)
   }
 #undef MGX_SETTLE_SET
