@@ -392,8 +392,22 @@ __global__ void __launch_bounds__(64) k_rk_finish(DevModel<T> m, BipedalIds ids,
                                                   const float* action, float* obs, double* reward, uint8_t* terminated,
                                                   uint8_t* truncated, float* final_obs, int autoreset, uint64_t seed,
                                                   int env_offset, int n_env, const uint8_t* mask, Pipe P, int banks,
-                                                  int stage) {
+                                                  int stage, int bank_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int* rks = P.at<int>(P.o_rks);
+  if (bank_part) {
+    // the bank records' stage (one wave per record), launched before the live part: a record
+    // finishing its tenth settle step here is ready for this step's resets
+    const int bi = blockIdx.x;
+    if (bi >= n_env * P.R) return;
+    const int slot = n_env + bi;
+    if (rks[slot] != RK_ACTIVE) return;
+    Env<T> f;
+    env_bind(m, f, smem);
+    rk_finish_slot(m, f, ids, s, be, action, obs, reward, terminated, truncated, final_obs, autoreset, seed, env_offset,
+                   P, bi / P.R, bi, slot, stage);
+    return;
+  }
   const int env = blockIdx.x;
   if (env >= n_env) return;
   if (env == 0 && lane_id() == 0) {  // this stage's solver lists are consumed
@@ -406,18 +420,6 @@ __global__ void __launch_bounds__(64) k_rk_finish(DevModel<T> m, BipedalIds ids,
     for (int b = lane_id(); b < P.nbk; b += 64) P.at<int>(P.o_hist)[b] = 0;
   Env<T> f;
   env_bind(m, f, smem);
-  const int* rks = P.at<int>(P.o_rks);
-  if (banks) {
-    for (int b = 0; b < P.R; b++) {
-      const int bi = env * P.R + b, slot = n_env + bi;
-      if (rks[slot] != RK_ACTIVE) continue;
-      rk_finish_slot(m, f, ids, s, be, action, obs, reward, terminated, truncated, final_obs, autoreset, seed, env_offset,
-                     P, env, bi, slot, stage);
-      wsync();
-    }
-    __threadfence();
-    wsync();
-  }
   if (mask && !mask[env]) return;
   if (rks[env] != RK_ACTIVE) return;
   rk_finish_slot(m, f, ids, s, be, action, obs, reward, terminated, truncated, final_obs, autoreset, seed, env_offset, P,
@@ -615,8 +617,11 @@ int step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms,
       launch_rk_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
       launch_rk_pgs<T>(P, wgrid, wlds, st, M.iterations, M.tolerance, scale, 1);
     }
+    if (banks && P.R > 0)
+      hipLaunchKernelGGL(k_rk_finish<T>, dim3(n_env * P.R), dim3(64), m->Lf.bytes, st, Mf, m->bp, *s, *e, action, obs,
+                         reward, terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks, k, 1);
     hipLaunchKernelGGL(k_rk_finish<T>, dim3(n_env), dim3(64), m->Lf.bytes, st, Mf, m->bp, *s, *e, action, obs, reward,
-                       terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks, k);
+                       terminated, truncated, final_obs, autoreset, seed, env_offset, n_env, mask, P, banks, k, 0);
   }
   const int fgrid = n_env < 256 ? n_env : 256;
   hipLaunchKernelGGL(k_rk_settle<T>, dim3(fgrid), dim3(64), settle_lds(m, P), st, Ms, Mf, m->bp, *s, *e,
