@@ -571,9 +571,11 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.o_carry = take(S * p.carry_stride * rb);
   p.o_carryi = take(S * p.carryi_stride * 4);
   p.o_ne = take(S * 4); p.o_blen = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_k2big = take(S * 4); p.o_fix = take((size_t)n_env * 4);
+  // the solver-list buckets are sized for the model's capacity, not the main launch's rows (a
+  // per-call hook changes those), so the workspace layout never depends on MGX_PGS_LDS_ROWS
   p.nbk = p.capE / 4 + 1;
-  p.o_hist = take((size_t)p.nbk * 4);
-  p.o_blist = take((size_t)p.nbk * S * 4);
+  p.o_hist = take((size_t)(p.maxE / 4 + 1) * 4);
+  p.o_blist = take((size_t)(p.maxE / 4 + 1) * S * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
   p.o_blk = take(S * p.maxE * p.tw / 2);  // tw uint16 per 4-row block
   p.o_B = take(S * (size_t)p.bcap * rb);
