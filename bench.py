@@ -391,7 +391,20 @@ def bench_mixed(args, dev, world, rank, dist):
                                   lambda: (torch.rand(N, 33, device=dev, generator=g) * 2 - 1) * 200.0,
                                   CONSTRUCTION_ALG_BYTES),
     }
-    streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
+    # HIP streams map onto GPU_MAX_HW_QUEUES hardware queues (4 on the box): with a stream per
+    # task (7, plus the staged tasks' side streams) unrelated tasks share queues and wait on each
+    # other's kernels. Four streams instead: construction and assembly (the long Newton steps)
+    # each on its own, the five PGS tasks split over two; no side streams (MGX_SIDE_STREAM=0).
+    # Construction's stream (the longest) runs at high priority (--mix-priority 1, measured 73.2k ->
+    # 75.5k env-steps/s). --mix-streams 7: the old one-stream-per-task layout (67.3k).
+    if args.mix_streams >= len(tasks):
+        streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
+    else:
+        os.environ["MGX_SIDE_STREAM"] = "0"
+        groups = [["humanoid_construction"], ["robotic_arm_assembly"],
+                  ["bipedal_rescue", "humanoid_soccer", "humanoid_dancing"], ["quadruped_parkour", "humanoid_martial_arts"]]
+        gs = [torch.cuda.Stream(device=dev, priority=-1 if i == 0 and args.mix_priority else 0) for i in range(len(groups))]
+        streams = {k: gs[i] for i, grp in enumerate(groups) for k in grp}
     pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
     for k, (env, _, _) in tasks.items():
         env.reset()
@@ -436,7 +449,7 @@ def bench_mixed(args, dev, world, rank, dist):
             "config": {"workload": "all tasks mixed, 1024 envs each on 1 GPU (BASELINE configs[4])",
                        "tasks": list(tasks), "tasks_missing": [],
                        "envs_per_task": N, "global_batch": N * len(tasks) * world,
-                       "parallelism": f"dp{world} (env shards), one HIP stream per task",
+                       "parallelism": f"dp{world} (env shards), {len(set(map(id, streams.values())))} HIP streams",
                        "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},
                        "task_dtype": {k: ("f64" if k in ("robotic_arm_assembly", "humanoid_construction")
                                           else args.precision) for k in tasks},
@@ -537,6 +550,8 @@ def main():
                     help="soccer: split the rank's envs into this many stream shards (overlapping pipelines)")
     ap.add_argument("--no-f64-line", "--no-other-line", dest="no_f64_line", action="store_true",
                     help="skip the other-precision soccer line (fp32 when the headline is fp64)")
+    ap.add_argument("--mix-streams", type=int, default=4, help="mixed: 4 grouped streams (default) or 7 (one per task)")
+    ap.add_argument("--mix-priority", type=int, default=1, help="mixed: construction's stream at high priority (1)")
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
                                                           "construction"])
     args = ap.parse_args()

@@ -931,6 +931,9 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   const int* list = P.at<int>(P.o_k2big);
   const int spn = spw < 0 ? -spw : spw;
   const int s = threadIdx.x / LPS;
+  // the wide launch's few long chains (slots over the main launch's rows) run beside the whole
+  // main launch and end the step when they trail it: they take their SIMD first
+  if (big) __builtin_amdgcn_s_setprio(3);
   for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
     const int idx = (s < spn && base + s < cnt) ? base + s : -1;
     const int slot = big ? (idx >= 0 ? list[idx] : -1) : sorted_slot(P, idx, LPS);
