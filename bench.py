@@ -7,8 +7,9 @@
 One "step" = one SoccerVectorEnv.step over all envs of a rank: action clip, goalkeeper, wind,
 mj_step (kinematics .. PGS .. Euler) and observation/reward/termination for every env, with
 same-step autoreset — mgx_soccer_step, the staged kernels k_soccer_rows -> k_pgs_groups ->
-k_soccer_finish -> k_soccer_fixup on one stream (--mono: one fused kernel).
-Reset settle steps of the precomputed reset banks run inside the same launches. Actions are
+k_soccer_bank_finish -> k_soccer_finish -> k_soccer_settle (the resets whose bank was not ready)
+on one stream (--mono: one fused kernel). Reset settle steps of the precomputed
+reset banks run as extra slots of the same launches. Actions are
 synthetic U(-150, 150)^33 float32 drawn before the timed region and resident in HBM.
 Ranks shard envs (global index = rank * envs + i); the only collective is the end-of-rollout
 metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
@@ -50,6 +51,7 @@ PMC_PROFILE = {"f64": "r04_head_pmc.json", "f32": "r03_f32_pmc.json"}
 PMC_PROFILE_BIPEDAL = "r04_bipedal_pmc.json"
 PMC_PROFILE_ASSEMBLY = "r03_assembly_pmc.json"
 PMC_PROFILE_PARKOUR = "r03_parkour_pmc.json"
+PMC_PROFILE_CONSTRUCTION = "r04_construction_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
@@ -707,7 +709,9 @@ def main():
                        "bad_state_resets": int(acc[5].item()), "capacity_overflow_steps": overflow_steps,
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": _pmc_traffic(PMC_PROFILE_CONSTRUCTION, N, "f64", "wide (two dofs per lane)"),
+                         "profile": f"profiles/{PMC_PROFILE_CONSTRUCTION}",
                          "kernel": "mgx_construction_step = k_construction<double,0>",
                          "alg_bytes_per_step": bytes_per_launch, "launch_ms": round(launch_ms, 4)},
         }
@@ -756,8 +760,8 @@ def main():
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("mgx_soccer_step = k_soccer_rows + k_pgs_groups + k_soccer_finish + k_soccer_fixup"
-                                    if mode == "staged" else "mgx_soccer_step = k_soccer<T,0>"),
+                         "kernel": ("mgx_soccer_step = k_soccer_rows + k_pgs_groups + k_soccer_bank_finish + "
+                                    "k_soccer_finish + k_soccer_settle (fixups)" if mode == "staged" else "mgx_soccer_step = k_soccer<T,0>"),
                          "profile": f"profiles/{PMC_PROFILE[args.precision]}",
                          "alg_bytes_per_step": bytes_per_launch, "launch_ms": round(launch_ms, 4),
                          "note": "achieved = algorithmic bytes of one env step x envs / HIP-event time of the "
