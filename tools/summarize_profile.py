@@ -20,6 +20,8 @@ STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_bank_finish", "k_socc
                 "k_parkour<float, 0>", "k_parkour<float, 0, true>", "k_parkour<float, 0, false>",
                 "k_martial<float, 0, true>", "k_martial<float, 0, false>",
                 "k_assembly<double, 0, true>", "k_assembly<double, 0, false>",
+                "k_parkour<double, 0, true>", "k_parkour<double, 0, false>", "k_martial<double, 0, true>",
+                "k_martial<double, 0, false>", "k_dancing<double, 0, true>", "k_dancing<double, 0, false>",
                 "k_construction<double, 0>", "k_construction<double, 0, true>", "k_construction<double, 0, false>"]
 
 
