@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(64) k_rk_finish(DevModel<T> m, BipedalIds ids,
 // in sequence (rk_rows_slot, the PGS of the one slot, rk_finish_slot).
 template <typename T>
 __device__ __forceinline__ void rk_settle_step(const DevModel<T>& Ms, const DevModel<T>& Mf, const BipedalIds& ids,
-                                               mgx_state s, mgx_bipedal_env be, const Pipe& P, char* smem, int* lst,
+                                               mgx_state s, mgx_bipedal_env be, const Pipe& P, char* smem,
                                                int env, int bi, int slot, int maxit, T tol, T scale) {
   for (int stage = 0; stage < 4; stage++) {
     {
@@ -440,8 +440,6 @@ __device__ __forceinline__ void rk_settle_step(const DevModel<T>& Ms, const DevM
       rk_rows_slot(Ms, e, ids, s, be, nullptr, P, env, bi, slot, stage, false);
     }
     __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) lst[0] = slot;
     __syncthreads();
     pgs_group<T, RK_EPL, RK_LPS, false, RK_TW>(P, smem, threadIdx.x < RK_LPS ? slot : -1, P.maxE, maxit, tol, scale,
                                                64 / RK_LPS);
@@ -461,7 +459,7 @@ __device__ __forceinline__ void rk_settle_step(const DevModel<T>& Ms, const DevM
 // (rescue_env.py:390-391); the record ends finalized with bk = 10.
 template <typename T>
 __device__ __forceinline__ void rk_settle_reset(const DevModel<T>& Ms, const DevModel<T>& Mf, const BipedalIds& ids,
-                                                mgx_state s, mgx_bipedal_env be, const Pipe& P, char* smem, int* lst,
+                                                mgx_state s, mgx_bipedal_env be, const Pipe& P, char* smem,
                                                 int env, int bi, int episode, const T* draws, uint64_t seed,
                                                 int env_offset, int maxit, T tol, T scale) {
   {
@@ -478,7 +476,7 @@ __device__ __forceinline__ void rk_settle_reset(const DevModel<T>& Ms, const Dev
   }
   __threadfence();
   __syncthreads();
-  for (int t = 0; t < 10; t++) rk_settle_step(Ms, Mf, ids, s, be, P, smem, lst, env, bi, env, maxit, tol, scale);
+  for (int t = 0; t < 10; t++) rk_settle_step(Ms, Mf, ids, s, be, P, smem, env, bi, env, maxit, tol, scale);
 }
 
 // reset() of a staged batch (RK_SETTLE_RESET, one workgroup per env; with Philox draws and banks
@@ -490,7 +488,6 @@ __global__ void __launch_bounds__(64) k_rk_settle(DevModel<T> Ms, DevModel<T> Mf
                                                   int env_offset, int n_env, const uint8_t* mask, Pipe P, int mode,
                                                   int maxit, T tol, T scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int lst[4];
   const int cnt = mode == RK_SETTLE_FIXUP ? P.ctr()[5] : n_env;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const int env = mode == RK_SETTLE_FIXUP ? P.at<int>(P.o_fix)[i] : i;
@@ -498,7 +495,7 @@ __global__ void __launch_bounds__(64) k_rk_settle(DevModel<T> Ms, DevModel<T> Mf
     const int E = be.episode ? be.episode[env] : 0;
     const int bi = P.R > 0 ? env * P.R + E % P.R : env;
     const T* d = draws ? draws + (size_t)env * 12 : nullptr;
-    rk_settle_reset(Ms, Mf, ids, s, be, P, smem, lst, env, bi, E, d, seed, env_offset, maxit, tol, scale);
+    rk_settle_reset(Ms, Mf, ids, s, be, P, smem, env, bi, E, d, seed, env_offset, maxit, tol, scale);
     rk_bank_copy_live(Mf, P, s, be, obs, env, bi, E);
     if (P.R > 0 && mode == RK_SETTLE_FIXUP) {
       Env<T> e;
@@ -507,7 +504,7 @@ __global__ void __launch_bounds__(64) k_rk_settle(DevModel<T> Ms, DevModel<T> Mf
       rk_bank_init(Ms, e, ids, P, env, bi, E + P.R, seed, env_offset);
     } else if (P.R > 0 && !draws) {
       for (int k = 1; k <= P.R; k++)
-        rk_settle_reset(Ms, Mf, ids, s, be, P, smem, lst, env, env * P.R + (E + k) % P.R, E + k, (const T*)nullptr, seed,
+        rk_settle_reset(Ms, Mf, ids, s, be, P, smem, env, env * P.R + (E + k) % P.R, E + k, (const T*)nullptr, seed,
                         env_offset, maxit, tol, scale);
     } else if (lane_id() == 0) {
       P.at<int>(P.o_bk)[bi] = -1;  // a scratch record: nothing to settle

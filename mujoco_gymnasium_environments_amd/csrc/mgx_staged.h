@@ -1144,7 +1144,7 @@ __device__ __forceinline__ bool bank_install(const DevModel<T>& m, Env<T>& e, co
 // count is a performance knob only. Returns with the finisher's Env (layout Mf) in `smem`.
 template <typename T, int EPL, int LPS>
 __device__ __forceinline__ void settle_step(const DevModel<T>& Ms, const DevModel<T>& Mf, const SoccerIds<T>& ids,
-                                            const Pipe& P, char* smem, int* lst, Env<T>& f, int bi, int slot,
+                                            const Pipe& P, char* smem, Env<T>& f, int bi, int slot,
                                             int maxit, T tol, T scale, bool last) {
   {
     Env<T> e;
@@ -1157,8 +1157,6 @@ __device__ __forceinline__ void settle_step(const DevModel<T>& Ms, const DevMode
     stage_rows(Ms, e, P, slot, warn, false);
   }
   __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) lst[0] = slot;
   __syncthreads();
   pgs_group<T, EPL, LPS, false>(P, smem, threadIdx.x < LPS ? slot : -1, P.maxE, maxit, tol, scale, 64 / LPS);
   __threadfence();
@@ -1179,7 +1177,7 @@ __device__ __forceinline__ void settle_step(const DevModel<T>& Ms, const DevMode
 // (soccer_env.py:378-379: 10 mj_steps from the randomised pose); bk = 10 at the end.
 template <typename T, int EPL, int LPS>
 __device__ __forceinline__ void settle_reset(const DevModel<T>& Ms, const DevModel<T>& Mf, const SoccerIds<T>& ids,
-                                             const Pipe& P, char* smem, int* lst, int env, int bi, int episode,
+                                             const Pipe& P, char* smem, int env, int bi, int episode,
                                              const T* draws, uint64_t seed, int env_offset, int maxit, T tol, T scale) {
   {
     Env<T> e;
@@ -1196,7 +1194,7 @@ __device__ __forceinline__ void settle_reset(const DevModel<T>& Ms, const DevMod
   __threadfence();
   __syncthreads();
   Env<T> f;
-  for (int t = 0; t < 10; t++) settle_step<T, EPL, LPS>(Ms, Mf, ids, P, smem, lst, f, bi, env, maxit, tol, scale, t == 9);
+  for (int t = 0; t < 10; t++) settle_step<T, EPL, LPS>(Ms, Mf, ids, P, smem, f, bi, env, maxit, tol, scale, t == 9);
   if (lane_id() == 0) P.at<int>(P.o_bk)[bi] = 10;
   __threadfence();
   __syncthreads();
@@ -1213,7 +1211,6 @@ __global__ void __launch_bounds__(64) k_soccer_settle(DevModel<T> Ms, DevModel<T
                                                       int env_offset, int n_env, const uint8_t* mask, Pipe P, int mode,
                                                       int maxit, T tol, T scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int lst[4];
   const int cnt = mode == SETTLE_FIXUP ? P.ctr()[0] : n_env;
   for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
     const int env = mode == SETTLE_FIXUP ? P.at<int>(P.o_fix)[i] >> 2 : i;
@@ -1221,7 +1218,7 @@ __global__ void __launch_bounds__(64) k_soccer_settle(DevModel<T> Ms, DevModel<T
     const int E = ev.episode ? ev.episode[env] : 0;
     const int bi = P.R > 0 ? env * P.R + E % P.R : env;  // R = 0: one scratch record per env
     const T* d = draws ? draws + (size_t)env * 36 : nullptr;
-    settle_reset<T, EPL, LPS>(Ms, Mf, ids, P, smem, lst, env, bi, E, d, seed, env_offset, maxit, tol, scale);
+    settle_reset<T, EPL, LPS>(Ms, Mf, ids, P, smem, env, bi, E, d, seed, env_offset, maxit, tol, scale);
     bank_copy_live(Mf, P, s, ev, obs, env, bi, E);
     if (P.R > 0 && mode == SETTLE_FIXUP) {
       // as bank_install: the consumed bank restarts for episode E + R (the pipeline settles it)
@@ -1232,7 +1229,7 @@ __global__ void __launch_bounds__(64) k_soccer_settle(DevModel<T> Ms, DevModel<T
     } else if (P.R > 0 && !draws) {
       // reset(): prefill the banks of episodes E + 1 .. E + R, so the first R terminations never wait
       for (int k = 1; k <= P.R; k++)
-        settle_reset<T, EPL, LPS>(Ms, Mf, ids, P, smem, lst, env, env * P.R + (E + k) % P.R, E + k, nullptr, seed,
+        settle_reset<T, EPL, LPS>(Ms, Mf, ids, P, smem, env, env * P.R + (E + k) % P.R, E + k, nullptr, seed,
                                   env_offset, maxit, tol, scale);
     } else if (lane_id() == 0) {
       P.at<int>(P.o_bk)[bi] = -1;  // a scratch record (R = 0, or host draws): nothing to settle
