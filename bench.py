@@ -407,7 +407,10 @@ def bench_mixed(args, dev, world, rank, dist):
         # beside bipedal and soccer, two A/B pairs on one box)
         groups = [["humanoid_construction"], ["robotic_arm_assembly"],
                   ["bipedal_rescue", "humanoid_soccer"], ["quadruped_parkour", "humanoid_martial_arts", "humanoid_dancing"]]
-        gs = [torch.cuda.Stream(device=dev, priority=-1 if i == 0 and args.mix_priority else 0) for i in range(len(groups))]
+        # MGX_MIX_PRIO_GROUPS (A/B hook): which groups run at high priority; 0 / 0,1 / 1 measured
+        # within noise of each other (75.3k - 75.9k, profiles/r04_mixed_priority_ab.json)
+        hi = {int(x) for x in os.environ.get("MGX_MIX_PRIO_GROUPS", "0").split(",") if x} if args.mix_priority else set()
+        gs = [torch.cuda.Stream(device=dev, priority=-1 if i in hi else 0) for i in range(len(groups))]
         streams = {k: gs[i] for i, grp in enumerate(groups) for k in grp}
     pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
     for k, (env, _, _) in tasks.items():
