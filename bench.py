@@ -62,6 +62,9 @@ ALG_BYTES_PER_ENV_STEP_F64 = 8 * (2 * 121 + 2 * 3 + 2 * 11) + 4 * (33 + 80) + 8 
 # ctrl, read action 16, r/w last_position 3 + max_progress 1 (fp32), r/w episode_reward (fp64)
 # + er_kind (u8) + reached/fall/stuck/step (int32), write obs 95, reward (fp64), flags (u8)
 PARKOUR_ALG_BYTES = 4 * (2 * 112 + 2 * 2 + 16 + 2 * 4 + 95) + 2 * 8 + 2 + 2 * 16 + 8 + 2
+# fp64 (the default precision): the physics state, the motor ctrl and last_position / max_progress
+# in 8 bytes
+PARKOUR_ALG_BYTES_F64 = 8 * (2 * 112 + 2 * 2 + 2 * 4) + 4 * (16 + 95) + 2 * 8 + 2 + 2 * 16 + 8 + 2
 PARKOUR_METRIC = "env steps/sec (whole node), quadruped_parkour 4096 envs/GPU (BASELINE configs[1])"
 # bipedal: r/w qpos 63 + qvel 63 + qacc_warmstart 63 and ctrl 26 (fp32), read
 # action 26, r/w nine int32 task scalars, energy + energy_used (fp32), carrying (u8), closest,
@@ -75,12 +78,14 @@ BIPEDAL_METRIC = "env steps/sec (whole node), bipedal_rescue 8192 envs/GPU (BASE
 # int32 task scalars + 3 hist, prev_jvel 23 (fp64), read the 20-move sequence (int32 + fp64),
 # obs 94, reward, flags
 DANCING_ALG_BYTES = 4 * (2 * 87 + 2 * 29 + 29 + 2 * 8 + 2 * 3 + 20 + 94) + 8 * (2 * 18 + 2 * 23 + 20 + 1) + 2
+DANCING_ALG_BYTES_F64 = 8 * (2 * 87 + 2 * 29) + 4 * (29 + 2 * 8 + 2 * 3 + 20 + 94) + 8 * (2 * 18 + 2 * 23 + 20 + 1) + 2
 # martial arts: r/w qpos 50 + qvel 47 + qacc_warmstart 47 and ctrl 28 (fp32), action 28, r/w 5 fp64
 # + 4 int32 task scalars, obs 113, reward, flags
 MARTIAL_ALG_BYTES = 4 * (2 * 144 + 2 * 28 + 28 + 2 * 4 + 113) + 8 * (2 * 5 + 1) + 2
-# assembly: r/w qpos 72 + qvel 63 + qacc_warmstart 63 and ctrl 9 (fp32), action 9, r/w 16 int32
-# task words + cumulative reward (fp64), obs 110, reward, flags
-ASSEMBLY_ALG_BYTES = 4 * (2 * 198 + 2 * 9 + 9 + 2 * 16 + 110) + 8 * (2 + 1) + 2
+MARTIAL_ALG_BYTES_F64 = 8 * (2 * 144 + 2 * 28) + 4 * (28 + 2 * 4 + 113) + 8 * (2 * 5 + 1) + 2
+# assembly (fp64 only): r/w qpos 72 + qvel 63 + qacc_warmstart 63 and ctrl 9 (fp64), action 9,
+# r/w 16 int32 task words + cumulative reward (fp64), obs 110 (fp32), reward, flags
+ASSEMBLY_ALG_BYTES = 8 * (2 * 198 + 2 * 9) + 4 * (9 + 2 * 16 + 110) + 8 * (2 + 1) + 2
 # construction (fp64): r/w qpos 110 + qvel 99 + qacc_warmstart 99 and ctrl 33, action 33 (fp32), r/w
 # 4 fp64 + 5 int32 task scalars and the fp32 total, obs 135, reward, flags
 CONSTRUCTION_ALG_BYTES = 8 * (2 * 308 + 2 * 33 + 2 * 4 + 1) + 4 * (33 + 2 * 5 + 2 + 135) + 2
@@ -352,6 +357,31 @@ def cpu_baseline_assembly(n_envs: int, n_steps: int, seed: int = 0) -> dict:
             "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
 
 
+MIXED_GROUPS = [["humanoid_construction"], ["robotic_arm_assembly"],
+                ["bipedal_rescue", "humanoid_soccer"], ["quadruped_parkour", "humanoid_martial_arts", "humanoid_dancing"]]
+
+
+def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
+    """The mixed run's HIP streams per task (tests/test_gpu_mixed.py steps the same layout).
+
+    HIP streams map onto GPU_MAX_HW_QUEUES hardware queues (4 on the box): with a stream per
+    task (7, plus the staged tasks' side streams) unrelated tasks share queues and wait on each
+    other's kernels. Four streams instead: construction and assembly (the long Newton steps)
+    each on its own, the five PGS tasks split over two; no side streams (MGX_SIDE_STREAM=0).
+    Construction's stream (the longest) runs at high priority (mix_priority 1, measured 73.2k ->
+    75.5k env-steps/s). mix_streams 7: the old one-stream-per-task layout (67.3k)."""
+    if mix_streams >= len(tasks):
+        return {k: torch.cuda.Stream(device=dev) for k in tasks}
+    os.environ["MGX_SIDE_STREAM"] = "0"
+    # (dancing with parkour and martial arts: 75.5 / 76.7k against 74.9 / 75.0k with dancing
+    # beside bipedal and soccer, two A/B pairs on one box)
+    # MGX_MIX_PRIO_GROUPS (A/B hook): which groups run at high priority; 0 / 0,1 / 1 measured
+    # within noise of each other (75.3k - 75.9k, profiles/r04_mixed_priority_ab.json)
+    hi = {int(x) for x in os.environ.get("MGX_MIX_PRIO_GROUPS", "0").split(",") if x} if mix_priority else set()
+    gs = [torch.cuda.Stream(device=dev, priority=-1 if i in hi else 0) for i in range(len(MIXED_GROUPS))]
+    return {k: gs[i] for i, grp in enumerate(MIXED_GROUPS) for k in grp if k in tasks}
+
+
 def bench_mixed(args, dev, world, rank, dist):
     """BASELINE configs[4]: every built task, N envs each, one HIP stream per task."""
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout
@@ -364,6 +394,7 @@ def bench_mixed(args, dev, world, rank, dist):
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     N = args.envs
     off = env_offset(rank, N)
+    f64 = args.precision == "f64"
     g = torch.Generator(device=dev)
     g.manual_seed(2000 + rank)
     plim = torch.as_tensor(action_limits(), dtype=torch.float32, device=dev)
@@ -373,16 +404,20 @@ def bench_mixed(args, dev, world, rank, dist):
     tasks = {
         "humanoid_soccer": (SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=11, env_offset=off,
                                             banks=args.banks), lambda: torch.rand(N, 33, device=dev, generator=g) * 300 - 150,
-                            ALG_BYTES_PER_ENV_STEP),
+                            ALG_BYTES_PER_ENV_STEP_F64 if f64 else ALG_BYTES_PER_ENV_STEP),
         "quadruped_parkour": (ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=12, env_offset=off),
-                              lambda: (torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim, PARKOUR_ALG_BYTES),
+                              lambda: (torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim,
+                              PARKOUR_ALG_BYTES_F64 if f64 else PARKOUR_ALG_BYTES),
         "bipedal_rescue": (BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=13, env_offset=off),
-                           lambda: (torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0, BIPEDAL_ALG_BYTES),
+                           lambda: (torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0,
+                           BIPEDAL_ALG_BYTES_F64 if f64 else BIPEDAL_ALG_BYTES),
         "humanoid_dancing": (DancingVectorEnv(N, device=str(dev), precision=args.precision, seed=14, env_offset=off),
-                             lambda: (torch.rand(N, 29, device=dev, generator=g) * 2 - 1) * 200.0, DANCING_ALG_BYTES),
+                             lambda: (torch.rand(N, 29, device=dev, generator=g) * 2 - 1) * 200.0,
+                             DANCING_ALG_BYTES_F64 if f64 else DANCING_ALG_BYTES),
         "humanoid_martial_arts": (MartialArtsVectorEnv(N, device=str(dev), precision=args.precision, seed=15,
                                                        env_offset=off),
-                                  lambda: torch.rand(N, 28, device=dev, generator=g) * 2 - 1, MARTIAL_ALG_BYTES),
+                                  lambda: torch.rand(N, 28, device=dev, generator=g) * 2 - 1,
+                                  MARTIAL_ALG_BYTES_F64 if f64 else MARTIAL_ALG_BYTES),
         # assembly's reset is deterministic (assembly_env.py:162-218): no seed; fp64 only (its
         # degenerate base contact breaks the fp32 Newton factorisation, envs/assembly.py)
         "robotic_arm_assembly": (AssemblyVectorEnv(N, device=str(dev), precision="f64"),
@@ -393,25 +428,7 @@ def bench_mixed(args, dev, world, rank, dist):
                                   lambda: (torch.rand(N, 33, device=dev, generator=g) * 2 - 1) * 200.0,
                                   CONSTRUCTION_ALG_BYTES),
     }
-    # HIP streams map onto GPU_MAX_HW_QUEUES hardware queues (4 on the box): with a stream per
-    # task (7, plus the staged tasks' side streams) unrelated tasks share queues and wait on each
-    # other's kernels. Four streams instead: construction and assembly (the long Newton steps)
-    # each on its own, the five PGS tasks split over two; no side streams (MGX_SIDE_STREAM=0).
-    # Construction's stream (the longest) runs at high priority (--mix-priority 1, measured 73.2k ->
-    # 75.5k env-steps/s). --mix-streams 7: the old one-stream-per-task layout (67.3k).
-    if args.mix_streams >= len(tasks):
-        streams = {k: torch.cuda.Stream(device=dev) for k in tasks}
-    else:
-        os.environ["MGX_SIDE_STREAM"] = "0"
-        # (dancing with parkour and martial arts: 75.5 / 76.7k against 74.9 / 75.0k with dancing
-        # beside bipedal and soccer, two A/B pairs on one box)
-        groups = [["humanoid_construction"], ["robotic_arm_assembly"],
-                  ["bipedal_rescue", "humanoid_soccer"], ["quadruped_parkour", "humanoid_martial_arts", "humanoid_dancing"]]
-        # MGX_MIX_PRIO_GROUPS (A/B hook): which groups run at high priority; 0 / 0,1 / 1 measured
-        # within noise of each other (75.3k - 75.9k, profiles/r04_mixed_priority_ab.json)
-        hi = {int(x) for x in os.environ.get("MGX_MIX_PRIO_GROUPS", "0").split(",") if x} if args.mix_priority else set()
-        gs = [torch.cuda.Stream(device=dev, priority=-1 if i in hi else 0) for i in range(len(groups))]
-        streams = {k: gs[i] for i, grp in enumerate(groups) for k in grp}
+    streams = mixed_streams(list(tasks), args.mix_streams, args.mix_priority, dev)
     pools = {k: [f().contiguous() for _ in range(8)] for k, (_, f, _) in tasks.items()}
     for k, (env, _, _) in tasks.items():
         env.reset()
@@ -552,7 +569,9 @@ def main():
     ap.add_argument("--mono", action="store_true", help="monolithic one-wave-per-env kernel instead of the staged step")
     ap.add_argument("--banks", type=int, default=3, help="reset banks per env (3: measured fastest, DESIGN.md §4)")
     ap.add_argument("--full-capacity", action="store_true",
-                    help="soccer: 96 contacts / 384 rows per env instead of 64 / 192 (no overflow, slower)")
+                    help="soccer: 96 contacts / 384 rows per env (the default since round 5; kept for old scripts)")
+    ap.add_argument("--reduced-capacity", action="store_true",
+                    help="soccer: the round-1 capacity, 64 contacts / 192 rows, rows beyond it dropped and counted")
     ap.add_argument("--streams", type=int, default=1,
                     help="soccer: split the rank's envs into this many stream shards (overlapping pipelines)")
     ap.add_argument("--no-f64-line", "--no-other-line", dest="no_f64_line", action="store_true",
@@ -616,7 +635,7 @@ def main():
         else:
             env = SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=1234,
                                   env_offset=env_offset(rank, N), staged=not args.mono, banks=args.banks,
-                                  full_capacity=args.full_capacity)
+                                  full_capacity=not (args.reduced_capacity or args.mono))
         pool = [(torch.rand(N, env.model.nu, device=dev, generator=g) * 300.0 - 150.0).contiguous() for _ in range(16)]
     env.reset()
     for k in range(args.warmup):
@@ -722,7 +741,7 @@ def main():
         }
         print(json.dumps(out))
     elif rank == 0 and args.task == "parkour":
-        bytes_per_launch = PARKOUR_ALG_BYTES * N
+        bytes_per_launch = (PARKOUR_ALG_BYTES_F64 if args.precision == "f64" else PARKOUR_ALG_BYTES) * N
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         out = {
             "metric": PARKOUR_METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world,
@@ -761,7 +780,7 @@ def main():
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "capacity_overflow_steps": overflow_steps,
-                       "capacity": "96 contacts / 384 rows" if args.full_capacity else "64 contacts / 192 rows",
+                       "capacity": "64 contacts / 192 rows" if (args.reduced_capacity or args.mono) else "96 contacts / 384 rows",
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -211,7 +211,8 @@ int mgx_soccer_workspace_init(const mgx_model *m, void *workspace, uint64_t byte
                               void *stream);
 /* Diagnostics: the workspace's solver-side layout, out[0..9] = byte offsets of the counters,
  * per-slot row counts, solver slot list, block tables, B, then bcap (reals per slot), max_nefc,
- * the main solver launch's LDS rows, slot count, real size (4 | 8). Returns 0 or an error. */
+ * the main solver launch's LDS rows, slot count, real size (4 | 8), and (n_out >= 11) the wide
+ * solver's slot list. Returns 0 or an error. */
 int mgx_soccer_workspace_layout(const mgx_model *m, int n_env, int banks, int64_t *out, int n_out);
 
 /* Test hook: env logic only, on caller-supplied frames and contact lists (no physics). */

@@ -347,9 +347,9 @@ Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon,
   L.cfs = 3;
   L.qpos = take(d->nq); L.qvel = take(nv); L.ctrl = take(d->nu);
   L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.subtree_com = take(3 * nb);
-  L.qLD = take(d->nM); L.con_dist = take(max_ncon); L.con_mu = take(max_ncon);
+  L.qLD = take(d->nM); L.con_dist = take(max_ncon);
   L.carry_lds = p;
-  L.xfrc = take(6 * nb); L.qMH = take(d->nM);
+  L.con_mu = take(max_ncon); L.xfrc = take(6 * nb); L.qMH = take(d->nM);
   L.carry_reals = p;
   p = L.carry_lds;  // the row builder's LDS continues after the LDS part of the carry
   const int nvw = nv > 64 ? 128 : 64;
@@ -370,8 +370,9 @@ Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon,
   const int ecap = std::min(max_nefc, align_up(2 * nj, 4));  // efc_id: the joint-limit rows only
   const int nlist = std::max(max_active, ecap);
   L.geom_xpos = R; L.geom_xmat = L.geom_xpos + a(3 * ng);
-  L.con_frame = L.geom_xmat + a(9 * ng); L.con_pos = L.con_frame + a(3 * max_ncon);
-  L.act_union = L.con_pos + a(3 * max_ncon);
+  L.con_frame = L.geom_xmat + a(9 * ng);
+  L.gcon = 1; L.con_pos = 0;  // the contact points live in the pipe (Pipe.o_cpos)
+  L.act_union = L.con_frame + a(3 * max_ncon);
   const int endC = L.act_union + a((nlist * 4 + real_bytes - 1) / real_bytes);
   // phase D: cacc (12 per body) over the geom poses when they cover it, else after phase C
   L.cacc = a(12 * nb) <= L.con_frame - R ? R : endC;
@@ -531,6 +532,21 @@ static int pgs_arena_bytes(int precision) {
   return pgs_lanes() == 64 ? a / 2 : a;
 }
 
+// LDS bytes of the soccer wide launch's one-slot waves with B in LDS (pgs_group BLDS sizes: whole
+// ring turns of blocks plus the look-ahead, 16-byte rounded B) for the model's largest slot, or 0
+// when that exceeds 160 KiB or MGX_PGS_WIDE_LDS=0 (B from global memory, the A/B alternative)
+static int wide_arena_bytes(const mgx_model* m) {
+  static const int wide_lds = getenv("MGX_PGS_WIDE_LDS") ? atoi(getenv("MGX_PGS_WIDE_LDS")) : 1;
+  const int rb = m->precision == MGX_F32 ? 4 : 8;
+  const int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
+  const int maxE = m->Ls.max_nefc;
+  const int nbRun = (maxE / 4 + MGX_PGS_RING_LDS - 1) / MGX_PGS_RING_LDS * MGX_PGS_RING_LDS;
+  const int nbA = nbRun + MGX_PGS_RING_LDS - 1;
+  const int bcap = 32 + (maxE / 4) * (8 + 32 * ((nv + 7) / 8));
+  const int worst = nbA * (4 * MGX_SCAL * rb + 4 * MGX_TW) + ((bcap + 3) & ~3) * rb;
+  return wide_lds && pgs_lanes() == 16 && worst + 64 <= 160 * 1024 ? (worst + 15) & ~15 : 0;
+}
+
 // Staged-step workspace layout for (model, n_env, banks); offsets in bytes, 256-aligned. rk: the
 // RK4 staged step's extra arrays (stage carry, template scratch); nobs: floats per bank observation.
 size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P, bool rk, int nobs) {
@@ -545,7 +561,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   // states exercise the wide-LDS launch (tests/test_gpu_capacity.py)
   const char* cap_env = getenv("MGX_PGS_LDS_ROWS");
   int capE = cap_env ? (atoi(cap_env) + 3) / 4 * 4 : MGX_PGS_LDS_ROWS;
-  if (capE < 4 || capE > MGX_PGS_LDS_ROWS) capE = MGX_PGS_LDS_ROWS;
+  if (capE < 4 || capE > p.maxE) capE = MGX_PGS_LDS_ROWS;
   if (rk) {
     // the RK4 pipeline's rows (bipedal: ~150 per forward, up to 512): MGX_RK_LDS_ROWS, default 256
     const char* rk_env = getenv("MGX_RK_LDS_ROWS");
@@ -553,6 +569,22 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
     if (capE < 4) capE = 256;
   }
   p.capE = p.maxE < capE ? p.maxE : capE;
+  // soccer at full capacity (more rows than the 192 the LDS-scalar main launch holds at four waves
+  // per CU): one main launch over every slot with its row scalars read from the pipe and only the
+  // forces in LDS (pgs_group SQG), so a slot of 200+ rows is solved in the heaviest-first main
+  // launch instead of a trailing wide launch. MGX_PGS_SPLIT=1 (A/B) or the MGX_PGS_LDS_ROWS test
+  // hook keep the split: 192 LDS-scalar rows in the main launch, the rest in the wide launch.
+  static const int split = getenv("MGX_PGS_SPLIT") ? atoi(getenv("MGX_PGS_SPLIT")) : 0;
+  p.sqg = 0;
+  if (!rk && !cap_env && !split && !pgs_lds_b() && p.maxE > MGX_PGS_LDS_ROWS) {
+    p.capE = p.maxE;
+    p.sqg = 1;
+  }
+  // the wide launch (slots over capE rows: soccer in the split mode) copies its one slot's B, row
+  // scalars and block table into LDS when the largest slot fits 160 KiB (MGX_PGS_WIDE_LDS=0: B
+  // from global memory, the A/B alternative). Same sizes as pgs_group's BLDS path: whole ring
+  // turns of blocks plus the look-ahead, 16-byte rounded B.
+  p.warena = !rk && p.maxE > p.capE ? wide_arena_bytes(m) : 0;
   // LDS arena of one main-launch solver wave (scalars + block table + B of its slots); the
   // test / tuning hook MGX_PGS_ARENA overrides it (read per call; a small arena sends waves to
   // the global-B launch)
@@ -562,7 +594,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
-  p.tw = nv > 56 ? 16 : 8;
+  p.tw = MGX_TW;  // block-table words per 4-row block: B offset + 64-bit dof support, any nv <= 64
   p.nobs = nobs;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t r = off; off = (off + bytes + 255) / 256 * 256; return r; };
@@ -577,7 +609,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.o_hist = take((size_t)(p.maxE / 4 + 1) * 4);
   p.o_blist = take((size_t)(p.maxE / 4 + 1) * S * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
-  p.o_blk = take(S * p.maxE * p.tw / 2);  // tw uint16 per 4-row block
+  p.o_blk = take(S * (p.maxE / 4) * p.tw * 4);  // tw uint32 per 4-row block
   p.o_B = take(S * (size_t)p.bcap * rb);
   p.o_vout = take(S * 64 * rb);
   p.o_bq = take(NB * nq * rb); p.o_bv = take(NB * nv * rb); p.o_ba = take(NB * nv * rb); p.o_btime = take(NB * rb);
@@ -585,6 +617,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.o_bk = take(NB * 4); p.o_bep = take(NB * 4); p.o_bwarn = take(NB * 4); p.o_bseed = take(NB * 8);
   int nb = m->precision == MGX_F32 ? m->mf.nbody : m->md.nbody;
   p.maxC = m->Ls.max_ncon;
+  p.o_cpos = take(S * 3 * (size_t)p.maxC * rb);
   p.o_tq = take(nq * rb); p.o_tv = take(nv * rb); p.o_ta = take(64 * rb); p.o_tt = take(rb);
   p.o_tx = take(3 * nb * rb); p.o_txq = take(4 * nb * rb); p.o_tsc = take(3 * nb * rb); p.o_tn = take(4);
   p.o_tcg = take(2 * p.maxC * 4); p.o_tcd = take(p.maxC * rb); p.o_tcm = take(p.maxC * rb);
@@ -605,16 +638,16 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 
 // LDS of one solver wave holding `rows` rows per slot (main launch: min(max_nefc,
 // MGX_PGS_LDS_ROWS); wide launch: max_nefc)
-int mgx::staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int tw) {
+int mgx::staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nb3 = (rows / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
   const int spw = 64 / lps;
   // the row scalars (or, SQG: the forces only; pgs_group) + the block table
-  const int sq = tw > 8 ? 4 : 4 * MGX_SCAL;
-  return spw * (sq * nb3 + 4) * rb + spw * nb3 * 4 * tw + 64;
+  const int sq = sqg ? 4 : 4 * MGX_SCAL;
+  return spw * (sq * nb3 + 4) * rb + spw * nb3 * 4 * MGX_TW + 64;
 }
-static int pgs_lds_bytes(const mgx_model* m, int rows) {
-  return staged_pgs_lds_bytes(m, rows, pgs_lanes(), 8);
+static int pgs_lds_bytes(const mgx_model* m, int rows, int sqg = 0) {
+  return staged_pgs_lds_bytes(m, rows, pgs_lanes(), sqg);
 }
 
 // MGX_SIDE_STREAM=0 (read per call) runs the wide solver launch after the main one on the caller's
@@ -680,7 +713,7 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   // main launch (MGX_PGS_LDS_B) it also takes the waves that did not fit their arena, so it
   // follows the main launch there.
   const int wgrid = 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, wlds = pgs_lds_bytes(m, P.maxE);
-  int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE);
+  int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE, P.sqg);
   // occupancy probe: MGX_PGS_LDS_PAD pads the main solver launch's LDS (fewer waves per CU)
   if (const char* pad = getenv("MGX_PGS_LDS_PAD"))
     if (atoi(pad) > mlds && atoi(pad) <= 96 * 1024) mlds = atoi(pad);
@@ -786,16 +819,18 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   // the monolithic layout of a staged model (its reset settle steps, the rare fixup resets,
   // --mono, mgx_debug_forward) keeps rows in LDS at the default 192 rows / 64 contacts; the
   // staged step itself carries the model's full capacity
-  const int mono_nefc = m->staged_ok && max_nefc > 192 ? 192 : max_nefc;
+  // the staged RK4 step (mgx_rk_staged.h, bipedal_rescue): RK4 + PGS, nv 49..64 (four register
+  // entries per solver lane, a 16-word block table)
+  m->staged_rk_ok = d->integrator == 1 && d->solver == 0 && condim13 && d->nv > 48 && d->nv <= 64 &&
+                    max_nefc <= 1024 && max_ncon <= 192;  // three contact-metadata lane sets (RK_NCS)
+  // ... and of a staged RK4 model (its checkAcc template, --mono) at most 512 rows, whose per-row
+  // LDS arrays fit next to its working set with the rows in global scratch
+  const int mono_nefc = m->staged_ok && max_nefc > 192 ? 192 : (m->staged_rk_ok && max_nefc > 512 ? 512 : max_nefc);
   const int mono_ncon = m->staged_ok && max_ncon > 64 ? 64 : max_ncon;
   m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active);
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024 || (d->layout_flags & MGX_ROWS_IN_SCRATCH))
     m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, true);
-  // the staged RK4 step (mgx_rk_staged.h, bipedal_rescue): RK4 + PGS, nv 49..64 (four register
-  // entries per solver lane, a 16-word block table)
-  m->staged_rk_ok = d->integrator == 1 && d->solver == 0 && condim13 && d->nv > 48 && d->nv <= 64 &&
-                    max_nefc <= 1024 && max_ncon <= 128;
   const bool any_staged = m->staged_ok || m->staged_rk_ok;
   m->Ls = make_staged_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active);
   m->Lf = finisher_layout(m->Ls, rb);
@@ -830,7 +865,7 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
     int pl = pgs_lds_bytes(m, m->Ls.max_nefc);  // the global-B launch's
     if (pl < 96 * 1024) pl = 96 * 1024;  // the arena (MGX_PGS_ARENA tuning up to 96 KiB)
     if (pl > 160 * 1024) { delete m; return fail(MGX_E_CAPACITY, "solver LDS exceeds 160 KiB: lower MGX_MAX_NEFC"); }
-    int r3 = pgs_configure_lds(precision, pl);
+    int r3 = pgs_configure_lds(precision, pl, wide_arena_bytes(m) + 64);
     if (r3 != MGX_OK) { delete m; return r3; }
   }
   *out = m;
@@ -963,9 +998,9 @@ int mgx_soccer_workspace_layout(const mgx_model* m, int n_env, int banks, int64_
   if (!m->staged_ok) return fail(MGX_E_UNSUPPORTED, "staged step: model exceeds the staged solver's capacity");
   Pipe P;
   make_pipe(m, nullptr, n_env, banks, &P);
-  const int64_t v[10] = {(int64_t)P.o_ctr, (int64_t)P.o_ne, (int64_t)P.o_k2list, (int64_t)P.o_blk, (int64_t)P.o_B,
-                         P.bcap, P.maxE, P.capE, P.S, m->precision == MGX_F32 ? 4 : 8};
-  for (int i = 0; i < 10; i++) out[i] = v[i];
+  const int64_t v[11] = {(int64_t)P.o_ctr, (int64_t)P.o_ne, (int64_t)P.o_k2list, (int64_t)P.o_blk, (int64_t)P.o_B,
+                         P.bcap, P.maxE, P.capE, P.S, m->precision == MGX_F32 ? 4 : 8, (int64_t)P.o_k2big};
+  for (int i = 0; i < (n_out < 11 ? n_out : 11); i++) out[i] = v[i];
   return MGX_OK;
 }
 

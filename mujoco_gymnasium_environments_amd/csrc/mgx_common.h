@@ -63,6 +63,9 @@ struct Layout {
   // staged row builder: LDS copy of xfrc_applied for the velocity stage (its per-dof force sums
   // read it nbody times per lane), in the phase-A region
   int xfrc_lds;
+  // staged row builder: the contact points (3 reals per contact, written by collision, read by the
+  // row blocks) live in the slot's pipe storage (Pipe.o_cpos, bind_carry_tail), not in LDS
+  int gcon;
 };
 
 // Device-resident model: pointers into one device allocation.

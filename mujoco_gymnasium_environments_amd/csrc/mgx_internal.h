@@ -79,7 +79,8 @@ int step_kernels_configure(const mgx_model* m);
 // the staged solver S2 (mgx_pgs.hip)
 template <typename T>
 void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big);
-int pgs_configure_lds(int precision, int bytes);
+// bytes: the solver kernels' dynamic-LDS limit; wide: the LDS-B instantiations' (the wide launch)
+int pgs_configure_lds(int precision, int bytes, int wide);
 // S1 / S3 and the one-wave settle (mgx_pgs.hip, the staged TU)
 template <typename T>
 void launch_soccer_rows(const DevModel<T>& Ms, const SoccerIds<T>& ids, const mgx_state& s, const mgx_soccer_env& ev,
@@ -99,7 +100,8 @@ int staged_kernels_configure(int precision, int ls, int lf, int settle);
 // staged-step workspace layout (mgx_api.hip) and the LDS of one solver wave holding `rows` rows
 // per slot with `lps` lanes per slot and `tw` table words per block
 size_t make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P, bool rk, int nobs);
-int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int tw);
+// sqg: row scalars in the pipe, only the forces in LDS (the RK4 pipeline; soccer at full capacity)
+int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg);
 // the wide solver launch beside the main one on a side stream (MGX_SIDE_STREAM, default 1)
 int side_streams();
 // the staged RK4 bipedal step (mgx_rk_staged.hip)

@@ -12,11 +12,16 @@
 namespace mgx {
 
 // lanes per slot of the solver kernels: MGX_PGS_LPS (compile-time default) or the MGX_PGS_LPS
-// environment variable (16 or 64), read per call like the other solver hooks, for A/B runs
+// environment variable (16 or 64), for A/B runs. Read once per process: the settle and solver
+// kernels' dynamic-LDS limits are set at model creation from this value, so it must not change
+// between configure and launch.
 int pgs_lanes() {
-  const char* v = getenv("MGX_PGS_LPS");
-  const int x = v ? atoi(v) : MGX_PGS_LPS;
-  return x == 64 ? 64 : 16;
+  static const int lanes = [] {
+    const char* v = getenv("MGX_PGS_LPS");
+    const int x = v ? atoi(v) : MGX_PGS_LPS;
+    return x == 64 ? 64 : 16;
+  }();
+  return lanes;
 }
 // main launch with B in an LDS arena (1) or read from global memory (0): MGX_PGS_LDS_B
 // (compile-time default) or the environment variable of that name, read per call
@@ -25,15 +30,17 @@ int pgs_lds_b() {
   return e ? (atoi(e) != 0) : MGX_PGS_LDS_B;
 }
 
-template <typename T, int LPS, bool BLDS>
-static void launch_lps(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big) {
+template <typename T, int LPS, bool BLDS, bool SQG = false>
+static void launch_lps(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big,
+                       int spw_force = 0) {
   static const int spw_env = getenv("MGX_PGS_SPW") ? atoi(getenv("MGX_PGS_SPW")) : 0;  // debug: slots per wave
-  const int spw = spw_env ? spw_env : 64 / LPS;
+  const int spw = spw_force ? spw_force : spw_env ? spw_env : 64 / LPS;
   int grid = (slots + (spw < 0 ? -spw : spw) - 1) / (spw < 0 ? -spw : spw);
   switch ((P.dpl + LPS / 8 - 1) / (LPS / 8)) {  // register entries per lane
 #define MGX_PGS_CASE(E)                                                                                          \
     case E:                                                                                                     \
-      hipLaunchKernelGGL((k_pgs_groups<T, E, LPS, BLDS>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw, big); \
+      hipLaunchKernelGGL((k_pgs_groups<T, E, LPS, BLDS, SQG>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale, spw, \
+                         big);                                                                                  \
       break;
     MGX_PGS_CASE(1)
     default:
@@ -47,12 +54,19 @@ static void launch_lps(const Pipe& P, int slots, int lds, hipStream_t st, int ma
 
 template <typename T>
 void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big) {
+  if (big && P.warena > 0 && pgs_lanes() == 16) {
+    // the wide launch with LDS-resident B: one slot per wave (all four lane groups on it), a
+    // small grid striding over the few slots past the main launch's rows
+    launch_lps<T, 16, true>(P, MGX_PGS_WIDE_LDS_GRID, P.warena + 64, st, maxit, tol, scale, big, 1);
+    return;
+  }
   const bool blds = !big && pgs_lds_b();
   if (pgs_lanes() == 64) {
     if (blds) launch_lps<T, 64, true>(P, slots, lds, st, maxit, tol, scale, big);
     else launch_lps<T, 64, false>(P, slots, lds, st, maxit, tol, scale, big);
   } else {
     if (blds) launch_lps<T, 16, true>(P, slots, lds, st, maxit, tol, scale, big);
+    else if (P.sqg && !big) launch_lps<T, 16, false, true>(P, slots, lds, st, maxit, tol, scale, big);
     else launch_lps<T, 16, false>(P, slots, lds, st, maxit, tol, scale, big);
   }
 }
@@ -251,9 +265,11 @@ int staged_kernels_configure(int precision, int ls, int lf, int settle) {
   return rc;
 }
 
-int pgs_configure_lds(int precision, int pl) {
+int pgs_configure_lds(int precision, int pl, int wl) {
   int rc = 0;
-#define MGX_PGS_SET(T, E, L) rc |= mgx_set_lds(k_pgs_groups<T, E, L, true>, pl) | mgx_set_lds(k_pgs_groups<T, E, L, false>, pl);
+#define MGX_PGS_SET(T, E, L)                                                                            \
+  rc |= mgx_set_lds(k_pgs_groups<T, E, L, true>, pl > wl ? pl : wl) | mgx_set_lds(k_pgs_groups<T, E, L, false>, pl) | \
+        mgx_set_lds(k_pgs_groups<T, E, L, false, true>, pl);
 #define MGX_PGS_SET_ALL(T) \
   MGX_PGS_SET(T, 1, 16) MGX_PGS_SET(T, 2, 16) MGX_PGS_SET(T, 3, 16) MGX_PGS_SET(T, 4, 16) MGX_PGS_SET(T, 1, 64)
   if (precision == MGX_F32) { MGX_PGS_SET_ALL(float) } else { MGX_PGS_SET_ALL(double) }

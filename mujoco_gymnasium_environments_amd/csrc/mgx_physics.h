@@ -62,7 +62,8 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   // the staged row builder lists only its joint-limit rows, after collision, in the broadphase list
   e.efc_id = L.staged ? e.act_list : I + L.efc_id;
   // the staged row builder's carry tail lives in global memory (bind_carry_tail)
-  if (L.carry_lds < L.carry_reals) { e.xfrc = nullptr; e.qMH = nullptr; }
+  if (L.carry_lds < L.carry_reals) { e.xfrc = nullptr; e.qMH = nullptr; e.con_mu = nullptr; }
+  if (L.gcon) e.con_pos = nullptr;
   int l = lane_id();
   e.chainlen = l < m.nv ? m.dof_chainlen[l] : 0;
   e.madr = l < m.nv ? m.dof_Madr[l] : 0;

@@ -29,12 +29,17 @@ namespace mgx {
 // scalar layout per 4-row block (20 reals, 16-byte aligned): [b x4][f x4][R x4][1/AR x4][AR/2 x4],
 // so the solver reads each quantity of a block with one 16-byte LDS load
 #define MGX_SQ(k, i) (4 * (k) + (i))
+// block table: 4 words per 4-row block — the block's B offset (its couplings A_ij, then the
+// B entries of the dofs in its support), the 64-bit dof support mask, one pad word (16 bytes: one
+// vector load)
+#define MGX_TW 4
 #define MGX_PGS_LPS 16         // solver: lanes per slot (16 or 64; MGX_PGS_LPS env overrides per process)
 #define MGX_PGS_LDS_B 0        // main solver launch: 1 = B in an LDS arena, 0 = B from global memory
 #define MGX_PGS_RING 2         // global-B solver: register ring of 4-row blocks (RING - 1 in flight; 3 and 4 measured no faster)
 #define MGX_PGS_RING_LDS 2     // LDS-B solver: one block in flight covers the LDS latency
 #define MGX_PGS_LDS_ROWS 192   // rows per slot the main solver launch keeps in LDS (2 waves / CU in fp64)
 #define MGX_PGS_WIDE_GRID 256  // waves of the global-B launch (slots over MGX_PGS_LDS_ROWS, waves over their arena)
+#define MGX_PGS_WIDE_LDS_GRID 32  // waves of the wide launch with LDS-resident B (one slot per wave)
 #define MGX_PGS_ARENA_F64 49152  // LDS arena per main-launch solver wave of 4 slots, fp64 (tools/pgs_census.py)
 #define MGX_PGS_ARENA_F32 32768  //                                                    fp32
 enum { FIX_RESET = 2 };
@@ -49,6 +54,11 @@ struct Pipe {
   int capE;            // rows the main solver launch holds in LDS per slot; slots with more rows (up
                        // to maxE) go to the second, wide-LDS launch (o_k2big)
   int arena;           // LDS bytes of one main-launch solver wave (scalars + block table + B of its slots)
+  int sqg;             // soccer main launch: row scalars read from the pipe, forces only in LDS (capE > 192)
+  int warena;          // > 0: LDS bytes of the wide launch's one-slot waves, which solve a slot of
+                       // more than capE rows with its B, scalars and table copied into LDS (the
+                       // latency-bound chain of a heavy slot reads LDS instead of L2 / MALL)
+  size_t o_cpos;        // contact points of the row builder, 3 * maxC reals per slot (Layout.gcon)
   size_t o_carry, o_carryi, o_ne, o_blen, o_niter, o_k2list, o_k2big, o_ctr, o_fix, o_scal, o_blk, o_B, o_vout;
   // the main solver launch's slots by block count: o_hist[b] slots with b blocks (b = 1 .. nbk - 1),
   // listed in o_blist[b * S ..]; the launch takes them heaviest first (sorted_slot), so a wave's
@@ -60,7 +70,7 @@ struct Pipe {
   // the checkAcc template: mj_step's outcome after mj_resetData (state + forward frames)
   size_t o_tq, o_tv, o_ta, o_tt, o_tx, o_txq, o_tsc, o_tn, o_tcg, o_tcd, o_tcm;
   int maxC;
-  int tw;              // block-table words per 4-row block (8: nv <= 56, 16: nv <= 64)
+  int tw;              // block-table words per 4-row block (MGX_TW: B offset, 64-bit dof support)
   int nobs;            // floats of a bank's reset observation
   // RK4 staged step (mgx_rk_staged.h): per slot the stage carry (rk_stride reals: X0 positions,
   // the stage's positions, stage velocities / accelerations, t0 / t_k), its state in the step
@@ -74,17 +84,20 @@ struct Pipe {
   __device__ __forceinline__ int* ctr() const { return at<int>(o_ctr); }
 };
 
-// The row builder's carry tail (Layout.carry_lds): xfrc_applied and qMH of `slot` are read and
-// written in its pipe carry (global memory), where the finisher's load_carry picks them up.
+// The row builder's carry tail (Layout.carry_lds): con_mu, xfrc_applied and qMH of `slot` are read
+// and written in its pipe carry (global memory), where the finisher's load_carry picks them up;
+// the contact points (Layout.gcon) in the slot's o_cpos storage, read back by the row blocks.
 // Every Env bound with the row-builder layout binds its tail before first use (env_bind leaves
-// the two pointers null).
+// those pointers null).
 template <typename T>
 __device__ __forceinline__ void bind_carry_tail(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot) {
   if (m.L.carry_lds < m.L.carry_reals) {
     T* cr = P.at<T>(P.o_carry) + (size_t)slot * P.carry_stride;
     e.xfrc = cr + (m.L.xfrc - m.L.qpos);
     e.qMH = cr + (m.L.qMH - m.L.qpos);
+    e.con_mu = cr + (m.L.con_mu - m.L.qpos);
   }
+  if (m.L.gcon) e.con_pos = P.at<T>(P.o_cpos) + (size_t)slot * 3 * P.maxC;
 }
 
 // ------------------------------------------------------------------ S1 helpers
@@ -230,12 +243,13 @@ __device__ __forceinline__ double readlane_t(double x, int l) { return readlane(
 // B = D^-1/2 L'^-1 J' by a readlane sweep over the block's dof support only (the two bodies'
 // chains, closed under ancestors, highest dof first); then B.B and the block couplings A_ij,
 // the row scalars and B -> pipe.
-// TW: block-table words per 4-row block (the A offset, then one per 8-dof group): 8 for nv <= 56,
-// 16 for nv <= 64. C2: contacts 64..127 read their metadata from cm2 (lane c - 64).
-template <typename T, int TW = 8, bool C2 = false>
+// NCS: contact-metadata lane sets (contact c reads set c / 64, lane c % 64): 1 for up to 64
+// contacts, 3 for up to 192 (bipedal_rescue).
+template <typename T, int NCS = 1>
 __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, const Pipe& P, int r0, int nlim, int nlim4,
-                                            const ContactMeta<T>& cm, const ContactMeta<T>& cm2, T dinvs, T* scal,
-                                            int* blk, T* Bo, int& boff) {
+                                            const ContactMeta<T>& cm, const ContactMeta<T>& cm2,
+                                            const ContactMeta<T>& cm3, T dinvs, T* scal, uint32_t* blk, T* Bo,
+                                            int& boff) {
   const int l = lane_id();
   const int nv = m.nv;
   const bool dl = l < nv;
@@ -267,8 +281,8 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
     }
   } else {
     const int c = (r0 - nlim4) >> 2;
-    const ContactMeta<T>& cs = (C2 && c >= 64) ? cm2 : cm;
-    const int cl = C2 ? (c & 63) : c;
+    const ContactMeta<T>& cs = (NCS > 2 && c >= 128) ? cm3 : (NCS > 1 && c >= 64) ? cm2 : cm;
+    const int cl = c & 63;
     const int dim = readlane(cs.dim, cl), b1 = readlane(cs.b1, cl), b2 = readlane(cs.b2, cl);
     const int rt1 = readlane(cs.rt1, cl), rt2 = readlane(cs.rt2, cl);
     const uint64_t m1 = readlane_u64(cs.m1, cl), m2 = readlane_u64(cs.m2, cl);
@@ -374,30 +388,23 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
       o[MGX_SQ(0, 0)] = 0; o[MGX_SQ(1, 0)] = 0; o[MGX_SQ(2, 0)] = 1; o[MGX_SQ(3, 0)] = 1; o[MGX_SQ(4, 0)] = (T)0.5;
     }
   }
-  // the block for the solver: [A10 A20 A21 A30 A31 A32 0 0] then, for each 8-dof group the
-  // block's support touches (ascending), [8 dofs][4 rows] (a lane's 4 rows are one 16-byte
-  // load). The block table entry holds 8 uint16 offsets: the A offset, then per group g < 7
-  // its data offset, or the slot's zero group (offset 0, 32 zeros never written) when the
-  // block does not touch it: no index math or selects in the sweeps.
+  // the block for the solver: [A10 A20 A21 A30 A31 A32 0 0], then for each dof of the block's
+  // support (ascending) the dof's 4 rows [r0 r1 r2 r3] (one 16-byte load per 4 rows and dof in
+  // the solver). The table entry: [B offset, support lo, support hi, 0]. A dof outside the
+  // support has B = 0 exactly (the J build and the L'^-1 sweep touch the support only); the
+  // solver points it at the slot's zero area (offset 0, never written).
   {
-    uint32_t gm = 0;
-#pragma unroll
-    for (int g = 0; g < 8; g++) gm |= ((sup >> (8 * g)) & 0xffull) ? (1u << g) : 0u;
     T* o = Bo + boff;
     if (l < 8) o[l] = l == 0 ? a10 : l == 1 ? a20 : l == 2 ? a21 : l == 3 ? a30 : l == 4 ? a31 : l == 5 ? a32 : (T)0;
-    // every lane of a touched group stores, so a group that runs past nv (bipedal: dofs 56..62 and
-    // the phantom 63) carries zeros there, not the slot's stale data (j* are 0 on lanes >= nv)
-    const int g = l >> 3, jj = l & 7;
-    if ((gm >> g) & 1u) {
-      T* og = o + 8 + 32 * __popc(gm & ((1u << g) - 1u)) + 4 * jj;
-      og[0] = j0; og[1] = j1; og[2] = j2; og[3] = j3;
+    if ((sup >> l) & 1ull) {
+      T* od = o + 8 + 4 * __popcll(sup & ((1ull << l) - 1ull));
+      od[0] = j0; od[1] = j1; od[2] = j2; od[3] = j3;
     }
-    if (l < TW) {
-      uint16_t* bt = reinterpret_cast<uint16_t*>(blk) + TW * (r0 >> 2);
-      int v = l == 0 ? boff : (((gm >> (l - 1)) & 1u) ? boff + 8 + 32 * __popc(gm & ((1u << (l - 1)) - 1u)) : 0);
-      bt[l] = (uint16_t)v;
+    if (l < MGX_TW) {
+      uint32_t* bt = blk + MGX_TW * (r0 >> 2);
+      bt[l] = l == 0 ? (uint32_t)boff : l == 1 ? (uint32_t)sup : l == 2 ? (uint32_t)(sup >> 32) : 0u;
     }
-    boff += 8 + 32 * __popc(gm);
+    boff += 8 + 4 * __popcll(sup);
   }
   MGX_BSTAMP(11);
 }
@@ -405,7 +412,7 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
 // S1 body: forward up to the constraint rows, rows -> pipe, carry -> pipe
 // list_slot: enter the slot in the solver launches' lists (the pipeline); the one-wave settle
 // (settle_step) solves the slot itself.
-template <typename T, int TW = 8, bool C2 = false>
+template <typename T, int NCS = 1>
 __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot, int warn,
                                            bool list_slot = true) {
   int l = lane_id();
@@ -438,12 +445,12 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
   e.nefc = ne;
   MGX_STAMP(6);
   const bool dl = l < nv;
-  int boff = 32;  // B reals of the slot; [0, 32): the zero group
+  int boff = 32;  // B reals of the slot; [0, 32): the zero area (A and B of absent entries)
   if (ne > 0) {
     const T dinvs = dl ? sqrt(e.diaginv) : (T)0;
     T* scal = P.at<T>(P.o_scal) + (size_t)slot * P.maxE * MGX_SCAL;
     T* Bo = P.at<T>(P.o_B) + (size_t)slot * P.bcap;
-    int* blk = P.at<int>(P.o_blk) + (size_t)slot * (P.maxE * TW / 8);  // TW uint16 per 4-row block
+    uint32_t* blk = P.at<uint32_t>(P.o_blk) + (size_t)slot * (P.maxE / 4) * MGX_TW;
     const int nlim4 = (nlim + 3) & ~3;
     // qacc_smooth / qacc_warmstart into LDS (limit rows) and their per-body chain sums
     if (dl) { e.vec1[l] = e.qacc_smooth; e.vec2[l] = e.qacc_ws; }
@@ -466,13 +473,14 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
       wsync();
     }
     rows_impedance(m, e, ne, nlim, nlim4, scal);
-    ContactMeta<T> cm, cm2;
+    ContactMeta<T> cm, cm2, cm3;
     contact_meta(m, e, ncf, cm);
-    if constexpr (C2) contact_meta(m, e, ncf, cm2, 64);
+    if constexpr (NCS > 1) contact_meta(m, e, ncf, cm2, 64);
+    if constexpr (NCS > 2) contact_meta(m, e, ncf, cm3, 128);
     __threadfence();  // the row constants are read back by other lanes of this wave (build_block)
     wsync();
     for (int r0 = 0; r0 < ne; r0 += 4)
-      build_block<T, TW, C2>(m, e, P, r0, nlim, nlim4, cm, cm2, dinvs, scal, blk, Bo, boff);
+      build_block<T, NCS>(m, e, P, r0, nlim, nlim4, cm, cm2, cm3, dinvs, scal, blk, Bo, boff);
   }
   MGX_STAMP(7);
   // carry + registers + ints
@@ -578,14 +586,19 @@ struct PgsTab {
   uint32_t a, g[EPL];
 };
 
-template <int EPL, int LPS, int TW = 8>
+template <int EPL, int LPS>
 __device__ __forceinline__ void pgs_load_tab(PgsTab<EPL>& t, const uint32_t* bt, int blk, int j) {
-  const uint32_t* e = bt + TW * blk;  // widened in LDS: no 16-bit extracts on the address path
-  t.a = e[0];
+  // one 16-byte LDS load: [B offset, support lo, support hi, 0]; this lane's dof j + 8 gi of each
+  // register entry is at rank popc(support below it) of the block's dof list, or absent (zero area)
+  const uint4 e = *reinterpret_cast<const uint4*>(bt + MGX_TW * blk);
+  t.a = e.x;
+  const uint64_t sup = (uint64_t)e.y | ((uint64_t)e.z << 32);
 #pragma unroll
   for (int d = 0; d < EPL; d++) {
-    const int gi = d * (LPS / 8) + (j >> 3);
-    t.g[d] = gi < TW - 1 ? e[1 + gi] : 0u;
+    const int dof = 8 * (d * (LPS / 8) + (j >> 3)) + (j & 7);
+    const uint64_t below = dof >= 64 ? sup : sup & ((1ull << dof) - 1ull);
+    const bool in = dof < 64 && ((sup >> (dof & 63)) & 1ull);
+    t.g[d] = in ? e.x + 8u + 4u * (uint32_t)__popcll(below) : 0u;
   }
 }
 
@@ -609,7 +622,7 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.a0 = pa[0];
   k.a1 = pa[1];
 #pragma unroll
-  for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t.g[d] + 4 * (j & 7));
+  for (int d = 0; d < EPL; d++) k.b[d] = *reinterpret_cast<const V4*>(Bsl + t.g[d]);
   const V4* q = reinterpret_cast<const V4*>(sq + 4 * MGX_SCAL * sblk);
   k.qb = q[0];
   k.qf = *reinterpret_cast<const V4*>(fb + FS * blk);
@@ -618,11 +631,11 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.qh = q[4];
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
 }
-template <typename T, int EPL, int LPS, int FS, int TW = 8>
+template <typename T, int EPL, int LPS, int FS>
 __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sq, const T* fb,
                                                const uint32_t* bt, int blk, int sblk, int j) {
   PgsTab<EPL> t;
-  pgs_load_tab<EPL, LPS, TW>(t, bt, blk, j);
+  pgs_load_tab<EPL, LPS>(t, bt, blk, j);
   pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, t, blk, sblk, j);
 }
 
@@ -708,9 +721,9 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
 // otherwise hold the launch to two waves per CU; bipedal 175.0k -> 186.6k env-steps/s); the
 // soccer launch keeps all scalars in LDS at four waves per CU, which measured faster than the
 // global scalars at any occupancy (MGX_PGS_LDS_PAD sweep).
-template <typename T, int EPL, int LPS, bool BLDS, int TW = 8, bool SQG = (TW > 8)>
+template <typename T, int EPL, int LPS, bool BLDS, bool SQG = false>
 __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, int capE, int maxit, T tol, T scale,
-                                          int spw) {
+                                          int spw, int arena = -1) {
   constexpr int RING = BLDS ? MGX_PGS_RING_LDS : MGX_PGS_RING;
   typedef typename Vec4T<T>::type V4;
   constexpr int SPW = 64 / LPS;
@@ -729,7 +742,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   const int nbRun = (nbMax + RING - 1) / RING * RING;
   const size_t sl = (size_t)(slot >= 0 ? slot : 0);
   const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
-  const uint16_t* gbt = reinterpret_cast<const uint16_t*>(P.at<int>(P.o_blk) + sl * (P.maxE * TW / 8));
+  const uint32_t* gbt = P.at<uint32_t>(P.o_blk) + sl * (P.maxE / 4) * MGX_TW;
   const T* gB = P.at<T>(P.o_B) + sl * P.bcap;
   int nbA;  // blocks of scalars / table entries per slot (the look-ahead stays inside)
   T* sc;
@@ -744,21 +757,31 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   if constexpr (BLDS) {
     nbA = nbRun + RING - 1;
     const int blen = slot >= 0 ? (P.at<int>(P.o_blen)[slot] + 3) & ~3 : 0;
-    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 4 * TW) + blen * (int)sizeof(T);  // 16-byte multiple
+    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 4 * MGX_TW) + blen * (int)sizeof(T);  // 16-byte multiple
     int off = 0, tot = 0;
+    if (arena < 0) {
+      // main launch: the wave's slots side by side
 #pragma unroll
-    for (int q = 0; q < SPW; q++) {
-      const int bq = __shfl(bytes, q * LPS);
-      off += q < s ? bq : 0;
-      tot += bq;
+      for (int q = 0; q < SPW; q++) {
+        const int bq = __shfl(bytes, q * LPS);
+        off += q < s ? bq : 0;
+        tot += bq;
+      }
+    } else {
+      // wide launch: every lane group of the wave runs the wave's one slot on one shared copy
+      // (identical values to identical addresses; the slot's arithmetic is the lane group's)
+      tot = bytes;
     }
-    if (__builtin_amdgcn_readfirstlane(tot) > P.arena) {
-      if (j == 0 && slot >= 0) P.at<int>(P.o_k2big)[atomicAdd(P.ctr() + 2, 1)] = slot;
+    if (__builtin_amdgcn_readfirstlane(tot) > (arena < 0 ? P.arena : arena)) {
+      // main launch: the wide launch takes the wave's slots. The wide launch's own arena
+      // (arena >= 0, P.warena) holds any one slot by construction (make_staged_pipe), so it never
+      // lands here
+      if (arena < 0 && j == 0 && slot >= 0) P.at<int>(P.o_k2big)[atomicAdd(P.ctr() + 2, 1)] = slot;
       return;
     }
     sc = reinterpret_cast<T*>(smem + off);
     bt = reinterpret_cast<uint32_t*>(sc + 4 * MGX_SCAL * nbA);
-    T* Bs = reinterpret_cast<T*>(bt + TW * nbA);
+    T* Bs = reinterpret_cast<T*>(bt + MGX_TW * nbA);
     for (int q = 4 * j; q < blen; q += 4 * LPS)
       *reinterpret_cast<V4*>(Bs + q) = *reinterpret_cast<const V4*>(gB + q);
     Bsl = Bs;
@@ -771,7 +794,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     nbA = (nbcap + RING - 1) / RING * RING;
     const int sstride = (SG ? 4 : 4 * MGX_SCAL) * nbA + 4;  // 16-byte aligned per slot
     sc = reinterpret_cast<T*>(smem) + s * sstride;
-    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * TW * nbA;
+    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * MGX_TW * nbA;
     Bsl = gB;
     if constexpr (SG) {
       sq = gsc;
@@ -786,7 +809,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   // scalar blocks past the slot's capacity are never real (masked); their loads stay inside it
   const int sbmax = P.maxE / 4 - 1;
   // block table: the slot's blocks, then zero-group entries up to the capacity
-  for (int q = j; q < TW * nbA; q += LPS) bt[q] = q < TW * nblk ? (uint32_t)gbt[q] : 0u;
+  for (int q = j; q < MGX_TW * nbA; q += LPS) bt[q] = q < MGX_TW * nblk ? gbt[q] : 0u;
   __syncthreads();
   // warmstart: v = B' f, dual cost, reset to zero if the cost is positive
   T v[EPL];
@@ -794,7 +817,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   for (int d = 0; d < EPL; d++) v[d] = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS, FS, TW>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
+    pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
     const T* qf = fb + FS * b;
     bool ok = b < nblk;
     T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[1] : (T)0, f2 = ok ? qf[2] : (T)0, f3 = ok ? qf[3] : (T)0;
@@ -803,7 +826,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   T cpart = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS, FS, TW>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
+    pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
     T d0, d1, d2, d3;
     pgs_dots(k, v, d0, d1, d2, d3);
     slot_sum4<LPS>(d0, d1, d2, d3);
@@ -839,11 +862,11 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     T impr = 0;
     PgsBlk<T, EPL> R[RING];
     PgsTab<EPL> tn;  // the table entry of the next block to load (one ring step ahead of its data)
-    pgs_load_tab<EPL, LPS, TW>(tn, bt, 0, j);
+    pgs_load_tab<EPL, LPS>(tn, bt, 0, j);
 #pragma unroll
     for (int k = 0; k < RING - 1; k++) {
       pgs_load_block<T, EPL, LPS, FS>(R[k], Bsl, sq, fb, tn, k, min(k, sbmax), j);
-      pgs_load_tab<EPL, LPS, TW>(tn, bt, k + 1, j);
+      pgs_load_tab<EPL, LPS>(tn, bt, k + 1, j);
     }
     // full ring turns, no early exit inside, so every prefetch is consumed on every path and
     // the compiler cannot sink the loads next to their use. The table has zero entries up to
@@ -854,7 +877,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
         // the slot consumed last lands the block RING - 1 ahead, then block b0 + k is solved
         const int bn = min(b0 + k + RING - 1, nbA - 1);
         pgs_load_block<T, EPL, LPS, FS>(R[(k + RING - 1) % RING], Bsl, sq, fb, tn, bn, min(bn, sbmax), j);
-        pgs_load_tab<EPL, LPS, TW>(tn, bt, min(bn + 1, nbA - 1), j);
+        pgs_load_tab<EPL, LPS>(tn, bt, min(bn + 1, nbA - 1), j);
         pgs_block<T, EPL, LPS>(R[k], v, fb + FS * (b0 + k), act && b0 + k < nblk, impr);
       }
     }
@@ -923,7 +946,7 @@ __device__ __forceinline__ int sorted_slot(const Pipe& P, int idx, int LPS) {
   return slot;
 }
 
-template <typename T, int EPL, int LPS, bool BLDS, int TW = 8>
+template <typename T, int EPL, int LPS, bool BLDS, bool SQG = false>
 __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw, int big) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (!big && blockIdx.x == 0 && threadIdx.x == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
@@ -934,10 +957,12 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   // the wide launch's few long chains (slots over the main launch's rows) run beside the whole
   // main launch and end the step when they trail it: they take their SIMD first
   if (big) __builtin_amdgcn_s_setprio(3);
+  const bool dup = big && BLDS;  // the wide LDS-B launch: one slot per wave, every lane group on it
   for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
-    const int idx = (s < spn && base + s < cnt) ? base + s : -1;
+    const int idx = dup ? base : (s < spn && base + s < cnt) ? base + s : -1;
     const int slot = big ? (idx >= 0 ? list[idx] : -1) : sorted_slot(P, idx, LPS);
-    pgs_group<T, EPL, LPS, BLDS && true, TW>(P, smem, slot, big ? P.maxE : P.capE, maxit, tol, scale, spw);
+    pgs_group<T, EPL, LPS, BLDS && true, SQG>(P, smem, slot, big ? P.maxE : P.capE, maxit, tol, scale, spw,
+                                                  big ? P.warena : -1);
     __syncthreads();  // the next group reuses the LDS
   }
 }

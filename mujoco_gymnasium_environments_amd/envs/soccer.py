@@ -43,11 +43,12 @@ REGISTERED_MAX_EPISODE_STEPS = 2500  # humanoid_soccer_env/__init__.py:21 (TimeL
 
 
 # Contact / row capacity. MuJoCo allocates contacts from its arena and keeps them all. The
-# default staged step holds 64 contacts / 192 rows per env and counts the rare env step beyond
-# it (mgx_state.overflow, MuJoCo's mjWARN_CONTACTFULL / CNSTRFULL semantics: drop in row
-# order); full_capacity=True holds 96 contacts / 384 rows — no overflow at bench conditions —
-# with the slots over 192 rows solved by the staged pipeline's wide-LDS launch, at a measured
-# throughput cost (Capacity).
+# staged step (the default) holds 96 contacts / 384 rows per env — no overflow at bench
+# conditions (measured maximum ~230 rows) — so the timed path computes mj_step's physics on every
+# env step. full_capacity=False keeps the round-1 capacity of 64 contacts / 192 rows and counts
+# the rare env step beyond it (mgx_state.overflow, MuJoCo's mjWARN_CONTACTFULL / CNSTRFULL
+# semantics: drop in row order); the monolithic kernel (staged=False) always holds 64 / 192
+# (Capacity).
 CON_CAPACITY = 96
 EFC_CAPACITY = 384
 
@@ -133,12 +134,14 @@ class SoccerVectorEnv:
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
-                 staged: bool = True, banks: int = 3, full_capacity: bool = False):
+                 staged: bool = True, banks: int = 3, full_capacity: Optional[bool] = None):
         """``staged`` selects the row-builder / lane-group PGS / finisher kernels
         with ``banks`` precomputed resets per env; ``staged=False`` runs one monolithic wave per
         env. Both compute the same step (parity-tested against each other and the oracle).
-        ``full_capacity`` raises the staged step's capacity from 64 contacts / 192 rows to
-        96 / 384 (see soccer_model)."""
+        ``full_capacity`` (default: the staged step's) holds 96 contacts / 384 rows instead of
+        64 / 192 (see soccer_model)."""
+        if full_capacity is None:
+            full_capacity = staged
         if full_capacity and not staged:
             # the monolithic layout holds 64 contacts / 192 rows whatever the model's capacity
             raise ValueError("full_capacity needs the staged pipeline (staged=True)")

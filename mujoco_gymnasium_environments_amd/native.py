@@ -13,7 +13,8 @@ from . import cabi
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libmgx.so")
+# MGX_LIB: load another build of the same sources (A/B measurements of a kernel variant)
+LIB_PATH = os.environ.get("MGX_LIB") or os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
 SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_rk_staged.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip",
            "mgx_dancing.hip",

@@ -44,6 +44,10 @@ struct ref_data {
   int *solver_niter;
   /* scratch */
   double *scratch;
+  /* test knob (ref_set_pgs_order): 1 sums each PGS residual b + sum_c AR_rc f_c in reverse
+     column order. The same algorithm with a different fp64 rounding: a twin that measures how
+     fast two fp64 implementations of the unconverged 50-sweep solve separate on a trajectory */
+  int pgs_reverse;
 };
 
 /* ====================================================================== vector helpers */
@@ -147,6 +151,8 @@ ref_data *ref_create(const mgx_model_desc *m, int ncon_max, int nefc_max) {
   ref_reset(m, d);
   return d;
 }
+
+void ref_set_pgs_order(ref_data *d, int reverse) { d->pgs_reverse = reverse != 0; }
 
 void ref_free(ref_data *d) {
   if (!d) return;
@@ -1614,7 +1620,10 @@ static void fwd_constraint(const mgx_model_desc *m, ref_data *d) {
     for (int r = 0; r < ne; r++) {
       const double *Ar = d->efc_AR + (size_t)r * ne;
       double res = d->efc_b[r];
-      for (int c = 0; c < ne; c++) res += Ar[c] * d->efc_force[c];
+      if (d->pgs_reverse)
+        for (int c = ne - 1; c >= 0; c--) res += Ar[c] * d->efc_force[c];
+      else
+        for (int c = 0; c < ne; c++) res += Ar[c] * d->efc_force[c];
       double Arr = Ar[r], old = d->efc_force[r];
       double f = old - res / Arr;
       if (d->efc_type[r] >= C_LIMIT_JOINT && f < 0) f = 0;

@@ -32,6 +32,8 @@ void ref_free(ref_data *d);
 void ref_reset(const mgx_model_desc *m, ref_data *d);       /* mj_resetData */
 void ref_forward(const mgx_model_desc *m, ref_data *d);     /* mj_forward */
 void ref_step(const mgx_model_desc *m, ref_data *d);        /* mj_step */
+/* test knob: 1 = sum each PGS residual in reverse column order (a different-rounding twin) */
+void ref_set_pgs_order(ref_data *d, int reverse);
 /* pointer + element count of a named field ("qpos", "xpos", "efc_J", "ncon", ...) */
 void *ref_field(ref_data *d, const char *name, int *count);
 

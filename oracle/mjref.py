@@ -42,6 +42,7 @@ def lib():
         _lib.ref_collide_pair.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         _lib.ref_collide_pair.restype = C.c_int
         _lib.ref_narrowphase_stats.argtypes = [C.POINTER(C.c_long), C.c_int]
+        _lib.ref_set_pgs_order.argtypes = [C.c_void_p, C.c_int]
     return _lib
 
 
@@ -82,6 +83,11 @@ class RefSim:
         if name in ("packed", "m", "L", "d"):
             raise AttributeError(name)
         return self.field(name)
+
+    def set_pgs_reverse(self, reverse: bool = True):
+        """Twin knob: sum each PGS residual in reverse column order (same algorithm, other
+        fp64 rounding; mjref.c ref_set_pgs_order)."""
+        self.L.ref_set_pgs_order(self.d, 1 if reverse else 0)
 
     def reset(self):
         self.L.ref_reset(C.addressof(self.packed.desc), self.d)

@@ -1,13 +1,14 @@
 """GPU: contact / row capacity of the staged soccer step (MuJoCo keeps every contact: its arena
 has no 64-contact / 192-row cap).
 
-With full_capacity=True the staged step stores up to EFC_CAPACITY = 384 rows / 96 contacts per
-env (the default keeps 192 / 64 and counts the overflow). Its main solver
-launch holds MGX_PGS_LDS_ROWS = 192 rows per slot in LDS; a slot with more rows is listed for a
-second, wide-LDS launch instead of being truncated. The test hook MGX_PGS_LDS_ROWS lowers that
-threshold (read per step), so ordinary bench-condition states — 40..120 rows — take the wide
-launch on every step:
-  * bit-identical to the default launch split (which launch solves a slot changes nothing);
+The staged step (the default SoccerVectorEnv) stores up to EFC_CAPACITY = 384 rows / 96 contacts
+per env; full_capacity=False keeps 192 / 64 and counts the overflow. Its main
+solver launch solves every slot (row scalars read from the pipe, make_staged_pipe `sqg`); the
+test hook MGX_PGS_LDS_ROWS instead gives the main launch that many LDS-scalar rows per slot and
+lists a slot with more for the wide launch (B, scalars and table in LDS, one slot per wave)
+instead of truncating it. Read per step, a low value sends ordinary bench-condition states —
+40..120 rows — through the wide launch on every step:
+  * bit-identical to the default launch (which launch solves a slot changes nothing);
   * fp64 end to end against the oracle (no cap) with every slot over the lowered threshold;
   * MGX_MAX_NEFC below a state's rows still truncates in MuJoCo's row order and counts the step
     in mgx_state.overflow (the documented behaviour past the storage capacity).

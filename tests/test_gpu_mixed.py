@@ -1,9 +1,11 @@
-"""GPU: BASELINE configs[4] — every built task stepping concurrently, one HIP stream per task.
+"""GPU: BASELINE configs[4] — every built task stepping concurrently, in the bench's layout.
 
 The mixed run overlaps all seven task kernels with different models (nv 29..99: construction on
-the wide two-dofs-per-lane kernels, ragged contact and row counts, fp32 and fp64, rows in LDS or
-in global scratch) on one GPU. Each task's outputs must be
-bit-identical to the same task stepped alone on the default stream with the same seeds and
+the wide two-dofs-per-lane kernels, ragged contact and row counts, rows in LDS or in global
+scratch) on one GPU, in the configuration `bench.py --task mixed` times: every task in fp64, the
+four grouped HIP streams of bench.mixed_streams with construction's at high priority and no side
+streams (and, as a second case, one stream per task with side streams). Each task's outputs must
+be bit-identical to the same task stepped alone on the default stream with the same seeds and
 actions: concurrency changes nothing but the schedule. Per-task parity with the CPU oracle is
 covered by the task's own test file.
 """
@@ -31,24 +33,24 @@ def _tasks():
     alo = torch.tensor([-2.0] * 7 + [0.0, 0.0], device=dev)
     alim = torch.tensor([4.0] * 7 + [100.0, 50.0], device=dev)
     acts = {
-        "soccer": [torch.rand(N, 33, device=dev, generator=g) * 300 - 150 for _ in range(STEPS)],
-        "parkour": [(torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim for _ in range(STEPS)],
-        "bipedal": [(torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0 for _ in range(STEPS)],
-        "dancing": [(torch.rand(N, 29, device=dev, generator=g) * 2 - 1) * 200.0 for _ in range(STEPS)],
-        "martial": [torch.rand(N, 28, device=dev, generator=g) * 2 - 1 for _ in range(STEPS)],
-        "assembly": [torch.rand(N, 9, device=dev, generator=g) * alim + alo for _ in range(STEPS)],
-        "construction": [(torch.rand(N, 33, device=dev, generator=g) * 2 - 1) * 200.0 for _ in range(STEPS)],
+        "humanoid_soccer": [torch.rand(N, 33, device=dev, generator=g) * 300 - 150 for _ in range(STEPS)],
+        "quadruped_parkour": [(torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim for _ in range(STEPS)],
+        "bipedal_rescue": [(torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0 for _ in range(STEPS)],
+        "humanoid_dancing": [(torch.rand(N, 29, device=dev, generator=g) * 2 - 1) * 200.0 for _ in range(STEPS)],
+        "humanoid_martial_arts": [torch.rand(N, 28, device=dev, generator=g) * 2 - 1 for _ in range(STEPS)],
+        "robotic_arm_assembly": [torch.rand(N, 9, device=dev, generator=g) * alim + alo for _ in range(STEPS)],
+        "humanoid_construction": [(torch.rand(N, 33, device=dev, generator=g) * 2 - 1) * 200.0 for _ in range(STEPS)],
     }
 
     def make():
         return {
-            "soccer": SoccerVectorEnv(N, precision="f32", seed=11),
-            "parkour": ParkourVectorEnv(N, precision="f32", seed=12),
-            "bipedal": BipedalVectorEnv(N, precision="f32", seed=13),
-            "dancing": DancingVectorEnv(N, precision="f32", seed=14),
-            "martial": MartialArtsVectorEnv(N, precision="f32", seed=15),
-            "assembly": AssemblyVectorEnv(N, precision="f64"),
-            "construction": ConstructionVectorEnv(N, precision="f64", seed=16),
+            "humanoid_soccer": SoccerVectorEnv(N, precision="f64", seed=11),
+            "quadruped_parkour": ParkourVectorEnv(N, precision="f64", seed=12),
+            "bipedal_rescue": BipedalVectorEnv(N, precision="f64", seed=13),
+            "humanoid_dancing": DancingVectorEnv(N, precision="f64", seed=14),
+            "humanoid_martial_arts": MartialArtsVectorEnv(N, precision="f64", seed=15),
+            "robotic_arm_assembly": AssemblyVectorEnv(N, precision="f64"),
+            "humanoid_construction": ConstructionVectorEnv(N, precision="f64", seed=16),
         }
     return make, {k: [a.contiguous() for a in v] for k, v in acts.items()}
 
@@ -78,11 +80,18 @@ def _same(a, b):
     return torch.equal(a, b)
 
 
-def test_mixed_streams_equal_sequential():
+@pytest.mark.parametrize("layout", ["bench", "stream_per_task"])
+def test_mixed_streams_equal_sequential(layout, monkeypatch):
+    """layout "bench": bench.py's default (4 grouped streams, construction's at high priority, no
+    side streams); "stream_per_task": 7 streams, the staged tasks' side streams on."""
+    import bench
+    # side streams on for the sequential run; bench.mixed_streams turns them off for the bench
+    # layout (monkeypatch restores the variable after the test)
+    monkeypatch.setenv("MGX_SIDE_STREAM", "1")
     make, acts = _tasks()
     seq = _run(make(), acts)
     envs = make()
-    streams = {k: torch.cuda.Stream() for k in envs}
+    streams = bench.mixed_streams(list(envs), 4 if layout == "bench" else len(envs), 1, torch.device("cuda:0"))
     con = _run(envs, acts, streams)
     for k in seq:
         for t in range(STEPS):

@@ -32,7 +32,8 @@ for k in range(4):
     W = a.workspace
     rk = W[o_rk:o_rk + S * stride * rb].view(torch.float64).reshape(S, stride).cpu().numpy()
     Bw = W[o_B:o_B + S * bcap * rb].view(torch.float64).reshape(S, bcap).cpu().numpy()
-    tab = W[o_blk:o_blk + S * maxE * 8].view(torch.int16).reshape(S, maxE // 4, 16).cpu().numpy().astype(np.int64) & 0xFFFF
+    # block table (mgx_staged.h MGX_TW): [B offset, dof support lo, hi, 0] per 4-row block
+    tab = W[o_blk:o_blk + S * maxE * 4].view(torch.int32).reshape(S, maxE // 4, 4).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
     ne_s = W[o_ne:o_ne + 4 * S].view(torch.int32).cpu().numpy()
     ctrl = a.batch.ctrl.cpu().numpy()
     for i in range(n):
@@ -54,9 +55,10 @@ for k in range(4):
         Bs = np.zeros((ns, 64))
         for blk in range(ns // 4):
             t = tab[i, blk]
-            for g in range(8):
-                off = t[1 + g]
-                Bs[4 * blk:4 * blk + 4, 8 * g:8 * g + 8] = Bw[i, off:off + 32].reshape(8, 4).T
+            sup = int(t[1]) | (int(t[2]) << 32)
+            dofs = [d for d in range(64) if (sup >> d) & 1]
+            for r, d in enumerate(dofs):  # dof d's 4 rows after the block's 8 couplings
+                Bs[4 * blk:4 * blk + 4, d] = Bw[i, t[0] + 8 + 4 * r:t[0] + 12 + 4 * r]
         # staged row index of each oracle row
         idx = list(range(nlim)) + [nlim4 + q for q in range(4 * ncon)]
         A_s = (Bs @ Bs.T)[np.ix_(idx, idx)]

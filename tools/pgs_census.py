@@ -52,13 +52,15 @@ def main():
         spilled.append(gb)
         lst = ws[o_list:o_list + 4 * cnt].view(torch.int32).cpu().numpy()
         ne = ws[o_ne:o_ne + 4 * S].view(torch.int32).cpu().numpy()
-        blk = ws[o_blk:o_blk + 4 * S * maxE].view(torch.int16).cpu().numpy().view(np.uint16).reshape(S, maxE * 2)
+        # block table (mgx_staged.h MGX_TW): [B offset, dof support lo, hi, 0] per 4-row block
+        blk = ws[o_blk:o_blk + 4 * S * maxE].view(torch.int32).cpu().numpy().view(np.uint32).reshape(S, maxE)
         cnts.append(cnt)
         per = []
         for s in lst:
             nb = ne[s] // 4
-            t = blk[s, :8 * nb].reshape(nb, 8).astype(np.int64)
-            end = max(int((t[:, 0] + 8).max()), int((t[:, 1:] + 32).max())) if nb else 32
+            t = blk[s, :4 * nb].reshape(nb, 4).astype(np.int64)
+            ndof = [bin(int(a) | (int(b) << 32)).count("1") for a, b in zip(t[:, 1], t[:, 2])]
+            end = int((t[:, 0] + 8 + 4 * np.array(ndof)).max()) if nb else 32
             per.append((ne[s], nb, end * rb))
         per = np.array(per)
         rows += list(per[:, 0]); blocks += list(per[:, 1]); bbytes += list(per[:, 2])
@@ -68,7 +70,7 @@ def main():
             # the main launch's arena need (mgx_staged.h pgs_group<BLDS>): per slot the row
             # scalars + table for the wave's block count (ring 2) and the slot's B
             nbA = (p[:, 1].max() + 1) // 2 * 2 + 1
-            need = len(p) * nbA * (20 * rb + 32) + int(((p[:, 2] // rb + 3) // 4 * 4).sum()) * rb
+            need = len(p) * nbA * (20 * rb + 16) + int(((p[:, 2] // rb + 3) // 4 * 4).sum()) * rb
             wave_need.setdefault("all", []).append(need)
     q = lambda x: {k: float(np.percentile(x, k)) for k in (10, 50, 90, 99, 100)} | {"mean": float(np.mean(x))}
     print(json.dumps({"precision": a.precision, "envs": a.envs, "steps": a.steps, "slots_listed_mean": float(np.mean(cnts)),
