@@ -14,7 +14,7 @@ synthetic U(-150, 150)^33 float32 drawn before the timed region and resident in 
 Ranks shard envs (global index = rank * envs + i); the only collective is the end-of-rollout
 metric all-reduce over RCCL. Rank 0 prints ONE JSON line.
 
---task parkour benchmarks BASELINE configs[1] instead (quadruped_parkour, 4096 envs/GPU): one
+--task parkour benchmarks BASELINE configs[1] instead (quadruped_parkour, 4096 envs/GPU, staged per substep; --mono: one wave per env): one
 step = ParkourVectorEnv.step = mgx_parkour_step (clip, 10 mj_step's of 1 ms, obstacle motors,
 obs/reward/termination, same-step autoreset), actions U(-lim, lim) per joint (80/80/60/40).
 
@@ -581,7 +581,7 @@ def main():
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
                                                           "construction"])
     args = ap.parse_args()
-    if args.task not in ("soccer", "bipedal"):
+    if args.task not in ("soccer", "bipedal", "parkour"):
         args.mono = True  # one fused wave-per-env launch per step
     if args.precision is None:
         args.precision = "f64"
@@ -606,7 +606,8 @@ def main():
     g.manual_seed(1000 + rank)
     if args.task == "parkour":
         from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv, action_limits
-        env = ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N))
+        env = ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=1234, env_offset=env_offset(rank, N),
+                               staged=not args.mono, banks=min(args.banks, 1) if args.banks > 0 else 0)
         lim = torch.as_tensor(action_limits(), dtype=torch.float32, device=dev)
         pool = [((torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * lim).contiguous() for _ in range(16)]
     elif args.task == "bipedal":
@@ -750,13 +751,17 @@ def main():
             "data": "synthetic (U(-lim,lim) actions per joint, Philox reset draws)",
             "config": {"workload": "quadruped_parkour_env, 4096 envs/GPU (BASELINE configs[1])", "envs_per_gpu": N,
                        "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
-                       "substeps_per_step": 10, "step_kernels": "mono", "episodes_started": int(acc[1].item()),
+                       "substeps_per_step": 10, "step_kernels": "mono" if args.mono else "staged",
+                       "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": _pmc_traffic(PMC_PROFILE_PARKOUR, N, args.precision, "mono"),
-                         "kernel": "mgx_parkour_step = k_parkour<float,0>", "alg_bytes_per_step": bytes_per_launch,
+                         "traffic": _pmc_traffic(PMC_PROFILE_PARKOUR, N, args.precision, "mono" if args.mono else "staged"),
+                         "kernel": ("mgx_parkour_step = k_parkour<T,0,GB>" if args.mono else
+                                    "mgx_parkour_step = 10 x (k_pk_rows + k_pgs_groups + k_pk_bank_finish + k_pk_finish)"
+                                    " + k_pk_settle (fixups)"),
+                         "alg_bytes_per_step": bytes_per_launch,
                          "launch_ms": round(launch_ms, 4)},
         }
         if not args.no_cpu_baseline:

@@ -260,9 +260,22 @@ typedef struct mgx_parkour_env {
   int32_t *episode;         /* [N]     episodes started (keys the device reset draws); nullable
                                        when every reset passes host draws */
   void *rollout;            /* [N][4]  reward, terminated, truncated, env steps (nullable) */
+  void *workspace;          /* nullable: staged-step workspace (mgx_parkour_workspace_bytes), bound to
+                               (model, N, banks); NULL = one wave per env for the whole env step */
+  uint64_t workspace_bytes;
+  int32_t banks;            /* reset banks per env of the staged step (1 covers every autoreset) */
+  int32_t pad0;
 } mgx_parkour_env;
 
 int mgx_parkour_configure(mgx_model *m, const mgx_parkour_ids *ids);
+
+/* Staged parkour step (replaces parkour_env.py:356-394's frame_skip loop, the reference's
+ * `for _ in range(10): mujoco.mj_step`): per physics substep a row builder, the lane-group PGS of
+ * mgx_soccer_step and a finisher, the task logic after substep 10, reset banks settled as extra
+ * slots. Workspace bytes for (model, N, banks) and its one-time initialisation; pass it in
+ * mgx_parkour_env.workspace to select the staged step in mgx_parkour_step / mgx_parkour_reset. */
+int64_t mgx_parkour_workspace_bytes(const mgx_model *m, int n_env, int banks);
+int mgx_parkour_workspace_init(const mgx_model *m, void *workspace, uint64_t bytes, int n_env, int banks, void *stream);
 
 /* One env step for N envs (parkour_env.py:356-394): action clip, ctrl[:16], 10 mj_step's,
  * obstacle motors, observation [N][95] float32, reward [N] float64, terminated/truncated.

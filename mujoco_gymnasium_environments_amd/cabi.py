@@ -103,7 +103,8 @@ class MgxParkourIds(C.Structure):
 class MgxParkourEnv(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ["last_position", "max_progress", "episode_reward", "er_kind", "reached", "fall_count", "stuck",
-                 "step", "episode", "rollout"]]
+                 "step", "episode", "rollout"]] + \
+               [("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32), ("pad0", C.c_int32)]
 
 
 class MgxParkourLogicIO(C.Structure):

@@ -371,8 +371,11 @@ Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon,
   const int nlist = std::max(max_active, ecap);
   L.geom_xpos = R; L.geom_xmat = L.geom_xpos + a(3 * ng);
   L.con_frame = L.geom_xmat + a(9 * ng);
-  L.gcon = 1; L.con_pos = 0;  // the contact points live in the pipe (Pipe.o_cpos)
-  L.act_union = L.con_frame + a(3 * max_ncon);
+  // the contact points live in the pipe (Pipe.o_cpos) unless MGX_GCON=0 (A/B: in phase C's LDS)
+  static const int gcon = getenv("MGX_GCON") ? atoi(getenv("MGX_GCON")) : 1;
+  L.gcon = gcon;
+  L.con_pos = gcon ? 0 : L.con_frame + a(3 * max_ncon);
+  L.act_union = L.con_frame + a(3 * max_ncon) + (gcon ? 0 : a(3 * max_ncon));
   const int endC = L.act_union + a((nlist * 4 + real_bytes - 1) / real_bytes);
   // phase D: cacc (12 per body) over the geom poses when they cover it, else after phase C
   L.cacc = a(12 * nb) <= L.con_frame - R ? R : endC;
@@ -543,7 +546,7 @@ static int wide_arena_bytes(const mgx_model* m) {
   const int nbRun = (maxE / 4 + MGX_PGS_RING_LDS - 1) / MGX_PGS_RING_LDS * MGX_PGS_RING_LDS;
   const int nbA = nbRun + MGX_PGS_RING_LDS - 1;
   const int bcap = 32 + (maxE / 4) * (8 + 32 * ((nv + 7) / 8));
-  const int worst = nbA * (4 * MGX_SCAL * rb + 4 * MGX_TW) + ((bcap + 3) & ~3) * rb;
+  const int worst = nbA * (4 * MGX_SCAL * rb + 4 * mgx_twl(false)) + ((bcap + 3) & ~3) * rb;
   return wide_lds && pgs_lanes() == 16 && worst + 64 <= 160 * 1024 ? (worst + 15) & ~15 : 0;
 }
 
@@ -569,16 +572,24 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
     if (capE < 4) capE = 256;
   }
   p.capE = p.maxE < capE ? p.maxE : capE;
-  // soccer at full capacity (more rows than the 192 the LDS-scalar main launch holds at four waves
-  // per CU): one main launch over every slot with its row scalars read from the pipe and only the
-  // forces in LDS (pgs_group SQG), so a slot of 200+ rows is solved in the heaviest-first main
-  // launch instead of a trailing wide launch. MGX_PGS_SPLIT=1 (A/B) or the MGX_PGS_LDS_ROWS test
-  // hook keep the split: 192 LDS-scalar rows in the main launch, the rest in the wide launch.
-  static const int split = getenv("MGX_PGS_SPLIT") ? atoi(getenv("MGX_PGS_SPLIT")) : 0;
+  // soccer at full capacity (more rows than MGX_PGS_LDS_ROWS): the main launch keeps as many rows
+  // of LDS row scalars per slot as four waves per CU allow (fp64: 224), the wide launch beside it
+  // solves the rare slot beyond that with its B in LDS (measured, one box: 1.554M env-steps/s
+  // against 1.460M for one main launch over every slot with its row scalars read from the pipe at
+  // six waves per CU, 1.534M for that launch held to four; reduced capacity 1.647M).
+  // MGX_PGS_SINGLE=1 selects the single main launch (A/B); the MGX_PGS_LDS_ROWS test hook sets the
+  // main launch's rows directly.
+  static const int single = getenv("MGX_PGS_SINGLE") ? atoi(getenv("MGX_PGS_SINGLE")) : 0;
   p.sqg = 0;
-  if (!rk && !cap_env && !split && !pgs_lds_b() && p.maxE > MGX_PGS_LDS_ROWS) {
-    p.capE = p.maxE;
-    p.sqg = 1;
+  if (!rk && !cap_env && !pgs_lds_b() && p.maxE > MGX_PGS_LDS_ROWS) {
+    if (single) {
+      p.capE = p.maxE;
+      p.sqg = 1;
+    } else {
+      int r = MGX_PGS_LDS_ROWS;
+      while (r + 8 <= p.maxE && staged_pgs_lds_bytes(m, r + 8, pgs_lanes(), 0, mgx_twl(false)) <= 160 * 1024 / 4) r += 8;
+      p.capE = r;
+    }
   }
   // the wide launch (slots over capE rows: soccer in the split mode) copies its one slot's B, row
   // scalars and block table into LDS when the largest slot fits 160 KiB (MGX_PGS_WIDE_LDS=0: B
@@ -594,7 +605,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
-  p.tw = MGX_TW;  // block-table words per 4-row block: B offset + 64-bit dof support, any nv <= 64
+  p.tw = MGX_TW;  // block-table words (uint32) per 4-row block in the pipe, either B layout (mgx_staged.h)
   p.nobs = nobs;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t r = off; off = (off + bytes + 255) / 256 * 256; return r; };
@@ -605,7 +616,13 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.o_ne = take(S * 4); p.o_blen = take(S * 4); p.o_niter = take(S * 4); p.o_k2list = take(S * 4); p.o_k2big = take(S * 4); p.o_fix = take((size_t)n_env * 4);
   // the solver-list buckets are sized for the model's capacity, not the main launch's rows (a
   // per-call hook changes those), so the workspace layout never depends on MGX_PGS_LDS_ROWS
-  p.nbk = p.capE / 4 + 1;
+  // heavy slots in the main launch (hmain, the full-capacity soccer default): when the SQG layout of
+  // maxE rows fits the LDS of a capE-row wave. The MGX_PGS_LDS_ROWS test hook keeps the wide launch.
+  p.hmain = !rk && !cap_env && !p.sqg && !pgs_lds_b() && p.capE < p.maxE &&
+            staged_pgs_lds_bytes(m, p.maxE, pgs_lanes(), 1, mgx_twl(false)) <=
+                staged_pgs_lds_bytes(m, p.capE, pgs_lanes(), 0, mgx_twl(false));
+  if (p.hmain) p.warena = 0;
+  p.nbk = (p.hmain ? p.maxE : p.capE) / 4 + 1;
   p.o_hist = take((size_t)(p.maxE / 4 + 1) * 4);
   p.o_blist = take((size_t)(p.maxE / 4 + 1) * S * 4);
   p.o_scal = take(S * p.maxE * MGX_SCAL * rb);
@@ -621,13 +638,16 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.o_tq = take(nq * rb); p.o_tv = take(nv * rb); p.o_ta = take(64 * rb); p.o_tt = take(rb);
   p.o_tx = take(3 * nb * rb); p.o_txq = take(4 * nb * rb); p.o_tsc = take(3 * nb * rb); p.o_tn = take(4);
   p.o_tcg = take(2 * p.maxC * 4); p.o_tcd = take(p.maxC * rb); p.o_tcm = take(p.maxC * rb);
+  // per-slot ints: the RK4 step's warnings / overflow over its stages, parkour's overflow flag over
+  // its substeps; the checkAcc template kernel's rows when the monolithic layout keeps them in
+  // global memory
+  p.o_rkw = take(S * 4);
+  p.o_tscr = take(m->L.gB ? (size_t)m->L.gB_stride * rb : 64);
   if (rk) {
     const int nq4 = (nq + 3) & ~3;
     p.rk_stride = 2 * nq4 + 8 * 64 + 4;
     p.o_rk = take(S * p.rk_stride * rb);
     p.o_rks = take(S * 4);
-    p.o_rkw = take(S * 4);
-    p.o_tscr = take(m->L.gB ? (size_t)m->L.gB_stride * rb : 64);
   }
   if (P) *P = p;
   return off;
@@ -638,16 +658,16 @@ static size_t make_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 
 // LDS of one solver wave holding `rows` rows per slot (main launch: min(max_nefc,
 // MGX_PGS_LDS_ROWS); wide launch: max_nefc)
-int mgx::staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg) {
+int mgx::staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg, int twl) {
   int rb = m->precision == MGX_F32 ? 4 : 8;
   int nb3 = (rows / 4 + MGX_PGS_RING - 1) / MGX_PGS_RING * MGX_PGS_RING;  // whole ring turns
   const int spw = 64 / lps;
   // the row scalars (or, SQG: the forces only; pgs_group) + the block table
   const int sq = sqg ? 4 : 4 * MGX_SCAL;
-  return spw * (sq * nb3 + 4) * rb + spw * nb3 * 4 * MGX_TW + 64;
+  return spw * (sq * nb3 + 4) * rb + spw * nb3 * 4 * twl + 64;
 }
 static int pgs_lds_bytes(const mgx_model* m, int rows, int sqg = 0) {
-  return staged_pgs_lds_bytes(m, rows, pgs_lanes(), sqg);
+  return staged_pgs_lds_bytes(m, rows, pgs_lanes(), sqg, mgx_twl(false));
 }
 
 // MGX_SIDE_STREAM=0 (read per call) runs the wide solver launch after the main one on the caller's
@@ -717,7 +737,7 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   // occupancy probe: MGX_PGS_LDS_PAD pads the main solver launch's LDS (fewer waves per CU)
   if (const char* pad = getenv("MGX_PGS_LDS_PAD"))
     if (atoi(pad) > mlds && atoi(pad) <= 96 * 1024) mlds = atoi(pad);
-  if (!pgs_lds_b() && P.maxE <= P.capE) {
+  if (!pgs_lds_b() && (P.maxE <= P.capE || P.hmain)) {
     // every slot fits the main launch (the default capacity): no wide launch at all
     launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
   } else if (SideStream* side = (!pgs_lds_b() && side_streams()) ? side_stream(st) : nullptr) {

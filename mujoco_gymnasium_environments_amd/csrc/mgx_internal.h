@@ -101,7 +101,8 @@ int staged_kernels_configure(int precision, int ls, int lf, int settle);
 // per slot with `lps` lanes per slot and `tw` table words per block
 size_t make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe* P, bool rk, int nobs);
 // sqg: row scalars in the pipe, only the forces in LDS (the RK4 pipeline; soccer at full capacity)
-int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg);
+// twl: block-table words per block in LDS (mgx_twl: 8 for the 8-dof group layout, 4 dof-granular)
+int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg, int twl);
 // the wide solver launch beside the main one on a side stream (MGX_SIDE_STREAM, default 1)
 int side_streams();
 // the staged RK4 bipedal step (mgx_rk_staged.hip)
@@ -113,6 +114,16 @@ int bipedal_reset_staged(const mgx_model* m, const mgx_state* s, const mgx_biped
                          float* obs, uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st);
 int64_t bipedal_workspace_bytes(const mgx_model* m, int n_env, int banks);
 int bipedal_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, hipStream_t st);
+// the staged quadruped_parkour step (mgx_pk_staged.hip)
+bool parkour_staged_ok(const mgx_model* m);
+int parkour_staged_configure(const mgx_model* m);
+int parkour_step_staged(const mgx_model* m, const mgx_state* s, const mgx_parkour_env* e, const float* action, float* obs,
+                        double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
+                        uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st);
+int parkour_reset_staged(const mgx_model* m, const mgx_state* s, const mgx_parkour_env* e, const void* draws,
+                         float* obs, uint64_t seed, int env_offset, int n_env, const uint8_t* mask, hipStream_t st);
+int64_t parkour_workspace_bytes(const mgx_model* m, int n_env, int banks);
+int parkour_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, hipStream_t st);
 int pgs_lanes();
 int pgs_lds_b();
 }  // namespace mgx

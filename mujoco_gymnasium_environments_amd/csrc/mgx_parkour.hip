@@ -175,6 +175,8 @@ int mgx_parkour_configure(mgx_model* m, const mgx_parkour_ids* ids) {
          mgx_set_lds(k_parkour_logic<double>, m->L.bytes);
   }
   if (rc != MGX_OK) return rc;
+  rc = parkour_staged_configure(m);
+  if (rc != MGX_OK) return rc;
   m->parkour_ok = true;
   return MGX_OK;
 }
@@ -188,9 +190,12 @@ int mgx_parkour_step(const mgx_model* m, const mgx_state* s, const mgx_parkour_e
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
-  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (e->workspace)  // the staged step (mgx_pk_staged.hip)
+    return parkour_step_staged(m, s, e, action, obs, reward, terminated, truncated, final_obs, autoreset, seed,
+                               env_offset, n_env, mask, st);
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (m->precision == MGX_F32)
     MGX_PK_LAUNCH(float, 0, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->pkf, *s, *e, action,
                        (const float*)nullptr, obs, reward, terminated, truncated, final_obs, autoreset, seed,
@@ -211,9 +216,11 @@ int mgx_parkour_reset(const mgx_model* m, const mgx_state* s, const mgx_parkour_
   if (!draws && !e->episode) return fail(MGX_E_ARG, "device draws need the episode counter buffer");
   int rc = host_check_state(s);
   if (rc) return rc;
-  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (n_env <= 0) return MGX_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (e->workspace)  // every reset of a staged batch settles through the staged stages
+    return parkour_reset_staged(m, s, e, draws, obs, seed, env_offset, n_env, mask, st);
+  if (m->L.gB && !s->scratch) return fail(MGX_E_ARG, "this model needs mgx_state.scratch (scratch_bytes_per_env)");
   if (m->precision == MGX_F32)
     MGX_PK_LAUNCH(float, 1, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, m->pkf, *s, *e,
                        (const float*)nullptr, (const float*)draws, obs, (double*)nullptr, (uint8_t*)nullptr,
@@ -224,6 +231,13 @@ int mgx_parkour_reset(const mgx_model* m, const mgx_state* s, const mgx_parkour_
                        (uint8_t*)nullptr, (float*)nullptr, 0, seed, env_offset, n_env, mask);
   MGX_HIPCHK(hipGetLastError());
   return MGX_OK;
+}
+
+int64_t mgx_parkour_workspace_bytes(const mgx_model* m, int n_env, int banks) {
+  return parkour_workspace_bytes(m, n_env, banks);
+}
+int mgx_parkour_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, void* stream) {
+  return parkour_workspace_init(m, workspace, bytes, n_env, banks, (hipStream_t)stream);
 }
 
 int mgx_parkour_logic_test(const mgx_model* m, const mgx_parkour_logic_io* io, const mgx_parkour_env* e, int n_env,

@@ -32,6 +32,7 @@ MGX_PROF_SETTER(mgx_prof_set_buffer_rk_staged)
 namespace mgx {
 
 constexpr int RK_NCS = 3;   // contact-metadata lane sets of the row builder: up to 192 contacts
+// B in the dof-granular layout (mgx_staged.h DOFB): this pipeline streams B from HBM every sweep
 constexpr int RK_LPS = 16;  // solver lanes per slot
 constexpr int RK_EPL = 4;   // solver register entries per lane (nv 49..64)
 constexpr int RK_OBS = 102; // rescue_env.py:545-600
@@ -193,7 +194,7 @@ __device__ __forceinline__ void rk_rows_slot(const DevModel<T>& m, Env<T>& e, co
     e.time = rk.t[1];
     wsync();
   }
-  stage_rows<T, RK_NCS>(m, e, P, slot, warn, list_slot);
+  stage_rows<T, RK_NCS, true>(m, e, P, slot, warn, list_slot);
 }
 
 // qacc of the stage from the solver's v (finish_physics' first half): qacc_smooth + L^-1 D^-1/2 v
@@ -441,7 +442,7 @@ __device__ __forceinline__ void rk_settle_step(const DevModel<T>& Ms, const DevM
     }
     __threadfence();
     __syncthreads();
-    pgs_group<T, RK_EPL, RK_LPS, false, true>(P, smem, threadIdx.x < RK_LPS ? slot : -1, P.maxE, maxit, tol, scale,
+    pgs_group<T, RK_EPL, RK_LPS, false, true, true>(P, smem, threadIdx.x < RK_LPS ? slot : -1, P.maxE, maxit, tol, scale,
                                                64 / RK_LPS);
     __threadfence();
     __syncthreads();
@@ -572,7 +573,7 @@ RkSide* rk_side(hipStream_t st) {
 }
 
 int settle_lds(const mgx_model* m, const Pipe& P) {
-  int b = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1);
+  int b = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1, 4);
   if (m->Ls.bytes > b) b = m->Ls.bytes;
   if (m->Lf.bytes > b) b = m->Lf.bytes;
   return b;
@@ -582,7 +583,7 @@ template <typename T>
 void launch_rk_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big) {
   const int spw = 64 / RK_LPS;
   const int grid = (slots + spw - 1) / spw;
-  hipLaunchKernelGGL((k_pgs_groups<T, RK_EPL, RK_LPS, false, true>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale,
+  hipLaunchKernelGGL((k_pgs_groups<T, RK_EPL, RK_LPS, false, true, true>), dim3(grid), dim3(64), lds, st, P, maxit, tol, scale,
                      spw, big);
 }
 
@@ -597,7 +598,7 @@ int step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms,
   if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_bipedal_workspace_bytes");
   const int slots = n_env * (1 + banks);
   const T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
-  const int mlds = staged_pgs_lds_bytes(m, P.capE, RK_LPS, 1), wlds = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1);
+  const int mlds = staged_pgs_lds_bytes(m, P.capE, RK_LPS, 1, 4), wlds = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1, 4);
   const int wgrid = 64 / RK_LPS * MGX_PGS_WIDE_GRID;
   RkSide* side = side_streams() ? rk_side(st) : nullptr;
   for (int k = 0; k < 4; k++) {
@@ -646,12 +647,12 @@ template <typename T>
 int configure_t(const mgx_model* m) {
   Pipe P;
   make_staged_pipe(m, nullptr, 1, 1, &P, true, RK_OBS);
-  const int wl = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1);
+  const int wl = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1, 4);
   if (wl > 160 * 1024) return fail(MGX_E_CAPACITY, "staged RK4 solver LDS exceeds 160 KiB");
   return mgx_set_lds(k_rk_rows<T>, m->Ls.bytes) | mgx_set_lds(k_rk_finish<T>, m->Lf.bytes) |
          mgx_set_lds(k_rk_settle<T>, settle_lds(m, P)) | mgx_set_lds(k_rk_template<T, true>, m->L.bytes) |
          mgx_set_lds(k_rk_template<T, false>, m->L.bytes) |
-         mgx_set_lds(k_pgs_groups<T, RK_EPL, RK_LPS, false, true>, wl > 96 * 1024 ? wl : 96 * 1024);
+         mgx_set_lds(k_pgs_groups<T, RK_EPL, RK_LPS, false, true, true>, wl > 96 * 1024 ? wl : 96 * 1024);
 }
 
 }  // namespace

@@ -29,10 +29,17 @@ namespace mgx {
 // scalar layout per 4-row block (20 reals, 16-byte aligned): [b x4][f x4][R x4][1/AR x4][AR/2 x4],
 // so the solver reads each quantity of a block with one 16-byte LDS load
 #define MGX_SQ(k, i) (4 * (k) + (i))
-// block table: 4 words per 4-row block — the block's B offset (its couplings A_ij, then the
-// B entries of the dofs in its support), the 64-bit dof support mask, one pad word (16 bytes: one
-// vector load)
-#define MGX_TW 4
+// Two B layouts per 4-row block (16 bytes of block table each in the pipe), template flag DOFB:
+//  * 8-dof groups (DOFB = false; soccer, parkour): [A 8][per touched group: 8 dofs x 4 rows], table
+//    of 8 uint16 — the A offset, then one offset per group (0 = the slot's zero group). The solver
+//    reads its lane's offsets straight from the table (widened to 8 words in LDS).
+//  * dof-granular (DOFB = true; the RK4 bipedal pipeline): [A 8][per support dof: 4 rows], table
+//    [B offset, support lo, support hi, 0] (4 uint32). Half the B bytes of the group layout (a
+//    contact's support is ~8 dofs, its groups ~2.6 x 8), at ~25 more VALU ops per block to decode
+//    a lane's rank: the bipedal solver streams B from HBM and gains, the soccer solver (one wave
+//    per SIMD, B from L2 / MALL) measured 3% slower with it.
+#define MGX_TW 4  // table words per block in the pipe (16 bytes)
+__host__ __device__ constexpr int mgx_twl(bool dofb) { return dofb ? 4 : 8; }  // table words per block in LDS
 #define MGX_PGS_LPS 16         // solver: lanes per slot (16 or 64; MGX_PGS_LPS env overrides per process)
 #define MGX_PGS_LDS_B 0        // main solver launch: 1 = B in an LDS arena, 0 = B from global memory
 #define MGX_PGS_RING 2         // global-B solver: register ring of 4-row blocks (RING - 1 in flight; 3 and 4 measured no faster)
@@ -55,6 +62,9 @@ struct Pipe {
                        // to maxE) go to the second, wide-LDS launch (o_k2big)
   int arena;           // LDS bytes of one main-launch solver wave (scalars + block table + B of its slots)
   int sqg;             // soccer main launch: row scalars read from the pipe, forces only in LDS (capE > 192)
+  int hmain;           // 1: slots over capE rows stay in the main launch's heaviest-first list; a wave
+                       // holding one runs with its row scalars read from the pipe (SQG), whose LDS
+                       // (forces + table for maxE rows) fits the wave's capE-row allocation
   int warena;          // > 0: LDS bytes of the wide launch's one-slot waves, which solve a slot of
                        // more than capE rows with its B, scalars and table copied into LDS (the
                        // latency-bound chain of a heavy slot reads LDS instead of L2 / MALL)
@@ -245,7 +255,7 @@ __device__ __forceinline__ double readlane_t(double x, int l) { return readlane(
 // the row scalars and B -> pipe.
 // NCS: contact-metadata lane sets (contact c reads set c / 64, lane c % 64): 1 for up to 64
 // contacts, 3 for up to 192 (bipedal_rescue).
-template <typename T, int NCS = 1>
+template <typename T, int NCS = 1, bool DOFB = false>
 __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, const Pipe& P, int r0, int nlim, int nlim4,
                                             const ContactMeta<T>& cm, const ContactMeta<T>& cm2,
                                             const ContactMeta<T>& cm3, T dinvs, T* scal, uint32_t* blk, T* Bo,
@@ -388,23 +398,40 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
       o[MGX_SQ(0, 0)] = 0; o[MGX_SQ(1, 0)] = 0; o[MGX_SQ(2, 0)] = 1; o[MGX_SQ(3, 0)] = 1; o[MGX_SQ(4, 0)] = (T)0.5;
     }
   }
-  // the block for the solver: [A10 A20 A21 A30 A31 A32 0 0], then for each dof of the block's
-  // support (ascending) the dof's 4 rows [r0 r1 r2 r3] (one 16-byte load per 4 rows and dof in
-  // the solver). The table entry: [B offset, support lo, support hi, 0]. A dof outside the
-  // support has B = 0 exactly (the J build and the L'^-1 sweep touch the support only); the
-  // solver points it at the slot's zero area (offset 0, never written).
+  // the block for the solver: [A10 A20 A21 A30 A31 A32 0 0], then its B entries (DOFB: per support
+  // dof ascending, the dof's 4 rows; else per touched 8-dof group ascending, [8 dofs][4 rows]) — a
+  // lane's 4 rows of one dof are one 16-byte load in the solver. A dof outside the support has B = 0
+  // exactly (the J build and the L'^-1 sweep touch the support only); every lane of a touched group
+  // stores, so a group running past nv (bipedal's phantom dof 63) carries zeros, not stale data.
   {
     T* o = Bo + boff;
     if (l < 8) o[l] = l == 0 ? a10 : l == 1 ? a20 : l == 2 ? a21 : l == 3 ? a30 : l == 4 ? a31 : l == 5 ? a32 : (T)0;
-    if ((sup >> l) & 1ull) {
-      T* od = o + 8 + 4 * __popcll(sup & ((1ull << l) - 1ull));
-      od[0] = j0; od[1] = j1; od[2] = j2; od[3] = j3;
+    if constexpr (DOFB) {
+      if ((sup >> l) & 1ull) {
+        T* od = o + 8 + 4 * __popcll(sup & ((1ull << l) - 1ull));
+        od[0] = j0; od[1] = j1; od[2] = j2; od[3] = j3;
+      }
+      if (l < MGX_TW) {
+        uint32_t* bt = blk + MGX_TW * (r0 >> 2);
+        bt[l] = l == 0 ? (uint32_t)boff : l == 1 ? (uint32_t)sup : l == 2 ? (uint32_t)(sup >> 32) : 0u;
+      }
+      boff += 8 + 4 * __popcll(sup);
+    } else {
+      uint32_t gm = 0;
+#pragma unroll
+      for (int g = 0; g < 8; g++) gm |= ((sup >> (8 * g)) & 0xffull) ? (1u << g) : 0u;
+      const int g = l >> 3, jj = l & 7;
+      if ((gm >> g) & 1u) {
+        T* og = o + 8 + 32 * __popc(gm & ((1u << g) - 1u)) + 4 * jj;
+        og[0] = j0; og[1] = j1; og[2] = j2; og[3] = j3;
+      }
+      if (l < 8) {  // 8 uint16: the A offset, then per group g < 7 its data offset or 0 (the zero group)
+        uint16_t* bt = reinterpret_cast<uint16_t*>(blk + MGX_TW * (r0 >> 2));
+        const int v = l == 0 ? boff : (((gm >> (l - 1)) & 1u) ? boff + 8 + 32 * __popc(gm & ((1u << (l - 1)) - 1u)) : 0);
+        bt[l] = (uint16_t)v;
+      }
+      boff += 8 + 32 * __popc(gm);
     }
-    if (l < MGX_TW) {
-      uint32_t* bt = blk + MGX_TW * (r0 >> 2);
-      bt[l] = l == 0 ? (uint32_t)boff : l == 1 ? (uint32_t)sup : l == 2 ? (uint32_t)(sup >> 32) : 0u;
-    }
-    boff += 8 + 4 * __popcll(sup);
   }
   MGX_BSTAMP(11);
 }
@@ -412,7 +439,7 @@ __device__ __forceinline__ void build_block(const DevModel<T>& m, Env<T>& e, con
 // S1 body: forward up to the constraint rows, rows -> pipe, carry -> pipe
 // list_slot: enter the slot in the solver launches' lists (the pipeline); the one-wave settle
 // (settle_step) solves the slot itself.
-template <typename T, int NCS = 1>
+template <typename T, int NCS = 1, bool DOFB = false>
 __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, const Pipe& P, int slot, int warn,
                                            bool list_slot = true) {
   int l = lane_id();
@@ -480,7 +507,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
     __threadfence();  // the row constants are read back by other lanes of this wave (build_block)
     wsync();
     for (int r0 = 0; r0 < ne; r0 += 4)
-      build_block<T, NCS>(m, e, P, r0, nlim, nlim4, cm, cm2, cm3, dinvs, scal, blk, Bo, boff);
+      build_block<T, NCS, DOFB>(m, e, P, r0, nlim, nlim4, cm, cm2, cm3, dinvs, scal, blk, Bo, boff);
   }
   MGX_STAMP(7);
   // carry + registers + ints
@@ -506,7 +533,7 @@ __device__ __forceinline__ void stage_rows(const DevModel<T>& m, Env<T>& e, cons
     }
 #endif
     if (!list_slot) {
-    } else if (ne > P.capE) {  // rare: more rows than the main solver launch keeps in LDS
+    } else if (ne > P.capE && !P.hmain) {  // rare: more rows than the main solver launch keeps in LDS
       int idx = atomicAdd(P.ctr() + 2, 1);
       P.at<int>(P.o_k2big)[idx] = slot;
     } else if (ne > 0) {
@@ -586,19 +613,31 @@ struct PgsTab {
   uint32_t a, g[EPL];
 };
 
-template <int EPL, int LPS>
+template <int EPL, int LPS, bool DOFB>
 __device__ __forceinline__ void pgs_load_tab(PgsTab<EPL>& t, const uint32_t* bt, int blk, int j) {
-  // one 16-byte LDS load: [B offset, support lo, support hi, 0]; this lane's dof j + 8 gi of each
-  // register entry is at rank popc(support below it) of the block's dof list, or absent (zero area)
-  const uint4 e = *reinterpret_cast<const uint4*>(bt + MGX_TW * blk);
-  t.a = e.x;
-  const uint64_t sup = (uint64_t)e.y | ((uint64_t)e.z << 32);
+  if constexpr (DOFB) {
+    // one 16-byte LDS load: [B offset, support lo, support hi, 0]; this lane's dof of each register
+    // entry is at rank popc(support below it) of the block's dof list, or absent (zero area)
+    const uint4 e = *reinterpret_cast<const uint4*>(bt + 4 * blk);
+    t.a = e.x;
+    const uint64_t sup = (uint64_t)e.y | ((uint64_t)e.z << 32);
 #pragma unroll
-  for (int d = 0; d < EPL; d++) {
-    const int dof = 8 * (d * (LPS / 8) + (j >> 3)) + (j & 7);
-    const uint64_t below = dof >= 64 ? sup : sup & ((1ull << dof) - 1ull);
-    const bool in = dof < 64 && ((sup >> (dof & 63)) & 1ull);
-    t.g[d] = in ? e.x + 8u + 4u * (uint32_t)__popcll(below) : 0u;
+    for (int d = 0; d < EPL; d++) {
+      const int dof = 8 * (d * (LPS / 8) + (j >> 3)) + (j & 7);
+      const uint64_t below = dof >= 64 ? sup : sup & ((1ull << dof) - 1ull);
+      const bool in = dof < 64 && ((sup >> (dof & 63)) & 1ull);
+      t.g[d] = in ? e.x + 8u + 4u * (uint32_t)__popcll(below) : 0u;
+    }
+  } else {
+    // the A offset and the offsets of the lane's EPL dof groups (widened in LDS: no 16-bit extracts
+    // on the address path); absent groups point at the zero group
+    const uint32_t* e = bt + 8 * blk;
+    t.a = e[0];
+#pragma unroll
+    for (int d = 0; d < EPL; d++) {
+      const int gi = d * (LPS / 8) + (j >> 3);
+      t.g[d] = (gi < 7 ? e[1 + gi] : 0u) + 4u * (uint32_t)(j & 7);
+    }
   }
 }
 
@@ -631,11 +670,11 @@ __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, 
   k.qh = q[4];
   __builtin_amdgcn_sched_barrier(0);  // keep the prefetch where it is issued
 }
-template <typename T, int EPL, int LPS, int FS>
+template <typename T, int EPL, int LPS, int FS, bool DOFB>
 __device__ __forceinline__ void pgs_load_block(PgsBlk<T, EPL>& k, const T* Bsl, const T* sq, const T* fb,
                                                const uint32_t* bt, int blk, int sblk, int j) {
   PgsTab<EPL> t;
-  pgs_load_tab<EPL, LPS>(t, bt, blk, j);
+  pgs_load_tab<EPL, LPS, DOFB>(t, bt, blk, j);
   pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, t, blk, sblk, j);
 }
 
@@ -721,7 +760,7 @@ __device__ __forceinline__ void pgs_block(const PgsBlk<T, EPL>& k, T (&v)[EPL], 
 // otherwise hold the launch to two waves per CU; bipedal 175.0k -> 186.6k env-steps/s); the
 // soccer launch keeps all scalars in LDS at four waves per CU, which measured faster than the
 // global scalars at any occupancy (MGX_PGS_LDS_PAD sweep).
-template <typename T, int EPL, int LPS, bool BLDS, bool SQG = false>
+template <typename T, int EPL, int LPS, bool BLDS, bool SQG = false, bool DOFB = false>
 __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, int capE, int maxit, T tol, T scale,
                                           int spw, int arena = -1) {
   constexpr int RING = BLDS ? MGX_PGS_RING_LDS : MGX_PGS_RING;
@@ -742,7 +781,9 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   const int nbRun = (nbMax + RING - 1) / RING * RING;
   const size_t sl = (size_t)(slot >= 0 ? slot : 0);
   const T* gsc = P.at<T>(P.o_scal) + sl * P.maxE * MGX_SCAL;
+  constexpr int TWL = mgx_twl(DOFB);  // table words per block in LDS
   const uint32_t* gbt = P.at<uint32_t>(P.o_blk) + sl * (P.maxE / 4) * MGX_TW;
+  const uint16_t* gbt16 = reinterpret_cast<const uint16_t*>(gbt);
   const T* gB = P.at<T>(P.o_B) + sl * P.bcap;
   int nbA;  // blocks of scalars / table entries per slot (the look-ahead stays inside)
   T* sc;
@@ -757,7 +798,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   if constexpr (BLDS) {
     nbA = nbRun + RING - 1;
     const int blen = slot >= 0 ? (P.at<int>(P.o_blen)[slot] + 3) & ~3 : 0;
-    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 4 * MGX_TW) + blen * (int)sizeof(T);  // 16-byte multiple
+    const int bytes = nbA * (4 * MGX_SCAL * (int)sizeof(T) + 4 * TWL) + blen * (int)sizeof(T);  // 16-byte multiple
     int off = 0, tot = 0;
     if (arena < 0) {
       // main launch: the wave's slots side by side
@@ -781,7 +822,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     }
     sc = reinterpret_cast<T*>(smem + off);
     bt = reinterpret_cast<uint32_t*>(sc + 4 * MGX_SCAL * nbA);
-    T* Bs = reinterpret_cast<T*>(bt + MGX_TW * nbA);
+    T* Bs = reinterpret_cast<T*>(bt + TWL * nbA);
     for (int q = 4 * j; q < blen; q += 4 * LPS)
       *reinterpret_cast<V4*>(Bs + q) = *reinterpret_cast<const V4*>(gB + q);
     Bsl = Bs;
@@ -794,7 +835,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     nbA = (nbcap + RING - 1) / RING * RING;
     const int sstride = (SG ? 4 : 4 * MGX_SCAL) * nbA + 4;  // 16-byte aligned per slot
     sc = reinterpret_cast<T*>(smem) + s * sstride;
-    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * MGX_TW * nbA;
+    bt = reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(smem) + SPW * sstride) + s * TWL * nbA;
     Bsl = gB;
     if constexpr (SG) {
       sq = gsc;
@@ -809,7 +850,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   // scalar blocks past the slot's capacity are never real (masked); their loads stay inside it
   const int sbmax = P.maxE / 4 - 1;
   // block table: the slot's blocks, then zero-group entries up to the capacity
-  for (int q = j; q < MGX_TW * nbA; q += LPS) bt[q] = q < MGX_TW * nblk ? gbt[q] : 0u;
+  for (int q = j; q < TWL * nbA; q += LPS) bt[q] = q < TWL * nblk ? (DOFB ? gbt[q] : (uint32_t)gbt16[q]) : 0u;
   __syncthreads();
   // warmstart: v = B' f, dual cost, reset to zero if the cost is positive
   T v[EPL];
@@ -817,7 +858,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   for (int d = 0; d < EPL; d++) v[d] = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
+    pgs_load_block<T, EPL, LPS, FS, DOFB>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
     const T* qf = fb + FS * b;
     bool ok = b < nblk;
     T f0 = ok ? qf[0] : (T)0, f1 = ok ? qf[1] : (T)0, f2 = ok ? qf[2] : (T)0, f3 = ok ? qf[3] : (T)0;
@@ -826,7 +867,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
   T cpart = 0;
   for (int b = 0; b < nbMax; b++) {
     PgsBlk<T, EPL> k;
-    pgs_load_block<T, EPL, LPS, FS>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
+    pgs_load_block<T, EPL, LPS, FS, DOFB>(k, Bsl, sq, fb, bt, b, min(b, sbmax), j);
     T d0, d1, d2, d3;
     pgs_dots(k, v, d0, d1, d2, d3);
     slot_sum4<LPS>(d0, d1, d2, d3);
@@ -862,11 +903,11 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
     T impr = 0;
     PgsBlk<T, EPL> R[RING];
     PgsTab<EPL> tn;  // the table entry of the next block to load (one ring step ahead of its data)
-    pgs_load_tab<EPL, LPS>(tn, bt, 0, j);
+    pgs_load_tab<EPL, LPS, DOFB>(tn, bt, 0, j);
 #pragma unroll
     for (int k = 0; k < RING - 1; k++) {
       pgs_load_block<T, EPL, LPS, FS>(R[k], Bsl, sq, fb, tn, k, min(k, sbmax), j);
-      pgs_load_tab<EPL, LPS>(tn, bt, k + 1, j);
+      pgs_load_tab<EPL, LPS, DOFB>(tn, bt, k + 1, j);
     }
     // full ring turns, no early exit inside, so every prefetch is consumed on every path and
     // the compiler cannot sink the loads next to their use. The table has zero entries up to
@@ -877,7 +918,7 @@ __device__ __forceinline__ void pgs_group(const Pipe& P, char* smem, int slot, i
         // the slot consumed last lands the block RING - 1 ahead, then block b0 + k is solved
         const int bn = min(b0 + k + RING - 1, nbA - 1);
         pgs_load_block<T, EPL, LPS, FS>(R[(k + RING - 1) % RING], Bsl, sq, fb, tn, bn, min(bn, sbmax), j);
-        pgs_load_tab<EPL, LPS>(tn, bt, min(bn + 1, nbA - 1), j);
+        pgs_load_tab<EPL, LPS, DOFB>(tn, bt, min(bn + 1, nbA - 1), j);
         pgs_block<T, EPL, LPS>(R[k], v, fb + FS * (b0 + k), act && b0 + k < nblk, impr);
       }
     }
@@ -946,7 +987,7 @@ __device__ __forceinline__ int sorted_slot(const Pipe& P, int idx, int LPS) {
   return slot;
 }
 
-template <typename T, int EPL, int LPS, bool BLDS, bool SQG = false>
+template <typename T, int EPL, int LPS, bool BLDS, bool SQG = false, bool DOFB = false>
 __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T scale, int spw, int big) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (!big && blockIdx.x == 0 && threadIdx.x == 0) P.ctr()[0] = 0;  // fixup list count, filled by the finisher
@@ -961,7 +1002,21 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
   for (int base = blockIdx.x * spn; base < cnt; base += gridDim.x * spn) {
     const int idx = dup ? base : (s < spn && base + s < cnt) ? base + s : -1;
     const int slot = big ? (idx >= 0 ? list[idx] : -1) : sorted_slot(P, idx, LPS);
-    pgs_group<T, EPL, LPS, BLDS && true, SQG>(P, smem, slot, big ? P.maxE : P.capE, maxit, tol, scale, spw,
+    if constexpr (!BLDS && !SQG) {
+      // a wave holding a slot over the main launch's LDS-scalar rows (heaviest first: the first
+      // waves) reads its row scalars from the pipe instead; same arithmetic, so the same results
+      if (!big && P.hmain) {
+        int nm = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;
+        nm = max(nm, __shfl_xor(nm, 16));
+        nm = max(nm, __shfl_xor(nm, 32));
+        if (__builtin_amdgcn_readfirstlane(nm) > P.capE) {
+          pgs_group<T, EPL, LPS, false, true, DOFB>(P, smem, slot, P.maxE, maxit, tol, scale, spw, -1);
+          __syncthreads();
+          continue;
+        }
+      }
+    }
+    pgs_group<T, EPL, LPS, BLDS && true, SQG, DOFB>(P, smem, slot, big ? P.maxE : P.capE, maxit, tol, scale, spw,
                                                   big ? P.warena : -1);
     __syncthreads();  // the next group reuses the LDS
   }

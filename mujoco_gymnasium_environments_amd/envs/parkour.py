@@ -22,7 +22,7 @@ import torch
 
 from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
-from ..native import check, lib
+from ..native import NativeError, check, lib
 from ..seeding import np_random
 from ..spaces import Box, EnvBase
 
@@ -107,7 +107,11 @@ class ParkourVectorEnv:
 
     def __init__(self, num_envs: int, device: str = "cuda:0", precision: str = "f64", seed: int = 0,
                  max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True, env_offset: int = 0,
-                 rows_in_scratch: Optional[bool] = None):
+                 rows_in_scratch: Optional[bool] = None, staged: bool = True, banks: int = 1):
+        """``staged`` selects the per-substep row builder / lane-group PGS / finisher kernels with
+        ``banks`` precomputed resets per env (one covers every autoreset: a bank settles within one
+        env step); ``staged=False`` runs one wave per env for the whole env step. Both compute the
+        same step (tests/test_gpu_parkour.py)."""
         self.num_envs = num_envs
         self.device = torch.device(device)
         self.model = parkour_model(rows_in_scratch)
@@ -138,6 +142,18 @@ class ParkourVectorEnv:
             self.stuck, self.step_count, self.episode, self.rollout)])
         ids = self.tables.ids_struct()
         check(lib().mgx_parkour_configure(self.native.handle, C.byref(ids)), "mgx_parkour_configure")
+        self.staged = staged
+        self.workspace = None
+        if staged:
+            nb = int(lib().mgx_parkour_workspace_bytes(self.native.handle, N, banks))
+            if nb <= 0:
+                raise NativeError(f"mgx_parkour_workspace_bytes: {lib().mgx_last_error().decode()}")
+            self.workspace = torch.empty(nb, dtype=torch.uint8, device=dev)
+            check(lib().mgx_parkour_workspace_init(self.native.handle, _ptr(self.workspace), nb, N, banks, None),
+                  "mgx_parkour_workspace_init")
+            self._env.workspace = self.workspace.data_ptr()
+            self._env.workspace_bytes = nb
+            self._env.banks = banks
         lim = action_limits()
         self.action_space = Box(low=-lim, high=lim, dtype=np.float32)
 

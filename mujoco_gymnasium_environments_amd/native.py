@@ -16,11 +16,12 @@ ROOT = os.path.dirname(PKG)
 # MGX_LIB: load another build of the same sources (A/B measurements of a kernel variant)
 LIB_PATH = os.environ.get("MGX_LIB") or os.path.join(PKG, "libmgx.so")
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_rk_staged.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip",
+SOURCES = ["mgx_api.hip", "mgx_pgs.hip", "mgx_rk_staged.hip", "mgx_pk_staged.hip", "mgx_step.hip", "mgx_parkour.hip", "mgx_bipedal.hip",
            "mgx_dancing.hip",
            "mgx_martial.hip", "mgx_assembly.hip", "mgx_construction.hip"]
 # per-translation-unit flags: the staged solver's FMA chains must not be SLP-packed (mgx_pgs.hip)
-SOURCE_FLAGS = {"mgx_pgs.hip": ["-fno-slp-vectorize"], "mgx_rk_staged.hip": ["-fno-slp-vectorize"]}
+SOURCE_FLAGS = {"mgx_pgs.hip": ["-fno-slp-vectorize"], "mgx_rk_staged.hip": ["-fno-slp-vectorize"],
+                "mgx_pk_staged.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["mgx_common.h", "mgx_collide.h", "mgx_physics.h", "mgx_soccer.h", "mgx_staged.h", "mgx_parkour.h",
            "mgx_bipedal.h", "mgx_dancing.h", "mgx_martial.h", "mgx_internal.h", "mgx_wide.h", "mgx_construction.h"]
 # task headers included by one translation unit only (so editing one rebuilds one object)
@@ -107,6 +108,8 @@ _SIGS = {
     "mgx_soccer_reset": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxSoccerEnv), _VP, _VP, C.c_uint64,
                           C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_soccer_logic_test": ([_VP, C.POINTER(cabi.MgxSoccerLogicIO), C.c_int, _VP], C.c_int),
+    "mgx_parkour_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
+    "mgx_parkour_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
     "mgx_bipedal_workspace_bytes": ([_VP, C.c_int, C.c_int], C.c_int64),
     "mgx_bipedal_workspace_init": ([_VP, _VP, C.c_uint64, C.c_int, C.c_int, _VP], C.c_int),
     "mgx_bipedal_workspace_layout": ([_VP, C.c_int, C.c_int, C.POINTER(C.c_int64), C.c_int], C.c_int),
