@@ -405,10 +405,12 @@ def bench_mixed(args, dev, world, rank, dist):
         "humanoid_soccer": (SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=11, env_offset=off,
                                             banks=args.banks), lambda: torch.rand(N, 33, device=dev, generator=g) * 300 - 150,
                             ALG_BYTES_PER_ENV_STEP_F64 if f64 else ALG_BYTES_PER_ENV_STEP),
-        "quadruped_parkour": (ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=12, env_offset=off),
+        "quadruped_parkour": (ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=12, env_offset=off,
+                                               staged=bool(args.mix_staged)),
                               lambda: (torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim,
                               PARKOUR_ALG_BYTES_F64 if f64 else PARKOUR_ALG_BYTES),
-        "bipedal_rescue": (BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=13, env_offset=off),
+        "bipedal_rescue": (BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=13, env_offset=off,
+                                            staged=bool(args.mix_staged)),
                            lambda: (torch.rand(N, 26, device=dev, generator=g) * 2 - 1) * 100.0,
                            BIPEDAL_ALG_BYTES_F64 if f64 else BIPEDAL_ALG_BYTES),
         "humanoid_dancing": (DancingVectorEnv(N, device=str(dev), precision=args.precision, seed=14, env_offset=off),
@@ -578,6 +580,8 @@ def main():
                     help="skip the other-precision soccer line (fp32 when the headline is fp64)")
     ap.add_argument("--mix-streams", type=int, default=4, help="mixed: 4 grouped streams (default) or 7 (one per task)")
     ap.add_argument("--mix-priority", type=int, default=1, help="mixed: construction's stream at high priority (1)")
+    ap.add_argument("--mix-staged", type=int, default=1,
+                    help="mixed: parkour and bipedal on their staged pipelines (1) or one wave per env (0)")
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
                                                           "construction"])
     args = ap.parse_args()

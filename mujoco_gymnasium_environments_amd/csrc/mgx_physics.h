@@ -1140,17 +1140,32 @@ __device__ __forceinline__ void chol_blocked(T* H, int nv) {
   const int nb = (nv + 15) >> 4;
   for (int kb = 0; kb < nb; kb++) {
     const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
-    // 1. diagonal block, left-looking within the block: lane i < bk owns row k0 + i
-    for (int c = 0; c < bk; c++) {
-      const bool act = l < bk && l >= c;
-      const int r = k0 + (act ? l : c);
-      const T* Lr = H + r * nv + k0;
-      const T* Lc = H + (k0 + c) * nv + k0;
-      T s = Lr[c];
-      for (int j = 0; j < c; j++) s -= Lr[j] * Lc[j];
-      const T dkk = readlane(s, c);
-      const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
-      if (act) H[r * nv + k0 + c] = l == c ? d : s / d;
+    // 1. diagonal block in registers: lane i < bk holds row k0 + i of the block (16 entries), the
+    //    factor is right-looking over the block's columns with the column values broadcast by
+    //    readlane — no LDS round trip or wave barrier per column. Entry (i, c) receives the same
+    //    products in the same order as the left-looking dot s = a_ic - sum_{j<c} l_ij l_cj.
+    {
+      T x[16];
+      const T* Lr = H + (k0 + (l < bk ? l : 0)) * nv + k0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) x[j] = (l < bk && j < bk) ? Lr[j] : (T)0;
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        if (c < bk) {
+          const T dkk = readlane(x[c], c);
+          const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
+          x[c] = l == c ? d : (l > c ? x[c] / d : x[c]);
+          const T lic = x[c];
+#pragma unroll
+          for (int j = c + 1; j < 16; j++)
+            if (j < bk && l >= j) x[j] -= lic * readlane(x[c], j);
+        }
+      }
+      T* Hr = H + (k0 + (l < bk ? l : 0)) * nv + k0;
+      if (l < bk)
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          if (j <= l) Hr[j] = x[j];
       wsync();
     }
     // 2. panel: rows below the block, x = a L_kk^-T by forward substitution (lane = row)

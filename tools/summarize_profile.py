@@ -15,7 +15,8 @@ import shutil
 import sys
 
 STEP_KERNELS = ["k_soccer_rows", "k_pgs_groups", "k_soccer_bank_finish", "k_soccer_finish", "k_soccer_fixup", "k_soccer_settle",
-                "k_rk_rows", "k_rk_finish", "k_rk_settle", "k_soccer<float, 0>",
+                "k_rk_rows", "k_rk_finish", "k_rk_settle", "k_pk_rows", "k_pk_bank_finish", "k_pk_finish", "k_pk_settle",
+                "k_soccer<float, 0>",
                 "k_soccer<double, 0>", "k_bipedal<float, 0, true>", "k_bipedal<float, 0, false>",
                 "k_parkour<float, 0>", "k_parkour<float, 0, true>", "k_parkour<float, 0, false>",
                 "k_martial<float, 0, true>", "k_martial<float, 0, false>",
