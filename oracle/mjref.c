@@ -1437,8 +1437,19 @@ static double newton_cost(const mgx_model_desc *m, ref_data *d, const double *a,
   return c;
 }
 
+/* Newton diagnostics (ref_newton_stats): solves, iterations, active rows summed over iterations,
+   rows whose active state changed since the previous iteration of the same solve */
+static long g_newton_stats[4];
+void ref_newton_stats(long *out, int reset) {
+  for (int k = 0; k < 4; k++) out[k] = g_newton_stats[k];
+  if (reset)
+    for (int k = 0; k < 4; k++) g_newton_stats[k] = 0;
+}
+
 static void newton_solve(const mgx_model_desc *m, ref_data *d) {
   int nv = m->nv, ne = d->nefc[0];
+  unsigned char *prev_act = calloc(ne > 0 ? ne : 1, 1);
+  g_newton_stats[0]++;
   double *M = malloc(sizeof(double) * (3 * nv * nv + 6 * nv + 3 * ne));
   double *H = M + nv * nv, *a = H + nv * nv, *g = a + nv, *p = g + nv, *Mp = p + nv, *tmp = Mp + nv;
   double *x = tmp + 2 * nv, *jp = x + ne, *xt = jp + ne;
@@ -1462,6 +1473,13 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
   /* mj_solNewton's loop order [ext]: every iteration updates, then tests the scaled improvement
      and the scaled gradient at the new point, so at least one iteration always runs */
   while (iter < m->iterations) {
+    g_newton_stats[1]++;
+    for (int r = 0; r < ne; r++) {
+      const unsigned char act = x[r] < 0;
+      g_newton_stats[2] += act;
+      if (iter > 0 && act != prev_act[r]) g_newton_stats[3]++;
+      prev_act[r] = act;
+    }
     /* H = M + J_A' D_A J_A, Cholesky (lower, in place) */
     memcpy(H, M, sizeof(double) * nv * nv);
     for (int r = 0; r < ne; r++) {
@@ -1569,6 +1587,7 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
     if (improvement < m->tolerance || scale * sqrt(gn) < m->tolerance) break;
   }
   d->solver_niter[0] = iter;
+  free(prev_act);
   memcpy(d->qacc, a, sizeof(double) * nv);
   for (int r = 0; r < ne; r++) d->efc_force[r] = x[r] < 0 ? -x[r] / d->efc_R[r] : 0;
   memset(d->qfrc_constraint, 0, sizeof(double) * nv);

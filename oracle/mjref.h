@@ -39,6 +39,8 @@ void *ref_field(ref_data *d, const char *name, int *count);
 
 /* narrowphase test hook: collide geoms g1, g2 of the current geom frames; returns ncon */
 int ref_collide_pair(const mgx_model_desc *m, ref_data *d, int pair_index);
+/* Newton diagnostics: solves, iterations, active rows over iterations, active-state changes */
+void ref_newton_stats(long *out, int reset);
 /* narrowphase branch counters since the last reset (16 longs, layout in mjref.c) */
 void ref_narrowphase_stats(long *out, int reset);
 
