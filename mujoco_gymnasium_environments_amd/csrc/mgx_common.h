@@ -44,6 +44,11 @@ struct Layout {
   // 1: the monolithic kernel keeps B rows in per-env global scratch (gB_stride reals per env)
   // instead of LDS, for models whose rows do not fit the LDS budget
   int gB, gB_stride;
+  // wide kernels (nv > 64): the per-row constraint data efc / efc_margin sit in the per-env global
+  // scratch at these real offsets instead of LDS (gB_efc >= 0), and the Newton Hessian is stored
+  // as a packed lower triangle, row i at i (i + 1) / 2 (hpk) — with both, humanoid_construction's
+  // per-env LDS fits two envs per CU
+  int gB_efc, gB_efm, hpk;
   // gB only: rows per chunk staged into the (dead) phase-A union region for the row transform
   int tchunk;
   // Newton solver (solver == mjSOL_NEWTON, monolithic kernels only): nv x nv Hessian

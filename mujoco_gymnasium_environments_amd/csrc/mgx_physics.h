@@ -37,8 +37,9 @@ struct Env {
   uint64_t ancmask;
 };
 
-// GB: B rows in global scratch (gB = this env's slice) instead of LDS (Layout.gB)
-template <typename T, bool GB = false>
+// GB: B rows in global scratch (gB = this env's slice) instead of LDS (Layout.gB); EG: the per-row
+// constraint data as well (Layout.gB_efc: the wide kernels)
+template <typename T, bool GB = false, bool EG = false>
 __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem, T* gB = nullptr) {
   T* R = reinterpret_cast<T*>(smem);
   const Layout& L = m.L;
@@ -51,6 +52,7 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.cacc = R + L.cacc; e.rowc = R + L.rowc; e.con_dist = R + L.con_dist;
   e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
   e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bs = L.Bstride;
+  if constexpr (EG) { e.efc = gB + L.gB_efc; e.efc_margin = gB + L.gB_efm; }
   if constexpr (GB) e.Bm = gB;
   else e.Bm = R + L.Bmat;
   e.rk = R + L.rk;
@@ -1132,8 +1134,14 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
 // column, <= 15-term dots), solve the panel below it against L_kk' (lane = row, L_kk read as LDS
 // broadcasts), then subtract L_I L_J' from every trailing lower tile on MFMA (16x16x4: four
 // per tile, accumulators initialised from the tile). Entries past nv read as 0 and are never
-// stored. Same pivot clamp as the unblocked factor (d = sqrt(max(dkk, minval))).
-template <typename T>
+// stored. Same pivot clamp as the unblocked factor (d = sqrt(max(dkk, minval))). PK: H is the
+// packed lower triangle (entry (r, c), c <= r, at r (r + 1) / 2 + c; Layout.hpk, the wide solver).
+template <bool PK>
+__device__ __forceinline__ int hidx(int r, int c, int nv) {
+  return PK ? (r * (r + 1) >> 1) + c : r * nv + c;
+}
+
+template <typename T, bool PK = false>
 __device__ __forceinline__ void chol_blocked(T* H, int nv) {
   typedef T V4 __attribute__((ext_vector_type(4)));
   const int l = lane_id();
@@ -1146,9 +1154,9 @@ __device__ __forceinline__ void chol_blocked(T* H, int nv) {
     //    products in the same order as the left-looking dot s = a_ic - sum_{j<c} l_ij l_cj.
     {
       T x[16];
-      const T* Lr = H + (k0 + (l < bk ? l : 0)) * nv + k0;
+      const T* Lr = H + hidx<PK>(k0 + (l < bk ? l : 0), k0, nv);
 #pragma unroll
-      for (int j = 0; j < 16; j++) x[j] = (l < bk && j < bk) ? Lr[j] : (T)0;
+      for (int j = 0; j < 16; j++) x[j] = (l < bk && j <= l) ? Lr[j] : (T)0;
 #pragma unroll
       for (int c = 0; c < 16; c++) {
         if (c < bk) {
@@ -1161,7 +1169,7 @@ __device__ __forceinline__ void chol_blocked(T* H, int nv) {
             if (j < bk && l >= j) x[j] -= lic * readlane(x[c], j);
         }
       }
-      T* Hr = H + (k0 + (l < bk ? l : 0)) * nv + k0;
+      T* Hr = H + hidx<PK>(k0 + (l < bk ? l : 0), k0, nv);
       if (l < bk)
 #pragma unroll
         for (int j = 0; j < 16; j++)
@@ -1169,18 +1177,17 @@ __device__ __forceinline__ void chol_blocked(T* H, int nv) {
       wsync();
     }
     // 2. panel: rows below the block, x = a L_kk^-T by forward substitution (lane = row)
-    const T* Lkk = H + k0 * nv + k0;
     for (int r = k0 + bk + l; r < nv + 64 && r - l < nv; r += 64) {
       if (r < nv) {
-        T* Ar = H + r * nv + k0;
+        T* Ar = H + hidx<PK>(r, k0, nv);
         T x[16];
 #pragma unroll
         for (int c = 0; c < 16; c++) {
           if (c < bk) {
             T t = Ar[c];
 #pragma unroll
-            for (int j = 0; j < c; j++) t -= x[j] * Lkk[c * nv + j];
-            x[c] = t / Lkk[c * nv + c];
+            for (int j = 0; j < c; j++) t -= x[j] * H[hidx<PK>(k0 + c, k0 + j, nv)];
+            x[c] = t / H[hidx<PK>(k0 + c, k0 + c, nv)];
           }
         }
 #pragma unroll
@@ -1198,14 +1205,14 @@ __device__ __forceinline__ void chol_blocked(T* H, int nv) {
 #pragma unroll
         for (int v = 0; v < 4; v++) {
           const int row = 16 * I + row_of(v), col = 16 * J + i;
-          acc[v] = (row < nv && col < nv) ? H[row * nv + col] : (T)0;
+          acc[v] = (row < nv && col <= row) ? H[hidx<PK>(row, col, nv)] : (T)0;
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const int kk = k0 + 4 * q + kq;  // this lane's k in the 16-wide block column
           const int ra = 16 * I + i, rb = 16 * J + i;
-          const T a = (ra < nv && kk < k0 + bk) ? -H[ra * nv + kk] : (T)0;
-          const T b = (rb < nv && kk < k0 + bk) ? H[rb * nv + kk] : (T)0;
+          const T a = (ra < nv && kk < k0 + bk) ? -H[hidx<PK>(ra, kk, nv)] : (T)0;
+          const T b = (rb < nv && kk < k0 + bk) ? H[hidx<PK>(rb, kk, nv)] : (T)0;
           if constexpr (sizeof(T) == 8)
             acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
           else
@@ -1214,7 +1221,7 @@ __device__ __forceinline__ void chol_blocked(T* H, int nv) {
 #pragma unroll
         for (int v = 0; v < 4; v++) {
           const int row = 16 * I + row_of(v), col = 16 * J + i;
-          if (row < nv && col <= row) H[row * nv + col] = acc[v];
+          if (row < nv && col <= row) H[hidx<PK>(row, col, nv)] = acc[v];
         }
       }
     }

@@ -40,7 +40,7 @@ __device__ __forceinline__ T wdot(const T (&a)[2], const T (&b)[2]) {
 
 template <typename T>
 __device__ __forceinline__ void wenv_bind(const DevModel<T>& m, WEnv<T>& w, char* smem, T* gB) {
-  env_bind<T, true>(m, w.e, smem, gB);
+  env_bind<T, true, true>(m, w.e, smem, gB);
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int d = wdof(k);
@@ -236,7 +236,7 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
 #pragma unroll
       for (int v = 0; v < 4; v++) {
         const int row = 16 * t + row_of(v), col = 16 * u + i;
-        if (t < nt && row < nv && col <= row) H[row * nv + col] = acc[q][v];
+        if (t < nt && row < nv && col <= row) H[hidx<true>(row, col, nv)] = acc[q][v];
       }
 }
 
@@ -350,12 +350,12 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     whessian(Bm, Bs, efc, ne, nv, H);
     wsync();
     MGX_STAMP(11);  // Hessian
-    chol_blocked(H, nv);
+    chol_blocked<T, true>(H, nv);
     MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y
     T rdiag[2];
 #pragma unroll
-    for (int k = 0; k < 2; k++) rdiag[k] = dl[k] ? (T)1 / H[(64 * k + l) * nv + 64 * k + l] : (T)0;
+    for (int k = 0; k < 2; k++) rdiag[k] = dl[k] ? (T)1 / H[hidx<true>(64 * k + l, 64 * k + l, nv)] : (T)0;
     T y[2] = {-g[0], -g[1]};
     for (int k = 0; k < nv; k++) {
       const T yk = wread(y, k) * wread(rdiag, k);
@@ -363,7 +363,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
       for (int wd2 = 0; wd2 < 2; wd2++) {
         const int i = 64 * wd2 + l;
         if (i == k) y[wd2] = yk;
-        else if (i < nv && i > k) y[wd2] -= H[i * nv + k] * yk;
+        else if (i < nv && i > k) y[wd2] -= H[hidx<true>(i, k, nv)] * yk;
       }
     }
     T p[2] = {y[0], y[1]};
@@ -373,7 +373,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
       for (int wd2 = 0; wd2 < 2; wd2++) {
         const int i = 64 * wd2 + l;
         if (i == k) p[wd2] = pk;
-        else if (i < k) p[wd2] -= H[k * nv + i] * pk;
+        else if (i < k) p[wd2] -= H[hidx<true>(k, i, nv)] * pk;
       }
     }
     p[0] = dl[0] ? p[0] : (T)0;
