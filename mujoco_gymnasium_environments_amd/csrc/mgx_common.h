@@ -49,6 +49,8 @@ struct Layout {
   // as a packed lower triangle, row i at i (i + 1) / 2 (hpk) — with both, humanoid_construction's
   // per-env LDS fits two envs per CU
   int gB_efc, gB_efm, hpk;
+  // wide kernels' helper wave (mgx_wide.h team_*): the section command words (ints)
+  int team;
   // gB only: rows per chunk staged into the (dead) phase-A union region for the row transform
   int tchunk;
   // Newton solver (solver == mjSOL_NEWTON, monolithic kernels only): nv x nv Hessian
@@ -134,7 +136,7 @@ static __device__ unsigned long long* g_mgx_prof = nullptr;
 #endif
 
 // ------------------------------------------------------------------ wave helpers
-__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }  // one env = wave 0 (+ helpers)
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
 __device__ __forceinline__ float readlane(float x, int l) {

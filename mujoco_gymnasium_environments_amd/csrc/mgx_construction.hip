@@ -22,9 +22,11 @@ __device__ __forceinline__ void bind(const DevModel<T>& m, WEnv<T>& w, char* sme
   wenv_bind<T>(m, w, smem, (T*)s.scratch + (size_t)env * m.L.gB_stride);
 }
 
-// MODE 0: one env step (+ same-step autoreset); MODE 1: reset (host draws or Philox)
+// MODE 0: one env step (+ same-step autoreset), four waves per env (wave 0 + the Newton helper
+// waves, mgx_wide.h team_helper); MODE 1: reset (host draws or Philox), one wave
+constexpr int kTeamThreads = 128;  // two waves: the kernel needs all 512 registers of a wave (one wave per SIMD)
 template <typename T, int MODE>
-__global__ void __launch_bounds__(64) k_construction(DevModel<T> m, ConstructionIds ids, mgx_state s,
+__global__ void __launch_bounds__(MODE == 0 ? kTeamThreads : 64) k_construction(DevModel<T> m, ConstructionIds ids, mgx_state s,
                                                      mgx_construction_env ce, const float* action, const T* draws,
                                                      float* obs, double* reward, uint8_t* terminated,
                                                      uint8_t* truncated, float* final_obs, int autoreset,
@@ -35,6 +37,13 @@ __global__ void __launch_bounds__(64) k_construction(DevModel<T> m, Construction
   if (mask && !mask[env]) return;
   WEnv<T> w;
   bind(m, w, smem, s, env);
+  if constexpr (MODE == 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0) {  // helper waves
+      team_helper(m, w);
+      return;
+    }
+  }
+  team_init(w);
   Env<T>& e = w.e;
   const int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
@@ -79,6 +88,7 @@ __global__ void __launch_bounds__(64) k_construction(DevModel<T> m, Construction
     if (s.warning) s.warning[env] += warn;
     if (s.overflow && e.overflow) s.overflow[env] += 1;
   }
+  team_exit(w);
 }
 
 // env-logic-only test hook: state from the caller (golden vectors), no physics
@@ -104,14 +114,19 @@ __global__ void __launch_bounds__(64) k_construction_logic(DevModel<T> m, Constr
 
 // generic wide-model physics: nsub mj_steps (mgx_step for models with nv > 64)
 template <typename T>
-__global__ void __launch_bounds__(64) k_wide_step(DevModel<T> m, mgx_state s, mgx_frames fr, int n_env, int nsub,
-                                                  const uint8_t* mask) {
+__global__ void __launch_bounds__(kTeamThreads) k_wide_step(DevModel<T> m, mgx_state s, mgx_frames fr, int n_env,
+                                                            int nsub, const uint8_t* mask) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
   if (env >= n_env) return;
   if (mask && !mask[env]) return;
   WEnv<T> w;
   bind(m, w, smem, s, env);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0) {
+    team_helper(m, w);
+    return;
+  }
+  team_init(w);
   Env<T>& e = w.e;
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
@@ -132,6 +147,7 @@ __global__ void __launch_bounds__(64) k_wide_step(DevModel<T> m, mgx_state s, mg
     if (fr.nefc) fr.nefc[env] = e.nefc;
     if (fr.niter) fr.niter[env] = e.niter;
   }
+  team_exit(w);
 }
 
 // Debug dump of one wide forward pass (mgx_debug_forward's layout, DbgOff in mgx_internal.h)
@@ -186,7 +202,8 @@ __global__ void __launch_bounds__(64) k_wide_debug(DevModel<T> m, mgx_state s, i
   }
   wsync();
   if (MGX_TRANSFORM_LANE_ROW) transform_rows<T, true>(m, e);
-  else wtransform_rows(m, w);  // as wforward
+  else wtransform_rows(m, w, __builtin_amdgcn_readfirstlane(e.nefc), 0, 1);  // as wforward
+  wsync();
   wsync();
   for (int r = l; r < e.nefc; r += 64)
     for (int k = 0; k < m.nv; k++) D[o.Bmat + r * m.nv + k] = e.Bm[r * e.Bs + k];
@@ -224,7 +241,7 @@ void launch(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const 
             const float* action, const T* draws, float* obs, double* reward, uint8_t* term, uint8_t* trunc,
             float* final_obs, int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t* mask,
             hipStream_t st) {
-  hipLaunchKernelGGL((k_construction<T, MODE>), dim3(n_env), dim3(64), m->L.bytes, st, M, m->cn, *s, *e, action, draws,
+  hipLaunchKernelGGL((k_construction<T, MODE>), dim3(n_env), dim3(MODE == 0 ? kTeamThreads : 64), m->L.bytes, st, M, m->cn, *s, *e, action, draws,
                      obs, reward, term, trunc, final_obs, autoreset, seed, env_offset, n_env, mask);
 }
 
@@ -247,9 +264,9 @@ int wide_step(const mgx_model* m, const mgx_state* s, const mgx_frames& fr, int 
   int rc = wide_supported(m);
   if (rc) return rc;
   if (m->precision == MGX_F32)
-    hipLaunchKernelGGL(k_wide_step<float>, dim3(n_env), dim3(64), m->L.bytes, st, m->mf, *s, fr, n_env, nsub, mask);
+    hipLaunchKernelGGL(k_wide_step<float>, dim3(n_env), dim3(kTeamThreads), m->L.bytes, st, m->mf, *s, fr, n_env, nsub, mask);
   else
-    hipLaunchKernelGGL(k_wide_step<double>, dim3(n_env), dim3(64), m->L.bytes, st, m->md, *s, fr, n_env, nsub, mask);
+    hipLaunchKernelGGL(k_wide_step<double>, dim3(n_env), dim3(kTeamThreads), m->L.bytes, st, m->md, *s, fr, n_env, nsub, mask);
   MGX_HIPCHK(hipGetLastError());
   return MGX_OK;
 }

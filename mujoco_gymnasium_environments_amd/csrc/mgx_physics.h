@@ -1141,90 +1141,113 @@ __device__ __forceinline__ int hidx(int r, int c, int nv) {
   return PK ? (r * (r + 1) >> 1) + c : r * nv + c;
 }
 
-template <typename T, bool PK = false>
-__device__ __forceinline__ void chol_blocked(T* H, int nv) {
-  typedef T V4 __attribute__((ext_vector_type(4)));
+// 1. diagonal block kb in registers: lane i < bk holds row k0 + i of the block (16 entries), the
+//    factor is right-looking over the block's columns with the column values broadcast by
+//    readlane — no LDS round trip or wave barrier per column. Entry (i, c) receives the same
+//    products in the same order as the left-looking dot s = a_ic - sum_{j<c} l_ij l_cj.
+template <typename T, bool PK>
+__device__ __forceinline__ void chol_diag(T* H, int nv, int kb) {
   const int l = lane_id();
-  const int nb = (nv + 15) >> 4;
-  for (int kb = 0; kb < nb; kb++) {
-    const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
-    // 1. diagonal block in registers: lane i < bk holds row k0 + i of the block (16 entries), the
-    //    factor is right-looking over the block's columns with the column values broadcast by
-    //    readlane — no LDS round trip or wave barrier per column. Entry (i, c) receives the same
-    //    products in the same order as the left-looking dot s = a_ic - sum_{j<c} l_ij l_cj.
-    {
-      T x[16];
-      const T* Lr = H + hidx<PK>(k0 + (l < bk ? l : 0), k0, nv);
+  const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
+  T x[16];
+  const T* Lr = H + hidx<PK>(k0 + (l < bk ? l : 0), k0, nv);
 #pragma unroll
-      for (int j = 0; j < 16; j++) x[j] = (l < bk && j <= l) ? Lr[j] : (T)0;
+  for (int j = 0; j < 16; j++) x[j] = (l < bk && j <= l) ? Lr[j] : (T)0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    if (c < bk) {
+      const T dkk = readlane(x[c], c);
+      const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
+      x[c] = l == c ? d : (l > c ? x[c] / d : x[c]);
+      const T lic = x[c];
+#pragma unroll
+      for (int j = c + 1; j < 16; j++)
+        if (j < bk && l >= j) x[j] -= lic * readlane(x[c], j);
+    }
+  }
+  T* Hr = H + hidx<PK>(k0 + (l < bk ? l : 0), k0, nv);
+  if (l < bk)
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (j <= l) Hr[j] = x[j];
+}
+
+// 2. panel of block column kb: rows below the block, x = a L_kk^-T by forward substitution (lane =
+//    row); row sets j = j0, j0 + js, ... of 64 rows each (one wave: all of them)
+template <typename T, bool PK>
+__device__ __forceinline__ void chol_panel(T* H, int nv, int kb, int j0, int js) {
+  const int l = lane_id();
+  const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
+  for (int rb = k0 + bk + 64 * j0; rb < nv; rb += 64 * js) {
+    const int r = rb + l;
+    if (r < nv) {
+      T* Ar = H + hidx<PK>(r, k0, nv);
+      T x[16];
 #pragma unroll
       for (int c = 0; c < 16; c++) {
         if (c < bk) {
-          const T dkk = readlane(x[c], c);
-          const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
-          x[c] = l == c ? d : (l > c ? x[c] / d : x[c]);
-          const T lic = x[c];
+          T t = Ar[c];
 #pragma unroll
-          for (int j = c + 1; j < 16; j++)
-            if (j < bk && l >= j) x[j] -= lic * readlane(x[c], j);
+          for (int j = 0; j < c; j++) t -= x[j] * H[hidx<PK>(k0 + c, k0 + j, nv)];
+          x[c] = t / H[hidx<PK>(k0 + c, k0 + c, nv)];
         }
       }
-      T* Hr = H + hidx<PK>(k0 + (l < bk ? l : 0), k0, nv);
-      if (l < bk)
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-          if (j <= l) Hr[j] = x[j];
-      wsync();
+      for (int c = 0; c < 16; c++)
+        if (c < bk) Ar[c] = x[c];
     }
-    // 2. panel: rows below the block, x = a L_kk^-T by forward substitution (lane = row)
-    for (int r = k0 + bk + l; r < nv + 64 && r - l < nv; r += 64) {
-      if (r < nv) {
-        T* Ar = H + hidx<PK>(r, k0, nv);
-        T x[16];
+  }
+}
+
+// 3. trailing lower tiles (I, J), kb < J <= I < nb: A_IJ -= L_Ik L_Jk' on MFMA; tiles q0, q0 + qs,
+//    ... in (I, J) order (one wave: all of them)
+template <typename T, bool PK>
+__device__ __forceinline__ void chol_trail(T* H, int nv, int kb, int q0, int qs) {
+  typedef T V4 __attribute__((ext_vector_type(4)));
+  const int l = lane_id();
+  const int nb = (nv + 15) >> 4;
+  const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
+  const int i = l & 15, kq = l >> 4;
+  auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
+  int q = 0;
+  for (int I = kb + 1; I < nb; I++) {
+    for (int J = kb + 1; J <= I; J++, q++) {
+      if (q < q0 || (q - q0) % qs) continue;
+      V4 acc;
 #pragma unroll
-        for (int c = 0; c < 16; c++) {
-          if (c < bk) {
-            T t = Ar[c];
+      for (int v = 0; v < 4; v++) {
+        const int row = 16 * I + row_of(v), col = 16 * J + i;
+        acc[v] = (row < nv && col <= row) ? H[hidx<PK>(row, col, nv)] : (T)0;
+      }
 #pragma unroll
-            for (int j = 0; j < c; j++) t -= x[j] * H[hidx<PK>(k0 + c, k0 + j, nv)];
-            x[c] = t / H[hidx<PK>(k0 + c, k0 + c, nv)];
-          }
-        }
+      for (int u = 0; u < 4; u++) {
+        const int kk = k0 + 4 * u + kq;  // this lane's k in the 16-wide block column
+        const int ra = 16 * I + i, rb = 16 * J + i;
+        const T a = (ra < nv && kk < k0 + bk) ? -H[hidx<PK>(ra, kk, nv)] : (T)0;
+        const T b = (rb < nv && kk < k0 + bk) ? H[hidx<PK>(rb, kk, nv)] : (T)0;
+        if constexpr (sizeof(T) == 8)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        else
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      }
 #pragma unroll
-        for (int c = 0; c < 16; c++)
-          if (c < bk) Ar[c] = x[c];
+      for (int v = 0; v < 4; v++) {
+        const int row = 16 * I + row_of(v), col = 16 * J + i;
+        if (row < nv && col <= row) H[hidx<PK>(row, col, nv)] = acc[v];
       }
     }
+  }
+}
+
+template <typename T, bool PK = false>
+__device__ __forceinline__ void chol_blocked(T* H, int nv) {
+  const int nb = (nv + 15) >> 4;
+  for (int kb = 0; kb < nb; kb++) {
+    chol_diag<T, PK>(H, nv, kb);
     wsync();
-    // 3. trailing lower tiles (I, J), kb < J <= I < nb: A_IJ -= L_Ik L_Jk' on MFMA
-    const int i = l & 15, kq = l >> 4;
-    auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
-    for (int I = kb + 1; I < nb; I++) {
-      for (int J = kb + 1; J <= I; J++) {
-        V4 acc;
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-          const int row = 16 * I + row_of(v), col = 16 * J + i;
-          acc[v] = (row < nv && col <= row) ? H[hidx<PK>(row, col, nv)] : (T)0;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int kk = k0 + 4 * q + kq;  // this lane's k in the 16-wide block column
-          const int ra = 16 * I + i, rb = 16 * J + i;
-          const T a = (ra < nv && kk < k0 + bk) ? -H[hidx<PK>(ra, kk, nv)] : (T)0;
-          const T b = (rb < nv && kk < k0 + bk) ? H[hidx<PK>(rb, kk, nv)] : (T)0;
-          if constexpr (sizeof(T) == 8)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-          else
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-          const int row = 16 * I + row_of(v), col = 16 * J + i;
-          if (row < nv && col <= row) H[hidx<PK>(row, col, nv)] = acc[v];
-        }
-      }
-    }
+    chol_panel<T, PK>(H, nv, kb, 0, 1);
+    wsync();
+    chol_trail<T, PK>(H, nv, kb, 0, 1);
     wsync();
   }
 }

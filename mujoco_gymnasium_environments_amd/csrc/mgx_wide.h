@@ -24,6 +24,8 @@ struct WEnv {
   T qacc_ws[2], qfrc_applied[2], qfrc_smooth[2], qacc_smooth[2], qacc[2], qfrc_constraint[2], diaginv[2];
   int chainlen[2], madr[2];
   uint64_t anc_lo[2], anc_hi[2];  // strict ancestors of dof 64 w + lane among dofs 0..63 / 64..127
+  int nw;    // waves per env: 1, or 2 (wave 0 + the helper, team_helper)
+  int* ctl;  // helper section command words (Layout.team)
 };
 
 __device__ __forceinline__ int wdof(int w) { return 64 * w + lane_id(); }
@@ -41,6 +43,8 @@ __device__ __forceinline__ T wdot(const T (&a)[2], const T (&b)[2]) {
 template <typename T>
 __device__ __forceinline__ void wenv_bind(const DevModel<T>& m, WEnv<T>& w, char* smem, T* gB) {
   env_bind<T, true, true>(m, w.e, smem, gB);
+  w.nw = blockDim.x >> 6;
+  w.ctl = reinterpret_cast<int*>(reinterpret_cast<T*>(smem) + m.L.reals) + m.L.team;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int d = wdof(k);
@@ -177,6 +181,42 @@ __device__ __forceinline__ void wsolve_M(const DevModel<T>& m, const WEnv<T>& w,
   wsolve_L(m, w, LD, x);
 }
 
+// ---------------------------------------------------------------- helper waves
+// k_construction (step) and k_wide_step run two waves per env (the kernels use all 512 registers of
+// a wave, so one wave per SIMD; two envs per CU by LDS): wave 0 executes the step (every stage of
+// this file), wave 1 waits in team_helper and takes shares of the row- and tile-parallel
+// passes of the Newton solver (MFMA Hessian tile-row passes, J p, gradient, Cholesky panel and
+// trailing update) and of the row transform. Every wsync() of wave 0 is a workgroup barrier that
+// the helpers consume; a section is: wave 0 posts the command in LDS -> barrier -> every wave runs
+// its share (no barriers inside) -> barrier -> wave 0 clears the command. Shares split the same
+// loops by chunk (chunk c to wave c mod nw), so a one-wave launch (nw = 1: the debug kernel, the
+// reset) runs the identical code with every chunk on wave 0 and the same results.
+enum { TEAM_NONE = 0, TEAM_EXIT = 1, TEAM_HESS, TEAM_PANEL, TEAM_TRAIL, TEAM_JP, TEAM_GRAD, TEAM_XFORM };
+
+template <typename T>
+__device__ __forceinline__ void team_begin(WEnv<T>& w, int cmd, int arg) {
+  if (w.nw > 1 && lane_id() == 0) { w.ctl[0] = cmd; w.ctl[1] = arg; }
+  wsync();
+}
+template <typename T>
+__device__ __forceinline__ void team_end(WEnv<T>& w) {
+  wsync();
+  if (w.nw > 1 && lane_id() == 0) w.ctl[0] = TEAM_NONE;
+}
+// wave 0, before its first wsync: the helpers read the command word after every barrier
+template <typename T>
+__device__ __forceinline__ void team_init(WEnv<T>& w) {
+  if (w.nw > 1 && lane_id() == 0) w.ctl[0] = TEAM_NONE;
+}
+// wave 0, at the end of the kernel (every path): releases the helpers
+template <typename T>
+__device__ __forceinline__ void team_exit(WEnv<T>& w) {
+  if (w.nw > 1) {
+    if (lane_id() == 0) w.ctl[0] = TEAM_EXIT;
+    wsync();
+  }
+}
+
 // ---------------------------------------------------------------- Newton Hessian on MFMA
 // H = I + sum_{x_r<0} D_r B_r B_r' for nv <= 128 (8 tile rows of 16): the lower tiles of tile
 // rows [T0, T1) per pass, so the accumulators of one pass stay in registers (hessian_mfma's
@@ -206,7 +246,7 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
 #pragma unroll
     for (int t = 0; t < T1; t++) {
       const int c = 16 * t + i;
-      b[t] = (r < ne && c < nv) ? Bm[r * Bs + c] : (T)0;
+      b[t] = (sc != (T)0 && c < nv) ? Bm[r * Bs + c] : (T)0;  // inactive rows: not streamed
     }
   };
   T bn[T1], sn;
@@ -217,6 +257,7 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
     for (int t = 0; t < T1; t++) b[t] = bn[t];
     const T sc = sn;
     load(r0 + 4, bn, sn);
+    if (__ballot(sc != (T)0) == 0ull) continue;  // four inactive rows: no MFMAs
 #pragma unroll
     for (int t = T0, q = 0; t < T1; t++)
 #pragma unroll
@@ -240,12 +281,92 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
       }
 }
 
+// pass q of the four to wave q mod nw
 template <typename T>
-__device__ __forceinline__ void whessian(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
-  whess_pass<T, 0, 4>(Bm, Bs, efc, ne, nv, H);  // 10 tiles
-  whess_pass<T, 4, 6>(Bm, Bs, efc, ne, nv, H);  // 11 tiles
-  whess_pass<T, 6, 7>(Bm, Bs, efc, ne, nv, H);  // 7 tiles
-  whess_pass<T, 7, 8>(Bm, Bs, efc, ne, nv, H);  // 8 tiles
+__device__ __forceinline__ void whess_share(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H, int wv, int nw) {
+  for (int q = wv; q < 4; q += nw) {
+    if (q == 0) whess_pass<T, 0, 4>(Bm, Bs, efc, ne, nv, H);       // 10 tiles
+    else if (q == 1) whess_pass<T, 4, 6>(Bm, Bs, efc, ne, nv, H);  // 11 tiles
+    else if (q == 2) whess_pass<T, 6, 7>(Bm, Bs, efc, ne, nv, H);  // 7 tiles
+    else whess_pass<T, 7, 8>(Bm, Bs, efc, ne, nv, H);              // 8 tiles
+  }
+}
+
+// blocked Cholesky of the packed H (chol_blocked's pieces): diagonal block on wave 0, the panel's
+// 64-row sets and the trailing tiles shared
+template <typename T>
+__device__ __forceinline__ void wchol(WEnv<T>& w, T* H, int nv) {
+  const int nb = (nv + 15) >> 4;
+  for (int kb = 0; kb < nb; kb++) {
+    chol_diag<T, true>(H, nv, kb);
+    team_begin(w, TEAM_PANEL, kb);
+    chol_panel<T, true>(H, nv, kb, 0, w.nw);
+    team_end(w);
+    if (kb + 1 < nb) {
+      team_begin(w, TEAM_TRAIL, kb);
+      chol_trail<T, true>(H, nv, kb, 0, w.nw);
+      team_end(w);
+    }
+  }
+}
+
+// J p for the rows of chunks c0, c0 + cs, ... (MGX_RB rows each); lane 0 stores efc[8 r + 3]
+template <typename T>
+__device__ __forceinline__ void wjp_share(const Env<T>& e, int nv, int ne, const T (&p)[2], int c0, int cs) {
+  const int l = lane_id();
+  const bool dl[2] = {l < nv, 64 + l < nv};
+  const int lc[2] = {dl[0] ? l : 0, dl[1] ? 64 + l : 0};
+  T* efc = e.efc;
+  for (int r0 = MGX_RB * c0; r0 < ne; r0 += MGX_RB * cs) {
+    T xa[MGX_RB], xb[MGX_RB];
+    load_rows(xa, e.Bm, e.Bs, r0, ne, lc[0], dl[0]);
+    load_rows(xb, e.Bm, e.Bs, r0, ne, lc[1], dl[1]);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j += 4) {
+      T s0 = xa[j] * p[0] + xb[j] * p[1], s1 = xa[j + 1] * p[0] + xb[j + 1] * p[1];
+      T s2 = xa[j + 2] * p[0] + xb[j + 2] * p[1], s3 = xa[j + 3] * p[0] + xb[j + 3] * p[1];
+      wave_sum4(s0, s1, s2, s3);
+      if (l == 0) {
+        if (r0 + j < ne) efc[8 * (r0 + j) + 3] = s0;
+        if (r0 + j + 1 < ne) efc[8 * (r0 + j + 1) + 3] = s1;
+        if (r0 + j + 2 < ne) efc[8 * (r0 + j + 2) + 3] = s2;
+        if (r0 + j + 3 < ne) efc[8 * (r0 + j + 3) + 3] = s3;
+      }
+    }
+  }
+}
+
+// sum_{x<0} D x B_r over the rows of chunks c0, c0 + cs, ...: only active rows are loaded
+template <typename T>
+__device__ __forceinline__ void wgrad_share(const Env<T>& e, int nv, int ne, int c0, int cs, T (&gg)[2]) {
+  const int l = lane_id();
+  const bool dl[2] = {l < nv, 64 + l < nv};
+  const T* efc = e.efc;
+  gg[0] = 0;
+  gg[1] = 0;
+  for (int r0 = MGX_RB * c0; r0 < ne; r0 += MGX_RB * cs) {
+    T xs[MGX_RB], sd[MGX_RB], xa[MGX_RB], xb[MGX_RB];
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      xs[j] = r < ne ? efc[8 * r + 1] : (T)0;
+      sd[j] = r < ne ? efc[8 * r + 4] : (T)0;
+    }
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      xa[j] = (xs[j] < 0 && dl[0]) ? e.Bm[r * e.Bs + l] : (T)0;
+      xb[j] = (xs[j] < 0 && dl[1]) ? e.Bm[r * e.Bs + 64 + l] : (T)0;
+    }
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      if (xs[j] < 0) {
+        const T s = sd[j] * xs[j];
+        gg[0] += s * xa[j];
+        gg[1] += s * xb[j];
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- Newton (mj_solNewton)
@@ -318,39 +439,32 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   const T eps = sizeof(T) == 4 ? (T)1e-7 : (T)1e-15;
   const int maxit = m.iterations;
   int iter = 0;
-  // whitened gradient g = u + sum_{x<0} D x B_r
+  // whitened gradient g = u + sum_{x<0} D x B_r as two partial sums over alternating row chunks
+  // (even chunks on wave 0, odd chunks on the helper, its sum via vec1), added in that order with
+  // one wave or two — the result does not depend on the launch's wave count
   auto gradient = [&](T (&gg)[2]) {
-    gg[0] = u[0];
-    gg[1] = u[1];
-    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-      T xa[MGX_RB], xb[MGX_RB];
-      load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
-      load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
-#pragma unroll
-      for (int j = 0; j < MGX_RB; j++) {
-        const int r = r0 + j;
-        if (r < ne) {
-          const T xr = efc[8 * r + 1];
-          if (xr < 0) {
-            const T s = efc[8 * r + 4] * xr;
-            gg[0] += s * xa[j];
-            gg[1] += s * xb[j];
-          }
-        }
-      }
+    T part[2], odd[2];
+    team_begin(w, TEAM_GRAD, ne);
+    wgrad_share(e, nv, ne, 0, 2, part);
+    if (w.nw == 1) wgrad_share(e, nv, ne, 1, 2, odd);
+    team_end(w);
+    if (w.nw > 1) {
+      odd[0] = dl[0] ? e.vec1[l] : (T)0;
+      odd[1] = dl[1] ? e.vec1[64 + l] : (T)0;
     }
-    gg[0] = dl[0] ? gg[0] : (T)0;
-    gg[1] = dl[1] ? gg[1] : (T)0;
+    gg[0] = dl[0] ? u[0] + part[0] + odd[0] : (T)0;
+    gg[1] = dl[1] ? u[1] + part[1] + odd[1] : (T)0;
   };
   T g[2];
   gradient(g);
   MGX_STAMP_DECL
   MGX_STAMP(10);  // setup
   while (iter < maxit) {
-    whessian(Bm, Bs, efc, ne, nv, H);
-    wsync();
+    team_begin(w, TEAM_HESS, ne);
+    whess_share(Bm, Bs, efc, ne, nv, H, 0, w.nw);
+    team_end(w);
     MGX_STAMP(11);  // Hessian
-    chol_blocked<T, true>(H, nv);
+    wchol(w, H, nv);
     MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y
     T rdiag[2];
@@ -379,25 +493,14 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     p[0] = dl[0] ? p[0] : (T)0;
     p[1] = dl[1] ? p[1] : (T)0;
     MGX_STAMP(13);  // triangular solves
-    // J p per row (row-major, wave reductions); lane 0 stores
-    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-      T xa[MGX_RB], xb[MGX_RB];
-      load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
-      load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
-#pragma unroll
-      for (int j = 0; j < MGX_RB; j += 4) {
-        T s0 = xa[j] * p[0] + xb[j] * p[1], s1 = xa[j + 1] * p[0] + xb[j + 1] * p[1];
-        T s2 = xa[j + 2] * p[0] + xb[j + 2] * p[1], s3 = xa[j + 3] * p[0] + xb[j + 3] * p[1];
-        wave_sum4(s0, s1, s2, s3);
-        if (l == 0) {
-          if (r0 + j < ne) efc[8 * (r0 + j) + 3] = s0;
-          if (r0 + j + 1 < ne) efc[8 * (r0 + j + 1) + 3] = s1;
-          if (r0 + j + 2 < ne) efc[8 * (r0 + j + 2) + 3] = s2;
-          if (r0 + j + 3 < ne) efc[8 * (r0 + j + 3) + 3] = s3;
-        }
-      }
+    // J p per row (row-major, wave reductions; row chunks shared, p to the helpers in vec0)
+    if (w.nw > 1) {
+      if (dl[0]) e.vec0[l] = p[0];
+      if (dl[1]) e.vec0[64 + l] = p[1];
     }
-    wsync();
+    team_begin(w, TEAM_JP, ne);
+    wjp_share(e, nv, ne, p, 0, w.nw);
+    team_end(w);
     MGX_STAMP(14);  // J p
     // line search (newton(), mgx_physics.h: MuJoCo's stop rule)
     const T g0 = wdot(u, p), pp = wdot(p, p);
@@ -493,16 +596,16 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
 // B_r = D^-1/2 L'^-1 J_r' in place, four rows at a time, row-major with two dofs per lane (the
 // narrow transform_rows_rm with two-word rows): a readlane sweep over the rows' dof support
 // (128-bit, ancestors joining as their descendants are reached), highest dof first.
+// Chunks of four rows c0, c0 + cs, ... (the helper-wave share); the caller synchronises.
 template <typename T>
-__device__ __forceinline__ void wtransform_rows(const DevModel<T>& m, WEnv<T>& w) {
+__device__ __forceinline__ void wtransform_rows(const DevModel<T>& m, WEnv<T>& w, int ne, int c0, int cs) {
   Env<T>& e = w.e;
   const int l = lane_id(), nv = m.nv;
-  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
   const bool v0 = l < nv, v1 = 64 + l < nv;
   T* Bm = e.Bm;
   const int Bs = e.Bs;
   const T s0 = v0 ? e.vec0[l] : (T)0, s1 = v1 ? e.vec0[64 + l] : (T)0;
-  for (int r0 = 0; r0 < ne; r0 += 4) {
+  for (int r0 = 4 * c0; r0 < ne; r0 += 4 * cs) {
     T x[4][2];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -536,7 +639,6 @@ __device__ __forceinline__ void wtransform_rows(const DevModel<T>& m, WEnv<T>& w
       }
     }
   }
-  wsync();
 }
 
 template <typename T>
@@ -574,8 +676,14 @@ __device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
     if (d < m.nv) e.vec0[d] = sqrt(w.diaginv[k]);
   }
   wsync();
-  if (MGX_TRANSFORM_LANE_ROW) transform_rows<T, true>(m, e);
-  else wtransform_rows(m, w);
+  if (MGX_TRANSFORM_LANE_ROW) {
+    transform_rows<T, true>(m, e);
+  } else {
+    const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+    team_begin(w, TEAM_XFORM, ne);
+    wtransform_rows(m, w, ne, 0, w.nw);
+    team_end(w);
+  }
   MGX_STAMP(7);
   wnewton(m, w);
   MGX_STAMP(8);
@@ -665,6 +773,40 @@ __device__ __forceinline__ int wmj_step(const DevModel<T>& m, WEnv<T>& w) {
   }
   wrk4(m, w);
   return warn;
+}
+
+// wave 1 of a two-wave env: one loop iteration per barrier of wave 0 (TEAM_NONE), a share per
+// posted section, until wave 0 posts TEAM_EXIT
+template <typename T>
+__device__ __forceinline__ void team_helper(const DevModel<T>& m, WEnv<T>& w) {
+  Env<T>& e = w.e;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l = lane_id(), nv = m.nv;
+  for (;;) {
+    __syncthreads();
+    const int cmd = __builtin_amdgcn_readfirstlane(w.ctl[0]);
+    if (cmd == TEAM_NONE) continue;
+    if (cmd == TEAM_EXIT) break;
+    const int a = __builtin_amdgcn_readfirstlane(w.ctl[1]);
+    if (cmd == TEAM_HESS) {
+      whess_share(e.Bm, e.Bs, e.efc, a, nv, e.hess, wv, w.nw);
+    } else if (cmd == TEAM_PANEL) {
+      chol_panel<T, true>(e.hess, nv, a, wv, w.nw);
+    } else if (cmd == TEAM_TRAIL) {
+      chol_trail<T, true>(e.hess, nv, a, wv, w.nw);
+    } else if (cmd == TEAM_JP) {
+      const T p[2] = {l < nv ? e.vec0[l] : (T)0, 64 + l < nv ? e.vec0[64 + l] : (T)0};
+      wjp_share(e, nv, a, p, wv, w.nw);
+    } else if (cmd == TEAM_GRAD) {  // the odd chunks (wnewton's gradient)
+      T g[2];
+      wgrad_share(e, nv, a, 1, 2, g);
+      e.vec1[l] = g[0];
+      e.vec1[64 + l] = g[1];
+    } else if (cmd == TEAM_XFORM) {
+      wtransform_rows(m, w, a, wv, w.nw);
+    }
+    __syncthreads();
+  }
 }
 
 }  // namespace mgx
