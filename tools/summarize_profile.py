@@ -89,9 +89,10 @@ def main(out, tag):
             b = json.loads(line[-1])
             shutil.copy(bj, os.path.join(summ, f"{tag}_bench_under_rocprof.json"))
             res["bench_step_ms_same_run"] = b["roofline"]["launch_ms"]
-            res["envs"] = b["config"]["envs_per_gpu"]
+            res["envs"] = b["config"].get("envs_per_gpu", b["config"].get("envs_per_task"))
             res["precision"] = b["dtype"]
-            res["mode"] = b["config"].get("step_kernels", "staged")
+            # the mixed run (every task's step kernels on four streams): mode "mixed"
+            res["mode"] = "mixed" if "envs_per_task" in b["config"] else b["config"].get("step_kernels", "staged")
             res["task"] = b["config"]["workload"].split("_env")[0]
     fetch = counter_means(os.path.join(out, "pmc_fetch"), "FETCH_SIZE")
     write = counter_means(os.path.join(out, "pmc_write"), "WRITE_SIZE")
