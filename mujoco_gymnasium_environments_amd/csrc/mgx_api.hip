@@ -325,7 +325,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.act_list = takei(max_active);
   L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
   L.con_efcadr = takei(1);
-  L.team = nv > 64 ? takei(4) : 0;
+  L.team = d->solver == 2 ? takei(4) : 0;  // Newton models: the helper-wave command words
   L.ints = q;
   L.bytes = L.reals * real_bytes + L.ints * 4;
   (void)vec_end;

@@ -1,7 +1,10 @@
 // mgx_assembly.hip — robotic_arm_assembly kernels and their C-ABI (include/mgx.h).
 //
-// One 64-thread workgroup (= one wavefront) per environment, as the generic step kernel
-// (mgx_step.hip): an assembly env step is clip -> ctrl -> 10 mj_steps (Euler, Newton: the
+// One 128-thread workgroup per environment: wave 0 runs the step as the generic step kernel
+// (mgx_step.hip) does, wave 1 takes every other row batch of the Newton solver's passes (setup,
+// gradient, J p, forces), tile row 3 of its MFMA Hessian and half of the Cholesky trailing tiles
+// (mgx_physics.h team_helper_n; the kernel uses all 512 registers of a wave, so two envs per CU
+// put one wave on each SIMD). An assembly env step is clip -> ctrl -> 10 mj_steps (Euler, Newton: the
 // nv x nv Hessian and its Cholesky factor in the env's LDS; constraint rows in LDS or, when the
 // scene's ~300 rows do not fit next to the rest, in per-env global scratch) -> gripper-contact
 // task state / reward / termination / observation, with same-step autoreset (10 settle steps),
@@ -25,8 +28,9 @@ __device__ __forceinline__ void bind(const DevModel<T>& m, Env<T>& e, char* smem
 // MODE 0: one env step (10 substeps; ended envs then reset in the same launch when autoreset);
 // MODE 1: reset. ONE physics call site: the step's substeps and a reset's settle steps share
 // the loop below, so the Newton forward pass is inlined once.
+constexpr int kTeamThreads = 128;  // wave 0 + the Newton helper wave (mgx_physics.h team_helper_n)
 template <typename T, int MODE, bool GB>
-__global__ void __launch_bounds__(64) k_assembly(DevModel<T> m, mgx_assembly_ids ids, mgx_state s, mgx_assembly_env ae,
+__global__ void __launch_bounds__(kTeamThreads) k_assembly(DevModel<T> m, mgx_assembly_ids ids, mgx_state s, mgx_assembly_env ae,
                                                  const float* action, float* obs, double* reward, uint8_t* terminated,
                                                  uint8_t* truncated, float* final_obs, int autoreset, int n_env,
                                                  const uint8_t* mask) {
@@ -36,6 +40,11 @@ __global__ void __launch_bounds__(64) k_assembly(DevModel<T> m, mgx_assembly_ids
   if (mask && !mask[env]) return;
   Env<T> e;
   bind<T, GB>(m, e, smem, s, env);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0) {  // the helper wave
+    team_helper_n(m, e);
+    return;
+  }
+  team_init(e);
   const int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
@@ -75,6 +84,7 @@ __global__ void __launch_bounds__(64) k_assembly(DevModel<T> m, mgx_assembly_ids
     if (s.warning) s.warning[env] += warn;
     if (s.overflow && e.overflow) s.overflow[env] += 1;
   }
+  team_exit(e);
 }
 
 // env-logic-only test hook: frames and contact lists from the caller (golden vectors)
@@ -119,10 +129,10 @@ void launch(const mgx_model* m, const DevModel<T>& M, const mgx_state* s, const 
             float* obs, double* reward, uint8_t* term, uint8_t* trunc, float* final_obs, int autoreset, int n_env,
             const uint8_t* mask, hipStream_t st) {
   if (m->L.gB)
-    hipLaunchKernelGGL((k_assembly<T, MODE, true>), dim3(n_env), dim3(64), m->L.bytes, st, M, m->as, *s, *e, action,
+    hipLaunchKernelGGL((k_assembly<T, MODE, true>), dim3(n_env), dim3(kTeamThreads), m->L.bytes, st, M, m->as, *s, *e, action,
                        obs, reward, term, trunc, final_obs, autoreset, n_env, mask);
   else
-    hipLaunchKernelGGL((k_assembly<T, MODE, false>), dim3(n_env), dim3(64), m->L.bytes, st, M, m->as, *s, *e, action,
+    hipLaunchKernelGGL((k_assembly<T, MODE, false>), dim3(n_env), dim3(kTeamThreads), m->L.bytes, st, M, m->as, *s, *e, action,
                        obs, reward, term, trunc, final_obs, autoreset, n_env, mask);
 }
 

@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(MODE == 0 ? kTeamThreads : 64) k_construction(
       return;
     }
   }
-  team_init(w);
+  team_init(w.e);
   Env<T>& e = w.e;
   const int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(MODE == 0 ? kTeamThreads : 64) k_construction(
     if (s.warning) s.warning[env] += warn;
     if (s.overflow && e.overflow) s.overflow[env] += 1;
   }
-  team_exit(w);
+  team_exit(w.e);
 }
 
 // env-logic-only test hook: state from the caller (golden vectors), no physics
@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(kTeamThreads) k_wide_step(DevModel<T> m, mgx_s
     team_helper(m, w);
     return;
   }
-  team_init(w);
+  team_init(w.e);
   Env<T>& e = w.e;
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(kTeamThreads) k_wide_step(DevModel<T> m, mgx_s
     if (fr.nefc) fr.nefc[env] = e.nefc;
     if (fr.niter) fr.niter[env] = e.niter;
   }
-  team_exit(w);
+  team_exit(w.e);
 }
 
 // Debug dump of one wide forward pass (mgx_debug_forward's layout, DbgOff in mgx_internal.h)

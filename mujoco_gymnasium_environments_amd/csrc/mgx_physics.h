@@ -31,6 +31,8 @@ struct Env {
   T *hess;  // Newton: nv x nv Hessian / its Cholesky factor (row-major, lower)
   int *con_geom, *con_pair, *act_list, *efc_type, *efc_id, *con_efcadr;
   int ncon, nefc, niter, overflow;
+  int nw;    // waves per env: 1, or 2 (wave 0 + a Newton helper wave, team_begin)
+  int* ctl;  // helper section command words (Layout.team)
   // dof-lane registers
   T qacc_ws, qfrc_applied, qfrc_smooth, qacc_smooth, qacc, qfrc_constraint, diaginv, time;
   int chainlen, madr;  // this lane's dof: chain length, dof_Madr
@@ -61,6 +63,8 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair;
   e.act_list = L.act_union > 0 ? reinterpret_cast<int*>(R + L.act_union) : I + L.act_list;
   e.efc_type = I + L.efc_type; e.con_efcadr = I + L.con_efcadr;
+  e.nw = blockDim.x >> 6;
+  e.ctl = I + L.team;
   // the staged row builder lists only its joint-limit rows, after collision, in the broadphase list
   e.efc_id = L.staged ? e.act_list : I + L.efc_id;
   // the staged row builder's carry tail lives in global memory (bind_carry_tail)
@@ -357,6 +361,65 @@ template <typename T>
 __device__ __forceinline__ void load_rows(T* x, const T* Bm, int Bs, int r0, int ne, int lc, bool dl) {
 #pragma unroll
   for (int j = 0; j < MGX_RB; j++) x[j] = (r0 + j < ne && dl) ? Bm[(r0 + j) * Bs + lc] : (T)0;
+}
+// Prefetched row batches: the next MGX_RD batches' loads are in flight while one is reduced
+// (a pass is otherwise one memory latency per batch; with B in global scratch, L2 misses).
+// xn holds batches r0 + MGX_RB, ... r0 + MGX_RD MGX_RB; next_rows hands out batch r0 and
+// issues r0 + (MGX_RD + 1) MGX_RB.
+#define MGX_RD 2
+#define MGX_HD 4  // Hessian passes: chunks of four rows in flight
+// Batches r0, r0 + step, ... (step = MGX_RB, or MGX_RB * waves when a helper wave takes every
+// other batch).
+template <typename T>
+__device__ __forceinline__ void first_rows(T (*xn)[MGX_RB], const T* Bm, int Bs, int ne, int lc, bool dl, int r0 = 0,
+                                           int step = MGX_RB) {
+#pragma unroll
+  for (int d = 0; d < MGX_RD; d++) load_rows(xn[d], Bm, Bs, r0 + d * step, ne, lc, dl);
+}
+template <typename T>
+__device__ __forceinline__ void next_rows(T* x, T (*xn)[MGX_RB], const T* Bm, int Bs, int r0, int ne, int lc, bool dl,
+                                          int step = MGX_RB) {
+#pragma unroll
+  for (int j = 0; j < MGX_RB; j++) x[j] = xn[0][j];
+#pragma unroll
+  for (int d = 0; d + 1 < MGX_RD; d++)
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) xn[d][j] = xn[d + 1][j];
+  load_rows(xn[MGX_RD - 1], Bm, Bs, r0 + MGX_RD * step, ne, lc, dl);
+}
+
+// ---------------------------------------------------------------- helper waves
+// The Newton kernels of assembly (narrow) and construction (mgx_wide.h) run two waves per env:
+// wave 0 executes the step, wave 1 waits in a helper loop (team_helper_n / team_helper) and takes
+// shares of the solver's row and tile passes. Every wsync() of wave 0 is a workgroup barrier the
+// helper consumes; a section is: wave 0 posts the command in LDS -> barrier -> every wave runs its
+// share (no barriers inside) -> barrier -> wave 0 clears the command. With one wave (nw = 1, every
+// other kernel) the sections are plain wave barriers and wave 0 runs every share itself.
+enum { TEAM_NONE = 0, TEAM_EXIT = 1, TEAM_HESS, TEAM_PANEL, TEAM_TRAIL, TEAM_JP, TEAM_GRAD, TEAM_XFORM, TEAM_SETUP,
+       TEAM_FORCE };
+
+template <typename T>
+__device__ __forceinline__ void team_begin(Env<T>& e, int cmd, int arg) {
+  if (e.nw > 1 && lane_id() == 0) { e.ctl[0] = cmd; e.ctl[1] = arg; }
+  wsync();
+}
+template <typename T>
+__device__ __forceinline__ void team_end(Env<T>& e) {
+  wsync();
+  if (e.nw > 1 && lane_id() == 0) e.ctl[0] = TEAM_NONE;
+}
+// wave 0, before its first wsync: the helper reads the command word after every barrier
+template <typename T>
+__device__ __forceinline__ void team_init(Env<T>& e) {
+  if (e.nw > 1 && lane_id() == 0) e.ctl[0] = TEAM_NONE;
+}
+// wave 0, at the end of the kernel (every path): releases the helper
+template <typename T>
+__device__ __forceinline__ void team_exit(Env<T>& e) {
+  if (e.nw > 1) {
+    if (lane_id() == 0) e.ctl[0] = TEAM_EXIT;
+    wsync();
+  }
 }
 
 template <typename T>
@@ -1069,15 +1132,17 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
 // nv <= 64. Lane l holds A[l&15][l>>4] / B[l>>4][l&15] (one element each, 4 loads per chunk, 16
 // consecutive columns of one row per 16 lanes); C/D: col = l&15, row = 4(l>>4)+v (f32) or
 // (l>>4)+4v (f64) (cdna_hip_programming.md, fragment layout).
-template <typename T>
+template <typename T, int T0 = 0, int T1 = 4>
 __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
   typedef T V4 __attribute__((ext_vector_type(4)));
   const int l = lane_id(), i = l & 15, kq = l >> 4;
   const int nt = (nv + 15) >> 4;
+  if (T0 >= nt) return;
   auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
-  V4 acc[10];
+  constexpr int NT = (T1 * (T1 + 1) - T0 * (T0 + 1)) / 2;  // tiles of tile rows [T0, T1)
+  V4 acc[NT];
 #pragma unroll
-  for (int t = 0, q = 0; t < 4; t++)
+  for (int t = T0, q = 0; t < T1; t++)
 #pragma unroll
     for (int u = 0; u <= t; u++, q++)
 #pragma unroll
@@ -1092,20 +1157,30 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
       sc = x < 0 ? efc[8 * r + 4] : (T)0;
     }
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
+    for (int t = 0; t < T1; t++) {
       const int c = 16 * t + i;
       b[t] = (sc != (T)0 && c < nv) ? Bm[r * Bs + c] : (T)0;
     }
   };
-  T bn[4], sn;
-  load(0, bn, sn);
+  // the next MGX_HD chunks are in flight during this chunk's MFMAs (B in global scratch: L2 misses)
+  T bq[MGX_HD][T1], sq[MGX_HD];
+#pragma unroll
+  for (int d = 0; d < MGX_HD; d++) load(4 * d, bq[d], sq[d]);
   for (int r0 = 0; r0 < ne; r0 += 4) {
-    T b[4] = {bn[0], bn[1], bn[2], bn[3]};
-    const T sc = sn;
-    load(r0 + 4, bn, sn);  // the next chunk is in flight during this chunk's MFMAs
+    T b[T1];
+#pragma unroll
+    for (int t = 0; t < T1; t++) b[t] = bq[0][t];
+    const T sc = sq[0];
+#pragma unroll
+    for (int d = 0; d + 1 < MGX_HD; d++) {
+      sq[d] = sq[d + 1];
+#pragma unroll
+      for (int t = 0; t < T1; t++) bq[d][t] = bq[d + 1][t];
+    }
+    load(r0 + 4 * MGX_HD, bq[MGX_HD - 1], sq[MGX_HD - 1]);
     if (__ballot(sc != (T)0) == 0ull) continue;
 #pragma unroll
-    for (int t = 0, q = 0; t < 4; t++)
+    for (int t = T0, q = 0; t < T1; t++)
 #pragma unroll
       for (int u = 0; u <= t; u++, q++) {
         if (t < nt) {
@@ -1117,7 +1192,7 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
       }
   }
 #pragma unroll
-  for (int t = 0, q = 0; t < 4; t++)
+  for (int t = T0, q = 0; t < T1; t++)
 #pragma unroll
     for (int u = 0; u <= t; u++, q++)
 #pragma unroll
@@ -1280,6 +1355,114 @@ __device__ __forceinline__ T row_cost_change(T x, T dx, T D) {
   return 0;
 }
 
+// newton()'s row passes over the batches b0, b0 + bs, ... of MGX_RB rows (bs = the wave count:
+// wave 0 takes the even batches, the helper wave the odd ones; one wave takes them all in order).
+// setup: aref, b, x at u = 0 and at the warmstart, D per row; the two costs' partial sums
+template <typename T>
+__device__ __forceinline__ void nt_setup_rows(const Env<T>& e, int ne, int nv, T wv, T ws, T wd, int b0, int bs, T& c0,
+                                              T& cw) {
+  const int l = lane_id();
+  const bool dl = l < nv;
+  const int lc = dl ? l : 0;
+  T* efc = e.efc;
+  const int step = MGX_RB * bs;
+  T xn[MGX_RD][MGX_RB];
+  first_rows(xn, e.Bm, e.Bs, ne, lc, dl, MGX_RB * b0, step);
+  for (int r0 = MGX_RB * b0; r0 < ne; r0 += step) {
+    T xb[MGX_RB];
+    next_rows(xb, xn, e.Bm, e.Bs, r0, ne, lc, dl, step);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      if (r < ne) {
+        T dv = xb[j] * wv, ds = xb[j] * ws, dw = xb[j] * wd, z = 0;
+        wave_sum4(dv, ds, dw, z);
+        T* q = efc + 8 * r;
+        const T aref = -q[6] * dv - q[5];
+        const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
+        if (b < 0) c0 += (T)0.5 * D * b * b;
+        if (xw < 0) cw += (T)0.5 * D * xw * xw;
+        if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
+      }
+    }
+  }
+}
+// J p per row (wave reductions; lane 0 stores efc[8 r + 3])
+template <typename T>
+__device__ __forceinline__ void nt_jp_rows(const Env<T>& e, int ne, int nv, T p, int b0, int bs) {
+  const int l = lane_id();
+  const bool dl = l < nv;
+  const int lc = dl ? l : 0;
+  T* efc = e.efc;
+  const int step = MGX_RB * bs;
+  T xn[MGX_RD][MGX_RB];
+  first_rows(xn, e.Bm, e.Bs, ne, lc, dl, MGX_RB * b0, step);
+  for (int r0 = MGX_RB * b0; r0 < ne; r0 += step) {
+    T xb[MGX_RB];
+    next_rows(xb, xn, e.Bm, e.Bs, r0, ne, lc, dl, step);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j += 4) {
+      T s0 = xb[j] * p, s1 = xb[j + 1] * p, s2 = xb[j + 2] * p, s3 = xb[j + 3] * p;
+      wave_sum4(s0, s1, s2, s3);
+      if (l == 0) {
+        if (r0 + j < ne) efc[8 * (r0 + j) + 3] = s0;
+        if (r0 + j + 1 < ne) efc[8 * (r0 + j + 1) + 3] = s1;
+        if (r0 + j + 2 < ne) efc[8 * (r0 + j + 2) + 3] = s2;
+        if (r0 + j + 3 < ne) efc[8 * (r0 + j + 3) + 3] = s3;
+      }
+    }
+  }
+}
+// gg + sum_{x<0} D x B_r (lane = dof); only the active rows are loaded
+template <typename T>
+__device__ __forceinline__ T nt_grad_rows(const Env<T>& e, int ne, int nv, T gg, int b0, int bs) {
+  const int l = lane_id();
+  const bool dl = l < nv;
+  const int lc = dl ? l : 0;
+  const T* efc = e.efc;
+  const int step = MGX_RB * bs;
+  T gn[MGX_RB], xq[MGX_RB], dq[MGX_RB];  // the next batch, in flight
+  auto load = [&](int r0, T* xb, T* xs, T* ds) {
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      xs[j] = r < ne ? efc[8 * r + 1] : (T)0;
+      ds[j] = xs[j] < 0 ? efc[8 * r + 4] : (T)0;
+      xb[j] = (xs[j] < 0 && dl) ? e.Bm[r * e.Bs + lc] : (T)0;
+    }
+  };
+  load(MGX_RB * b0, gn, xq, dq);
+  for (int r0 = MGX_RB * b0; r0 < ne; r0 += step) {
+    T xb[MGX_RB], xs[MGX_RB], ds[MGX_RB];
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) { xb[j] = gn[j]; xs[j] = xq[j]; ds[j] = dq[j]; }
+    load(r0 + step, gn, xq, dq);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++)
+      if (xs[j] < 0) gg += ds[j] * xs[j] * xb[j];
+  }
+  return gg;
+}
+// v + sum_r f_r B_r (lane = dof; f in efc[8 r + 1])
+template <typename T>
+__device__ __forceinline__ T nt_force_rows(const Env<T>& e, int ne, int nv, T v, int b0, int bs) {
+  const int l = lane_id();
+  const bool dl = l < nv;
+  const int lc = dl ? l : 0;
+  const T* efc = e.efc;
+  const int step = MGX_RB * bs;
+  T xn[MGX_RD][MGX_RB];
+  first_rows(xn, e.Bm, e.Bs, ne, lc, dl, MGX_RB * b0, step);
+  for (int r0 = MGX_RB * b0; r0 < ne; r0 += step) {
+    T xb[MGX_RB];
+    next_rows(xb, xn, e.Bm, e.Bs, r0, ne, lc, dl, step);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++)
+      if (r0 + j < ne) v += efc[8 * (r0 + j) + 1] * xb[j];
+  }
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   const int l = lane_id();
@@ -1308,25 +1491,17 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // what keeps the global-scratch rows (Layout.gB) off the latency path; the row scalars are
   // uniform and lane 0 stores them.
   T c0 = 0, cw = 0;
-  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-    T xb[MGX_RB];
-    load_rows(xb, Bm, Bs, r0, ne, lc, dl);
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) {
-      const int r = r0 + j;
-      if (r < ne) {
-        T dv = xb[j] * wv, ds = xb[j] * ws, dw = xb[j] * wd, z = 0;
-        wave_sum4(dv, ds, dw, z);
-        T* q = efc + 8 * r;
-        const T aref = -q[6] * dv - q[5];
-        const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
-        if (b < 0) c0 += (T)0.5 * D * b * b;
-        if (xw < 0) cw += (T)0.5 * D * xw * xw;
-        if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
-      }
-    }
+  const int nw = e.nw;
+  if (nw > 1) {  // the helper's inputs
+    if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = wd; }
   }
-  wsync();
+  team_begin(e, TEAM_SETUP, ne);
+  nt_setup_rows(e, ne, nv, wv, ws, wd, 0, nw, c0, cw);
+  team_end(e);
+  if (nw > 1) {  // the helper's partial costs (odd batches), in vec3[0..1]
+    c0 += e.vec3[0];
+    cw += e.vec3[1];
+  }
   const T uw = wd;
   cw += usum((T)0.5 * uw * uw);
   const bool warm = cw < c0;
@@ -1341,25 +1516,10 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   int iter = 0;
   // whitened gradient g = u + sum_{x<0} D x B_r (lane = dof)
   auto gradient = [&]() {
-    T gg = u;
-    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-      // only the active rows (x < 0) are loaded: the others add nothing
-      T xb[MGX_RB], xs[MGX_RB];
-#pragma unroll
-      for (int j = 0; j < MGX_RB; j++) {
-        const int r = r0 + j;
-        xs[j] = r < ne ? efc[8 * r + 1] : (T)0;
-        xb[j] = (xs[j] < 0 && dl) ? Bm[r * Bs + lc] : (T)0;
-      }
-#pragma unroll
-      for (int j = 0; j < MGX_RB; j++) {
-        const int r = r0 + j;
-        if (r < ne) {
-          const T xr = xs[j];
-          if (xr < 0) gg += efc[8 * r + 4] * xr * xb[j];
-        }
-      }
-    }
+    team_begin(e, TEAM_GRAD, ne);
+    T gg = nt_grad_rows(e, ne, nv, u, 0, nw);
+    team_end(e);
+    if (nw > 1) gg += e.vec1[lc];  // the helper's partial (odd batches)
     return dl ? gg : (T)0;
   };
   T g = gradient();
@@ -1368,11 +1528,27 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // scaled gradient at the new point, so at least one iteration runs
   while (iter < maxit) {
     // H = I + sum_{x<0} D B_r B_r' on MFMA (hessian_mfma), lower triangle
-    hessian_mfma(Bm, Bs, efc, ne, nv, H);
-    wsync();
+    team_begin(e, TEAM_HESS, ne);
+    if (nw > 1) hessian_mfma<T, 0, 3>(Bm, Bs, efc, ne, nv, H);  // the helper: tile row 3
+    else hessian_mfma(Bm, Bs, efc, ne, nv, H);
+    team_end(e);
     MGX_STAMP(11);  // Hessian
     // Cholesky H = L L' in place: 16-wide block columns, trailing update on MFMA (chol_blocked)
-    chol_blocked(H, nv);
+    {
+      const int nb = (nv + 15) >> 4;
+      for (int kb = 0; kb < nb; kb++) {
+        chol_diag<T, false>(H, nv, kb);
+        wsync();
+        chol_panel<T, false>(H, nv, kb, 0, 1);
+        if (kb + 1 < nb) {
+          team_begin(e, TEAM_TRAIL, kb);
+          chol_trail<T, false>(H, nv, kb, 0, nw);
+          team_end(e);
+        } else {
+          wsync();
+        }
+      }
+    }
     MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y (reciprocal pivots computed once, lane-parallel)
     const T rdiag = dl ? (T)1 / H[l * nv + l] : (T)0;
@@ -1391,22 +1567,10 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     p = dl ? p : (T)0;
     MGX_STAMP(13);  // triangular solves
     // J p per row, row-major (coalesced, 8 rows per batch) with wave reductions; lane 0 stores
-    for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-      T xb[MGX_RB];
-      load_rows(xb, Bm, Bs, r0, ne, lc, dl);
-#pragma unroll
-      for (int j = 0; j < MGX_RB; j += 4) {
-        T s0 = xb[j] * p, s1 = xb[j + 1] * p, s2 = xb[j + 2] * p, s3 = xb[j + 3] * p;
-        wave_sum4(s0, s1, s2, s3);
-        if (l == 0) {
-          if (r0 + j < ne) efc[8 * (r0 + j) + 3] = s0;
-          if (r0 + j + 1 < ne) efc[8 * (r0 + j + 1) + 3] = s1;
-          if (r0 + j + 2 < ne) efc[8 * (r0 + j + 2) + 3] = s2;
-          if (r0 + j + 3 < ne) efc[8 * (r0 + j + 3) + 3] = s3;
-        }
-      }
-    }
-    wsync();
+    if (nw > 1 && dl) e.vec0[l] = p;  // the helper's input
+    team_begin(e, TEAM_JP, ne);
+    nt_jp_rows(e, ne, nv, p, 0, nw);
+    team_end(e);
     MGX_STAMP(14);  // J p
     // line search along p (oracle/mjref.c newton_solve, MuJoCo's stop rule [ext]): f'(al) = u.p +
     // al p.p + sum_{x + al jp < 0} D (x + al jp) jp; first point the Newton step from al = 0, then
@@ -1470,20 +1634,49 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   }
   wsync();
   // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = J'f = L' D^1/2 (sum f_r B_r)
-  T v = 0;
-  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-    T xb[MGX_RB];
-    load_rows(xb, Bm, Bs, r0, ne, lc, dl);
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++)
-      if (r0 + j < ne) v += efc[8 * (r0 + j) + 1] * xb[j];
-  }
+  team_begin(e, TEAM_FORCE, ne);
+  T v = nt_force_rows(e, ne, nv, (T)0, 0, nw);
+  team_end(e);
+  if (nw > 1) v += e.vec1[lc];  // the helper's partial (odd batches)
   v = dl ? v : (T)0;
   T z = dl ? u * e.diaginv * sqrtD : (T)0;
   z = solve_L(m, e, e.qLD, z);
   e.qacc = e.qacc_smooth + z;
   e.qfrc_constraint = mul_LT(m, e, e.qLD, sqrtD * v);
   wsync();
+}
+
+// wave 1 of a two-wave narrow Newton env (k_assembly): one loop iteration per barrier of wave 0
+// (TEAM_NONE), the odd batches / tile row 3 / every other trailing tile of each posted section,
+// until wave 0 posts TEAM_EXIT
+template <typename T>
+__device__ __forceinline__ void team_helper_n(const DevModel<T>& m, Env<T>& e) {
+  const int l = lane_id(), nv = m.nv;
+  const bool dl = l < nv;
+  for (;;) {
+    __syncthreads();
+    const int cmd = __builtin_amdgcn_readfirstlane(e.ctl[0]);
+    if (cmd == TEAM_NONE) continue;
+    if (cmd == TEAM_EXIT) break;
+    const int a = __builtin_amdgcn_readfirstlane(e.ctl[1]);
+    if (cmd == TEAM_SETUP) {
+      const T wv = dl ? e.vec0[l] : (T)0, ws = dl ? e.vec1[l] : (T)0, wd = dl ? e.vec2[l] : (T)0;
+      T c0 = 0, cw = 0;
+      nt_setup_rows(e, a, nv, wv, ws, wd, 1, 2, c0, cw);
+      if (l == 0) { e.vec3[0] = c0; e.vec3[1] = cw; }
+    } else if (cmd == TEAM_GRAD) {
+      e.vec1[l] = nt_grad_rows(e, a, nv, (T)0, 1, 2);
+    } else if (cmd == TEAM_HESS) {
+      hessian_mfma<T, 3, 4>(e.Bm, e.Bs, e.efc, a, nv, e.hess);
+    } else if (cmd == TEAM_TRAIL) {
+      chol_trail<T, false>(e.hess, nv, a, 1, 2);
+    } else if (cmd == TEAM_JP) {
+      nt_jp_rows(e, a, nv, dl ? e.vec0[l] : (T)0, 1, 2);
+    } else if (cmd == TEAM_FORCE) {
+      e.vec1[l] = nt_force_rows(e, a, nv, (T)0, 1, 2);
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- integration

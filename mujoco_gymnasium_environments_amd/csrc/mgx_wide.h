@@ -24,8 +24,6 @@ struct WEnv {
   T qacc_ws[2], qfrc_applied[2], qfrc_smooth[2], qacc_smooth[2], qacc[2], qfrc_constraint[2], diaginv[2];
   int chainlen[2], madr[2];
   uint64_t anc_lo[2], anc_hi[2];  // strict ancestors of dof 64 w + lane among dofs 0..63 / 64..127
-  int nw;    // waves per env: 1, or 2 (wave 0 + the helper, team_helper)
-  int* ctl;  // helper section command words (Layout.team)
 };
 
 __device__ __forceinline__ int wdof(int w) { return 64 * w + lane_id(); }
@@ -43,8 +41,6 @@ __device__ __forceinline__ T wdot(const T (&a)[2], const T (&b)[2]) {
 template <typename T>
 __device__ __forceinline__ void wenv_bind(const DevModel<T>& m, WEnv<T>& w, char* smem, T* gB) {
   env_bind<T, true, true>(m, w.e, smem, gB);
-  w.nw = blockDim.x >> 6;
-  w.ctl = reinterpret_cast<int*>(reinterpret_cast<T*>(smem) + m.L.reals) + m.L.team;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int d = wdof(k);
@@ -191,31 +187,7 @@ __device__ __forceinline__ void wsolve_M(const DevModel<T>& m, const WEnv<T>& w,
 // its share (no barriers inside) -> barrier -> wave 0 clears the command. Shares split the same
 // loops by chunk (chunk c to wave c mod nw), so a one-wave launch (nw = 1: the debug kernel, the
 // reset) runs the identical code with every chunk on wave 0 and the same results.
-enum { TEAM_NONE = 0, TEAM_EXIT = 1, TEAM_HESS, TEAM_PANEL, TEAM_TRAIL, TEAM_JP, TEAM_GRAD, TEAM_XFORM };
-
-template <typename T>
-__device__ __forceinline__ void team_begin(WEnv<T>& w, int cmd, int arg) {
-  if (w.nw > 1 && lane_id() == 0) { w.ctl[0] = cmd; w.ctl[1] = arg; }
-  wsync();
-}
-template <typename T>
-__device__ __forceinline__ void team_end(WEnv<T>& w) {
-  wsync();
-  if (w.nw > 1 && lane_id() == 0) w.ctl[0] = TEAM_NONE;
-}
-// wave 0, before its first wsync: the helpers read the command word after every barrier
-template <typename T>
-__device__ __forceinline__ void team_init(WEnv<T>& w) {
-  if (w.nw > 1 && lane_id() == 0) w.ctl[0] = TEAM_NONE;
-}
-// wave 0, at the end of the kernel (every path): releases the helpers
-template <typename T>
-__device__ __forceinline__ void team_exit(WEnv<T>& w) {
-  if (w.nw > 1) {
-    if (lane_id() == 0) w.ctl[0] = TEAM_EXIT;
-    wsync();
-  }
-}
+// (team_begin / team_end / TEAM_* in mgx_physics.h)
 
 // ---------------------------------------------------------------- Newton Hessian on MFMA
 // H = I + sum_{x_r<0} D_r B_r B_r' for nv <= 128 (8 tile rows of 16): the lower tiles of tile
@@ -249,14 +221,22 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
       b[t] = (sc != (T)0 && c < nv) ? Bm[r * Bs + c] : (T)0;  // inactive rows: not streamed
     }
   };
-  T bn[T1], sn;
-  load(0, bn, sn);
+  constexpr int HD = 2;  // chunks in flight (the register budget of the wide kernels)
+  T bq[HD][T1], sq[HD];
+#pragma unroll
+  for (int d = 0; d < HD; d++) load(4 * d, bq[d], sq[d]);
   for (int r0 = 0; r0 < ne; r0 += 4) {
     T b[T1];
 #pragma unroll
-    for (int t = 0; t < T1; t++) b[t] = bn[t];
-    const T sc = sn;
-    load(r0 + 4, bn, sn);
+    for (int t = 0; t < T1; t++) b[t] = bq[0][t];
+    const T sc = sq[0];
+#pragma unroll
+    for (int d = 0; d + 1 < HD; d++) {
+      sq[d] = sq[d + 1];
+#pragma unroll
+      for (int t = 0; t < T1; t++) bq[d][t] = bq[d + 1][t];
+    }
+    load(r0 + 4 * HD, bq[HD - 1], sq[HD - 1]);
     if (__ballot(sc != (T)0) == 0ull) continue;  // four inactive rows: no MFMAs
 #pragma unroll
     for (int t = T0, q = 0; t < T1; t++)
@@ -299,13 +279,13 @@ __device__ __forceinline__ void wchol(WEnv<T>& w, T* H, int nv) {
   const int nb = (nv + 15) >> 4;
   for (int kb = 0; kb < nb; kb++) {
     chol_diag<T, true>(H, nv, kb);
-    team_begin(w, TEAM_PANEL, kb);
-    chol_panel<T, true>(H, nv, kb, 0, w.nw);
-    team_end(w);
+    team_begin(w.e, TEAM_PANEL, kb);
+    chol_panel<T, true>(H, nv, kb, 0, w.e.nw);
+    team_end(w.e);
     if (kb + 1 < nb) {
-      team_begin(w, TEAM_TRAIL, kb);
-      chol_trail<T, true>(H, nv, kb, 0, w.nw);
-      team_end(w);
+      team_begin(w.e, TEAM_TRAIL, kb);
+      chol_trail<T, true>(H, nv, kb, 0, w.e.nw);
+      team_end(w.e);
     }
   }
 }
@@ -317,10 +297,15 @@ __device__ __forceinline__ void wjp_share(const Env<T>& e, int nv, int ne, const
   const bool dl[2] = {l < nv, 64 + l < nv};
   const int lc[2] = {dl[0] ? l : 0, dl[1] ? 64 + l : 0};
   T* efc = e.efc;
+  T na[MGX_RB], nb[MGX_RB];  // the next chunk, in flight
+  load_rows(na, e.Bm, e.Bs, MGX_RB * c0, ne, lc[0], dl[0]);
+  load_rows(nb, e.Bm, e.Bs, MGX_RB * c0, ne, lc[1], dl[1]);
   for (int r0 = MGX_RB * c0; r0 < ne; r0 += MGX_RB * cs) {
     T xa[MGX_RB], xb[MGX_RB];
-    load_rows(xa, e.Bm, e.Bs, r0, ne, lc[0], dl[0]);
-    load_rows(xb, e.Bm, e.Bs, r0, ne, lc[1], dl[1]);
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) { xa[j] = na[j]; xb[j] = nb[j]; }
+    load_rows(na, e.Bm, e.Bs, r0 + MGX_RB * cs, ne, lc[0], dl[0]);
+    load_rows(nb, e.Bm, e.Bs, r0 + MGX_RB * cs, ne, lc[1], dl[1]);
 #pragma unroll
     for (int j = 0; j < MGX_RB; j += 4) {
       T s0 = xa[j] * p[0] + xb[j] * p[1], s1 = xa[j + 1] * p[0] + xb[j + 1] * p[1];
@@ -344,20 +329,23 @@ __device__ __forceinline__ void wgrad_share(const Env<T>& e, int nv, int ne, int
   const T* efc = e.efc;
   gg[0] = 0;
   gg[1] = 0;
+  T nx[MGX_RB], nd[MGX_RB], na[MGX_RB], nb[MGX_RB];  // the next chunk, in flight
+  auto load = [&](int r0) {
+#pragma unroll
+    for (int j = 0; j < MGX_RB; j++) {
+      const int r = r0 + j;
+      nx[j] = r < ne ? efc[8 * r + 1] : (T)0;
+      nd[j] = nx[j] < 0 ? efc[8 * r + 4] : (T)0;
+      na[j] = (nx[j] < 0 && dl[0]) ? e.Bm[r * e.Bs + l] : (T)0;
+      nb[j] = (nx[j] < 0 && dl[1]) ? e.Bm[r * e.Bs + 64 + l] : (T)0;
+    }
+  };
+  load(MGX_RB * c0);
   for (int r0 = MGX_RB * c0; r0 < ne; r0 += MGX_RB * cs) {
     T xs[MGX_RB], sd[MGX_RB], xa[MGX_RB], xb[MGX_RB];
 #pragma unroll
-    for (int j = 0; j < MGX_RB; j++) {
-      const int r = r0 + j;
-      xs[j] = r < ne ? efc[8 * r + 1] : (T)0;
-      sd[j] = r < ne ? efc[8 * r + 4] : (T)0;
-    }
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) {
-      const int r = r0 + j;
-      xa[j] = (xs[j] < 0 && dl[0]) ? e.Bm[r * e.Bs + l] : (T)0;
-      xb[j] = (xs[j] < 0 && dl[1]) ? e.Bm[r * e.Bs + 64 + l] : (T)0;
-    }
+    for (int j = 0; j < MGX_RB; j++) { xs[j] = nx[j]; sd[j] = nd[j]; xa[j] = na[j]; xb[j] = nb[j]; }
+    load(r0 + MGX_RB * cs);
 #pragma unroll
     for (int j = 0; j < MGX_RB; j++) {
       if (xs[j] < 0) {
@@ -407,10 +395,13 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   const int Bs = e.Bs;
   // per row: aref, b = J qacc_smooth - aref, D; x at u = 0 (q[1]) and at the warmstart (q[3])
   T c0 = 0, cw = 0;
+  T na[MGX_RD][MGX_RB], nb[MGX_RD][MGX_RB];  // the next batches, in flight
+  first_rows(na, Bm, Bs, ne, lc[0], dl[0]);
+  first_rows(nb, Bm, Bs, ne, lc[1], dl[1]);
   for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
     T xa[MGX_RB], xb[MGX_RB];
-    load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
-    load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
+    next_rows(xa, na, Bm, Bs, r0, ne, lc[0], dl[0]);
+    next_rows(xb, nb, Bm, Bs, r0, ne, lc[1], dl[1]);
 #pragma unroll
     for (int j = 0; j < MGX_RB; j++) {
       const int r = r0 + j;
@@ -444,11 +435,11 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   // one wave or two — the result does not depend on the launch's wave count
   auto gradient = [&](T (&gg)[2]) {
     T part[2], odd[2];
-    team_begin(w, TEAM_GRAD, ne);
+    team_begin(w.e, TEAM_GRAD, ne);
     wgrad_share(e, nv, ne, 0, 2, part);
-    if (w.nw == 1) wgrad_share(e, nv, ne, 1, 2, odd);
-    team_end(w);
-    if (w.nw > 1) {
+    if (w.e.nw == 1) wgrad_share(e, nv, ne, 1, 2, odd);
+    team_end(w.e);
+    if (w.e.nw > 1) {
       odd[0] = dl[0] ? e.vec1[l] : (T)0;
       odd[1] = dl[1] ? e.vec1[64 + l] : (T)0;
     }
@@ -460,9 +451,9 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   MGX_STAMP_DECL
   MGX_STAMP(10);  // setup
   while (iter < maxit) {
-    team_begin(w, TEAM_HESS, ne);
-    whess_share(Bm, Bs, efc, ne, nv, H, 0, w.nw);
-    team_end(w);
+    team_begin(w.e, TEAM_HESS, ne);
+    whess_share(Bm, Bs, efc, ne, nv, H, 0, w.e.nw);
+    team_end(w.e);
     MGX_STAMP(11);  // Hessian
     wchol(w, H, nv);
     MGX_STAMP(12);  // Cholesky
@@ -494,13 +485,13 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     p[1] = dl[1] ? p[1] : (T)0;
     MGX_STAMP(13);  // triangular solves
     // J p per row (row-major, wave reductions; row chunks shared, p to the helpers in vec0)
-    if (w.nw > 1) {
+    if (w.e.nw > 1) {
       if (dl[0]) e.vec0[l] = p[0];
       if (dl[1]) e.vec0[64 + l] = p[1];
     }
-    team_begin(w, TEAM_JP, ne);
-    wjp_share(e, nv, ne, p, 0, w.nw);
-    team_end(w);
+    team_begin(w.e, TEAM_JP, ne);
+    wjp_share(e, nv, ne, p, 0, w.e.nw);
+    team_end(w.e);
     MGX_STAMP(14);  // J p
     // line search (newton(), mgx_physics.h: MuJoCo's stop rule)
     const T g0 = wdot(u, p), pp = wdot(p, p);
@@ -567,10 +558,12 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   wsync();
   // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = L' D^1/2 (sum f_r B_r)
   T v[2] = {0, 0};
+  first_rows(na, Bm, Bs, ne, lc[0], dl[0]);
+  first_rows(nb, Bm, Bs, ne, lc[1], dl[1]);
   for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
     T xa[MGX_RB], xb[MGX_RB];
-    load_rows(xa, Bm, Bs, r0, ne, lc[0], dl[0]);
-    load_rows(xb, Bm, Bs, r0, ne, lc[1], dl[1]);
+    next_rows(xa, na, Bm, Bs, r0, ne, lc[0], dl[0]);
+    next_rows(xb, nb, Bm, Bs, r0, ne, lc[1], dl[1]);
 #pragma unroll
     for (int j = 0; j < MGX_RB; j++)
       if (r0 + j < ne) {
@@ -680,9 +673,9 @@ __device__ __forceinline__ void wforward(const DevModel<T>& m, WEnv<T>& w) {
     transform_rows<T, true>(m, e);
   } else {
     const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
-    team_begin(w, TEAM_XFORM, ne);
-    wtransform_rows(m, w, ne, 0, w.nw);
-    team_end(w);
+    team_begin(w.e, TEAM_XFORM, ne);
+    wtransform_rows(m, w, ne, 0, w.e.nw);
+    team_end(w.e);
   }
   MGX_STAMP(7);
   wnewton(m, w);
@@ -784,26 +777,26 @@ __device__ __forceinline__ void team_helper(const DevModel<T>& m, WEnv<T>& w) {
   const int l = lane_id(), nv = m.nv;
   for (;;) {
     __syncthreads();
-    const int cmd = __builtin_amdgcn_readfirstlane(w.ctl[0]);
+    const int cmd = __builtin_amdgcn_readfirstlane(w.e.ctl[0]);
     if (cmd == TEAM_NONE) continue;
     if (cmd == TEAM_EXIT) break;
-    const int a = __builtin_amdgcn_readfirstlane(w.ctl[1]);
+    const int a = __builtin_amdgcn_readfirstlane(w.e.ctl[1]);
     if (cmd == TEAM_HESS) {
-      whess_share(e.Bm, e.Bs, e.efc, a, nv, e.hess, wv, w.nw);
+      whess_share(e.Bm, e.Bs, e.efc, a, nv, e.hess, wv, w.e.nw);
     } else if (cmd == TEAM_PANEL) {
-      chol_panel<T, true>(e.hess, nv, a, wv, w.nw);
+      chol_panel<T, true>(e.hess, nv, a, wv, w.e.nw);
     } else if (cmd == TEAM_TRAIL) {
-      chol_trail<T, true>(e.hess, nv, a, wv, w.nw);
+      chol_trail<T, true>(e.hess, nv, a, wv, w.e.nw);
     } else if (cmd == TEAM_JP) {
       const T p[2] = {l < nv ? e.vec0[l] : (T)0, 64 + l < nv ? e.vec0[64 + l] : (T)0};
-      wjp_share(e, nv, a, p, wv, w.nw);
+      wjp_share(e, nv, a, p, wv, w.e.nw);
     } else if (cmd == TEAM_GRAD) {  // the odd chunks (wnewton's gradient)
       T g[2];
       wgrad_share(e, nv, a, 1, 2, g);
       e.vec1[l] = g[0];
       e.vec1[64 + l] = g[1];
     } else if (cmd == TEAM_XFORM) {
-      wtransform_rows(m, w, a, wv, w.nw);
+      wtransform_rows(m, w, a, wv, w.e.nw);
     }
     __syncthreads();
   }
