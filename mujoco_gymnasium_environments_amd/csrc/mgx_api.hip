@@ -265,7 +265,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   const bool mono_overlay = gB && !hess_union && !(d->layout_flags & MGX_KEEP_CVEL) &&
                             cp3 + cf9 + align_up(max_nefc, al) + act_r <= union_dead + cvel_sz;
   if (!hess_union && !mono_overlay) { L.con_pos = take(3 * max_ncon); L.con_frame = take(9 * max_ncon); }
-  // wide Newton models: efc / efc_margin in global scratch (L.gB_efc), the Hessian packed lower
+  // wide Newton models: efc / efc_margin in global scratch (gb_efc_off), the Hessian packed lower
   const bool efcg = gB && nv > 64 && d->solver == 2;
   L.efc = take(efcg ? 1 : 8 * max_nefc); L.efc_margin = take(mono_overlay || efcg ? 1 : max_nefc);
   L.efc_blk = take(hess_union ? 1 : 2 * max_nefc);
@@ -295,16 +295,13 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.Bstride = nv | 1;  // odd stride: lane-per-row access is bank-conflict free
   L.Bmat = u0;
   L.chunk_rows = max_nefc;
-  L.gB_efc = -1; L.gB_efm = -1; L.hpk = 0;
   if (gB) {  // rows in per-env global scratch
     L.gB = 1;
     L.gB_stride = align_up(max_nefc * L.Bstride, al);
     L.chunk_rows = 0;
-    if (efcg) {
-      L.gB_efc = L.gB_stride;
-      L.gB_efm = L.gB_efc + align_up(8 * max_nefc, al);
-      L.gB_stride = L.gB_efm + align_up(max_nefc, al);
-      L.hpk = 1;
+    if (efcg) {  // then efc, efc_margin (the device derives the same offsets)
+      L.gB_stride = gb_efm_off(L, real_bytes) + align_up(max_nefc, al);
+      if (gb_efc_off(L, real_bytes) != align_up(max_nefc * L.Bstride, al)) abort();
     }
   }
   // gB: the row transform stages up to 64 rows at a time in the phase-A union (dead by then)
@@ -313,7 +310,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
     L.hess = u0;
     L.con_pos = endA;
     L.con_frame = align_up(L.con_pos + 3 * max_ncon, al);
-    endA = std::max(align_up(L.con_frame + 9 * max_ncon, al), align_up(u0 + (L.hpk ? nv * (nv + 1) / 2 : nv * nv), al));
+    endA = std::max(align_up(L.con_frame + 9 * max_ncon, al), align_up(u0 + (efcg ? nv * (nv + 1) / 2 : nv * nv), al));
   }
   int endB = align_up(u0 + L.chunk_rows * L.Bstride, al);
   L.reals = endA > endB ? endA : endB;
@@ -325,7 +322,7 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
   L.act_list = takei(max_active);
   L.efc_type = takei(max_nefc); L.efc_id = takei(max_nefc);
   L.con_efcadr = takei(1);
-  L.team = d->solver == 2 ? takei(4) : 0;  // Newton models: the helper-wave command words
+  if (d->solver == 2 && takei(4) != team_off(L)) abort();  // Newton models: the helper-wave command words
   L.ints = q;
   L.bytes = L.reals * real_bytes + L.ints * 4;
   (void)vec_end;

@@ -9,6 +9,7 @@
 // scene's ~300 rows do not fit next to the rest, in per-env global scratch) -> gripper-contact
 // task state / reward / termination / observation, with same-step autoreset (10 settle steps),
 // all in one launch.
+#define MGX_TEAM  // kernels with a Newton helper wave (lane_id, team_begin)
 #include "mgx_internal.h"
 #include "mgx_assembly.h"
 

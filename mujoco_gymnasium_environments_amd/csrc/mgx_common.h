@@ -44,13 +44,6 @@ struct Layout {
   // 1: the monolithic kernel keeps B rows in per-env global scratch (gB_stride reals per env)
   // instead of LDS, for models whose rows do not fit the LDS budget
   int gB, gB_stride;
-  // wide kernels (nv > 64): the per-row constraint data efc / efc_margin sit in the per-env global
-  // scratch at these real offsets instead of LDS (gB_efc >= 0), and the Newton Hessian is stored
-  // as a packed lower triangle, row i at i (i + 1) / 2 (hpk) — with both, humanoid_construction's
-  // per-env LDS fits two envs per CU
-  int gB_efc, gB_efm, hpk;
-  // wide kernels' helper wave (mgx_wide.h team_*): the section command words (ints)
-  int team;
   // gB only: rows per chunk staged into the (dead) phase-A union region for the row transform
   int tchunk;
   // Newton solver (solver == mjSOL_NEWTON, monolithic kernels only): nv x nv Hessian
@@ -74,6 +67,19 @@ struct Layout {
   // row blocks) live in the slot's pipe storage (Pipe.o_cpos, bind_carry_tail), not in LDS
   int gcon;
 };
+// Derived, not stored (the Layout / DevModel kernel-argument layout stays that of the task
+// kernels): wide Newton models (nv > 64, rows in global scratch) keep the per-row constraint data
+// efc / efc_margin in the env's global scratch after its rows, at these real offsets, and store
+// the Hessian as a packed lower triangle (row i at i (i + 1) / 2); Newton models keep the helper
+// wave's command words (mgx_physics.h team_begin) in the four ints after con_efcadr.
+__host__ __device__ inline int mgx_align(int x, int a) { return (x + a - 1) / a * a; }
+__host__ __device__ inline int gb_efc_off(const Layout& L, int real_bytes) {
+  return mgx_align(L.max_nefc * L.Bstride, 16 / real_bytes);
+}
+__host__ __device__ inline int gb_efm_off(const Layout& L, int real_bytes) {
+  return gb_efc_off(L, real_bytes) + mgx_align(8 * L.max_nefc, 16 / real_bytes);
+}
+__host__ __device__ inline int team_off(const Layout& L) { return L.con_efcadr + 4; }
 
 // Device-resident model: pointers into one device allocation.
 template <typename T>
@@ -136,7 +142,14 @@ static __device__ unsigned long long* g_mgx_prof = nullptr;
 #endif
 
 // ------------------------------------------------------------------ wave helpers
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }  // one env = wave 0 (+ helpers)
+// MGX_TEAM (the translation units whose kernels run a helper wave beside wave 0: assembly and
+// construction): lane = thread index mod 64. Every other kernel is one wave per workgroup and keeps
+// the plain thread index (its code generation unchanged).
+#ifdef MGX_TEAM
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+#else
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+#endif
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
 __device__ __forceinline__ float readlane(float x, int l) {

@@ -7,6 +7,7 @@
 // lane. A construction env step is clip -> ctrl -> one RK4 mj_step (Newton) -> progress /
 // reward / termination / observation, with same-step autoreset (mj_resetData + draws, no
 // forward pass), all in one launch. The rows B live in per-env global scratch.
+#define MGX_TEAM  // kernels with a Newton helper wave (lane_id, team_begin)
 #include "mgx_internal.h"
 
 using namespace mgx;

@@ -32,7 +32,7 @@ struct Env {
   int *con_geom, *con_pair, *act_list, *efc_type, *efc_id, *con_efcadr;
   int ncon, nefc, niter, overflow;
   int nw;    // waves per env: 1, or 2 (wave 0 + a Newton helper wave, team_begin)
-  int* ctl;  // helper section command words (Layout.team)
+  int* ctl;  // helper section command words (team_off)
   // dof-lane registers
   T qacc_ws, qfrc_applied, qfrc_smooth, qacc_smooth, qacc, qfrc_constraint, diaginv, time;
   int chainlen, madr;  // this lane's dof: chain length, dof_Madr
@@ -40,7 +40,7 @@ struct Env {
 };
 
 // GB: B rows in global scratch (gB = this env's slice) instead of LDS (Layout.gB); EG: the per-row
-// constraint data as well (Layout.gB_efc: the wide kernels)
+// constraint data as well (gb_efc_off: the wide kernels)
 template <typename T, bool GB = false, bool EG = false>
 __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* smem, T* gB = nullptr) {
   T* R = reinterpret_cast<T*>(smem);
@@ -54,7 +54,7 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.geom_xmat = R + L.geom_xmat; e.act_force = R + L.act_force; e.cacc = R + L.cacc; e.rowc = R + L.rowc; e.con_dist = R + L.con_dist;
   e.con_pos = R + L.con_pos; e.con_frame = R + L.con_frame; e.con_mu = R + L.con_mu; e.efc = R + L.efc;
   e.efc_margin = R + L.efc_margin; e.efc_blk = R + L.efc_blk; e.Bs = L.Bstride;
-  if constexpr (EG) { e.efc = gB + L.gB_efc; e.efc_margin = gB + L.gB_efm; }
+  if constexpr (EG) { e.efc = gB + gb_efc_off(L, sizeof(T)); e.efc_margin = gB + gb_efm_off(L, sizeof(T)); }
   if constexpr (GB) e.Bm = gB;
   else e.Bm = R + L.Bmat;
   e.rk = R + L.rk;
@@ -63,8 +63,13 @@ __device__ __forceinline__ void env_bind(const DevModel<T>& m, Env<T>& e, char* 
   e.con_geom = I + L.con_geom; e.con_pair = I + L.con_pair;
   e.act_list = L.act_union > 0 ? reinterpret_cast<int*>(R + L.act_union) : I + L.act_list;
   e.efc_type = I + L.efc_type; e.con_efcadr = I + L.con_efcadr;
+#ifdef MGX_TEAM
   e.nw = blockDim.x >> 6;
-  e.ctl = I + L.team;
+  e.ctl = I + team_off(L);
+#else
+  e.nw = 1;  // one wave per workgroup (lane_id, mgx_common.h)
+  e.ctl = nullptr;
+#endif
   // the staged row builder lists only its joint-limit rows, after collision, in the broadphase list
   e.efc_id = L.staged ? e.act_list : I + L.efc_id;
   // the staged row builder's carry tail lives in global memory (bind_carry_tail)
@@ -1210,7 +1215,7 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
 // broadcasts), then subtract L_I L_J' from every trailing lower tile on MFMA (16x16x4: four
 // per tile, accumulators initialised from the tile). Entries past nv read as 0 and are never
 // stored. Same pivot clamp as the unblocked factor (d = sqrt(max(dkk, minval))). PK: H is the
-// packed lower triangle (entry (r, c), c <= r, at r (r + 1) / 2 + c; Layout.hpk, the wide solver).
+// packed lower triangle (entry (r, c), c <= r, at r (r + 1) / 2 + c; the wide solver, gb_efc_off).
 template <bool PK>
 __device__ __forceinline__ int hidx(int r, int c, int nv) {
   return PK ? (r * (r + 1) >> 1) + c : r * nv + c;
