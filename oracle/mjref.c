@@ -1496,10 +1496,11 @@ static void newton_solve(const mgx_model_desc *m, ref_data *d) {
       for (int j = 0; j < k; j++) s -= H[k * nv + j] * H[k * nv + j];
       s = sqrt(s > MINVAL ? s : MINVAL);
       H[k * nv + k] = s;
+      const double inv = 1 / s; /* mju_cholFactor scales the column by 1 / L_kk */
       for (int i = k + 1; i < nv; i++) {
         double t = H[i * nv + k];
         for (int j = 0; j < k; j++) t -= H[i * nv + j] * H[k * nv + j];
-        H[i * nv + k] = t / s;
+        H[i * nv + k] = t * inv;
       }
     }
     for (int i = 0; i < nv; i++) { /* L y = -g */
