@@ -761,10 +761,11 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
 // same order as transform_row), then the D^-1/2 scale and one coalesced store per row. A
 // contact row's support is two body chains (~10-20 of nv dofs), so a block costs tens of
 // steps, where the lane-per-row walk visits all nv dofs of every row.
+// Chunks of four rows c0, c0 + cs, ... (a helper wave takes every other chunk); the caller
+// synchronises.
 template <typename T>
-__device__ __forceinline__ void transform_rows_rm(const DevModel<T>& m, Env<T>& e) {
+__device__ __forceinline__ void transform_rows_rm(const DevModel<T>& m, Env<T>& e, int ne, int c0, int cs) {
   const int l = lane_id(), nv = m.nv;
-  const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
   const bool dl = l < nv;
   const int lc = dl ? l : 0;
   T* Bm = e.Bm;
@@ -777,10 +778,10 @@ __device__ __forceinline__ void transform_rows_rm(const DevModel<T>& m, Env<T>& 
     d = (dl && r0 + 3 < ne) ? Bm[(r0 + 3) * Bs + lc] : (T)0;
   };
   T n0, n1, n2, n3;
-  ld4(0, n0, n1, n2, n3);
-  for (int r0 = 0; r0 < ne; r0 += 4) {
+  ld4(4 * c0, n0, n1, n2, n3);
+  for (int r0 = 4 * c0; r0 < ne; r0 += 4 * cs) {
     T x0 = n0, x1 = n1, x2 = n2, x3 = n3;
-    if (r0 + 4 < ne) ld4(r0 + 4, n0, n1, n2, n3);
+    if (r0 + 4 * cs < ne) ld4(r0 + 4 * cs, n0, n1, n2, n3);
     uint64_t sp = ballot(x0 != (T)0 || x1 != (T)0 || x2 != (T)0 || x3 != (T)0);
     while (sp) {
       const int k = 63 - __clzll(sp);
@@ -798,7 +799,6 @@ __device__ __forceinline__ void transform_rows_rm(const DevModel<T>& m, Env<T>& 
       if (r0 + 3 < ne) Bm[(r0 + 3) * Bs + l] = x3 * dinvs;
     }
   }
-  wsync();
 }
 
 template <typename T, bool WIDE = false>
@@ -806,7 +806,11 @@ __device__ __forceinline__ void transform_rows(const DevModel<T>& m, Env<T>& e) 
   int l = lane_id();
   if constexpr (!WIDE) {
     if (!(MGX_TRANSFORM_LANE_ROW)) {
-      transform_rows_rm(m, e);
+      // four-row chunks, every other one on the helper wave when there is one
+      const int ne = __builtin_amdgcn_readfirstlane(e.nefc);
+      team_begin(e, TEAM_XFORM, ne);
+      transform_rows_rm(m, e, ne, 0, e.nw);
+      team_end(e);
       return;
     }
   }
@@ -1137,14 +1141,27 @@ __device__ __forceinline__ void pgs(const DevModel<T>& m, Env<T>& e) {
 // nv <= 64. Lane l holds A[l&15][l>>4] / B[l>>4][l&15] (one element each, 4 loads per chunk, 16
 // consecutive columns of one row per 16 lanes); C/D: col = l&15, row = 4(l>>4)+v (f32) or
 // (l>>4)+4v (f64) (cdna_hip_programming.md, fragment layout).
-template <typename T, int T0 = 0, int T1 = 4>
-__device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
+// GRAD (T1 = 4: every dof column is loaded): the same pass also returns sum_{x<0} D x B_r for this
+// lane's dof (lane = dof): per lane the rows kq, kq + 4, ... of each tile column, then the four
+// row groups added (xor 16, xor 32) — Newton's gradient off the Hessian's own row stream.
+template <typename T>
+__device__ __forceinline__ T xor_sum_kq(T x) {
+  x += __shfl_xor(x, 16);
+  x += __shfl_xor(x, 32);
+  return x;
+}
+template <typename T, int T0 = 0, int T1 = 4, bool GRAD = false>
+__device__ __forceinline__ T hessian_mfma(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
   typedef T V4 __attribute__((ext_vector_type(4)));
   const int l = lane_id(), i = l & 15, kq = l >> 4;
   const int nt = (nv + 15) >> 4;
-  if (T0 >= nt) return;
+  if (!GRAD && T0 >= nt) return (T)0;
+  static_assert(!GRAD || T1 == 4, "the fused gradient needs every dof column");
   auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
   constexpr int NT = (T1 * (T1 + 1) - T0 * (T0 + 1)) / 2;  // tiles of tile rows [T0, T1)
+  T gp[T1];
+#pragma unroll
+  for (int t = 0; t < T1; t++) gp[t] = 0;
   V4 acc[NT];
 #pragma unroll
   for (int t = T0, q = 0; t < T1; t++)
@@ -1154,12 +1171,14 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
       for (int v = 0; v < 4; v++) acc[q][v] = (t == u && row_of(v) == i) ? (T)1 : (T)0;
   // rows with x >= 0 add nothing (s_k = 0): their B is not loaded (zeros instead), and a chunk
   // of four inactive rows skips its MFMAs — the same sums, without streaming inactive rows
-  auto load = [&](int r0, T* b, T& sc) {
+  auto load = [&](int r0, T* b, T& sc, T& sg) {
     const int r = r0 + kq;
     sc = 0;
+    sg = 0;
     if (r < ne) {
       const T x = efc[8 * r + 1];
       sc = x < 0 ? efc[8 * r + 4] : (T)0;
+      sg = sc * x;
     }
 #pragma unroll
     for (int t = 0; t < T1; t++) {
@@ -1168,22 +1187,27 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
     }
   };
   // the next MGX_HD chunks are in flight during this chunk's MFMAs (B in global scratch: L2 misses)
-  T bq[MGX_HD][T1], sq[MGX_HD];
+  T bq[MGX_HD][T1], sq[MGX_HD], gq[MGX_HD];
 #pragma unroll
-  for (int d = 0; d < MGX_HD; d++) load(4 * d, bq[d], sq[d]);
+  for (int d = 0; d < MGX_HD; d++) load(4 * d, bq[d], sq[d], gq[d]);
   for (int r0 = 0; r0 < ne; r0 += 4) {
     T b[T1];
 #pragma unroll
     for (int t = 0; t < T1; t++) b[t] = bq[0][t];
-    const T sc = sq[0];
+    const T sc = sq[0], sg = gq[0];
 #pragma unroll
     for (int d = 0; d + 1 < MGX_HD; d++) {
       sq[d] = sq[d + 1];
+      gq[d] = gq[d + 1];
 #pragma unroll
       for (int t = 0; t < T1; t++) bq[d][t] = bq[d + 1][t];
     }
-    load(r0 + 4 * MGX_HD, bq[MGX_HD - 1], sq[MGX_HD - 1]);
+    load(r0 + 4 * MGX_HD, bq[MGX_HD - 1], sq[MGX_HD - 1], gq[MGX_HD - 1]);
     if (__ballot(sc != (T)0) == 0ull) continue;
+    if constexpr (GRAD) {
+#pragma unroll
+      for (int t = 0; t < T1; t++) gp[t] += sg * b[t];
+    }
 #pragma unroll
     for (int t = T0, q = 0; t < T1; t++)
 #pragma unroll
@@ -1205,6 +1229,17 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
         const int row = 16 * t + row_of(v), col = 16 * u + i;
         if (t < nt && row < nv && col <= row) H[row * nv + col] = acc[q][v];
       }
+  if constexpr (GRAD) {
+    // lane l = 16 kq + i holds dof 16 t + i of tile column t = kq after the row-group sums
+    T g = 0;
+#pragma unroll
+    for (int t = 0; t < T1; t++) {
+      const T s = xor_sum_kq(gp[t]);
+      g = kq == t ? s : g;
+    }
+    return l < nv ? g : (T)0;
+  }
+  return (T)0;
 }
 
 // ---------------------------------------------------------------- blocked Cholesky
@@ -1214,7 +1249,8 @@ __device__ __forceinline__ void hessian_mfma(const T* Bm, int Bs, const T* efc, 
 // column, <= 15-term dots), solve the panel below it against L_kk' (lane = row, L_kk read as LDS
 // broadcasts), then subtract L_I L_J' from every trailing lower tile on MFMA (16x16x4: four
 // per tile, accumulators initialised from the tile). Entries past nv read as 0 and are never
-// stored. Same pivot clamp as the unblocked factor (d = sqrt(max(dkk, minval))). PK: H is the
+// stored. Same pivot clamp as the unblocked factor (d = sqrt(max(dkk, minval))); the column
+// below a pivot is scaled by 1 / d as mju_cholFactor [ext] does. PK: H is the
 // packed lower triangle (entry (r, c), c <= r, at r (r + 1) / 2 + c; the wide solver, gb_efc_off).
 template <bool PK>
 __device__ __forceinline__ int hidx(int r, int c, int nv) {
@@ -1238,7 +1274,8 @@ __device__ __forceinline__ void chol_diag(T* H, int nv, int kb) {
     if (c < bk) {
       const T dkk = readlane(x[c], c);
       const T d = sqrt(dkk > minval<T>() ? dkk : minval<T>());
-      x[c] = l == c ? d : (l > c ? x[c] / d : x[c]);
+      const T rd = (T)1 / d;  // mju_cholFactor: the column is scaled by 1 / L_cc
+      x[c] = l == c ? d : (l > c ? x[c] * rd : x[c]);
       const T lic = x[c];
 #pragma unroll
       for (int j = c + 1; j < 16; j++)
@@ -1258,6 +1295,11 @@ template <typename T, bool PK>
 __device__ __forceinline__ void chol_panel(T* H, int nv, int kb, int j0, int js) {
   const int l = lane_id();
   const int k0 = 16 * kb, bk = nv - k0 < 16 ? nv - k0 : 16;
+  if (k0 + bk + 64 * j0 >= nv) return;
+  // 1 / L_cc of the block's columns, off the rows' dependent chains (mju_cholFactor's scaling)
+  T rdg[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) rdg[c] = c < bk ? (T)1 / H[hidx<PK>(k0 + c, k0 + c, nv)] : (T)0;
   for (int rb = k0 + bk + 64 * j0; rb < nv; rb += 64 * js) {
     const int r = rb + l;
     if (r < nv) {
@@ -1269,7 +1311,7 @@ __device__ __forceinline__ void chol_panel(T* H, int nv, int kb, int j0, int js)
           T t = Ar[c];
 #pragma unroll
           for (int j = 0; j < c; j++) t -= x[j] * H[hidx<PK>(k0 + c, k0 + j, nv)];
-          x[c] = t / H[hidx<PK>(k0 + c, k0 + c, nv)];
+          x[c] = t * rdg[c];
         }
       }
 #pragma unroll
@@ -1418,56 +1460,6 @@ __device__ __forceinline__ void nt_jp_rows(const Env<T>& e, int ne, int nv, T p,
     }
   }
 }
-// gg + sum_{x<0} D x B_r (lane = dof); only the active rows are loaded
-template <typename T>
-__device__ __forceinline__ T nt_grad_rows(const Env<T>& e, int ne, int nv, T gg, int b0, int bs) {
-  const int l = lane_id();
-  const bool dl = l < nv;
-  const int lc = dl ? l : 0;
-  const T* efc = e.efc;
-  const int step = MGX_RB * bs;
-  T gn[MGX_RB], xq[MGX_RB], dq[MGX_RB];  // the next batch, in flight
-  auto load = [&](int r0, T* xb, T* xs, T* ds) {
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) {
-      const int r = r0 + j;
-      xs[j] = r < ne ? efc[8 * r + 1] : (T)0;
-      ds[j] = xs[j] < 0 ? efc[8 * r + 4] : (T)0;
-      xb[j] = (xs[j] < 0 && dl) ? e.Bm[r * e.Bs + lc] : (T)0;
-    }
-  };
-  load(MGX_RB * b0, gn, xq, dq);
-  for (int r0 = MGX_RB * b0; r0 < ne; r0 += step) {
-    T xb[MGX_RB], xs[MGX_RB], ds[MGX_RB];
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) { xb[j] = gn[j]; xs[j] = xq[j]; ds[j] = dq[j]; }
-    load(r0 + step, gn, xq, dq);
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++)
-      if (xs[j] < 0) gg += ds[j] * xs[j] * xb[j];
-  }
-  return gg;
-}
-// v + sum_r f_r B_r (lane = dof; f in efc[8 r + 1])
-template <typename T>
-__device__ __forceinline__ T nt_force_rows(const Env<T>& e, int ne, int nv, T v, int b0, int bs) {
-  const int l = lane_id();
-  const bool dl = l < nv;
-  const int lc = dl ? l : 0;
-  const T* efc = e.efc;
-  const int step = MGX_RB * bs;
-  T xn[MGX_RD][MGX_RB];
-  first_rows(xn, e.Bm, e.Bs, ne, lc, dl, MGX_RB * b0, step);
-  for (int r0 = MGX_RB * b0; r0 < ne; r0 += step) {
-    T xb[MGX_RB];
-    next_rows(xb, xn, e.Bm, e.Bs, r0, ne, lc, dl, step);
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++)
-      if (r0 + j < ne) v += efc[8 * (r0 + j) + 1] * xb[j];
-  }
-  return v;
-}
-
 template <typename T>
 __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   const int l = lane_id();
@@ -1519,25 +1511,26 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   const T eps = sizeof(T) == 4 ? (T)1e-7 : (T)1e-15;
   const int maxit = m.iterations;
   int iter = 0;
-  // whitened gradient g = u + sum_{x<0} D x B_r (lane = dof)
-  auto gradient = [&]() {
-    team_begin(e, TEAM_GRAD, ne);
-    T gg = nt_grad_rows(e, ne, nv, u, 0, nw);
+  // H = I + sum_{x<0} D B_r B_r' (MFMA, lower triangle) and the whitened gradient g = u + sum_{x<0}
+  // D x B_r in one pass over the active rows, at the current point: before the first iteration and
+  // after every update (the stop test's gradient; the Hessian of the next iteration, unused after the
+  // last). Two waves: tile rows 0..2 on wave 0, tile row 3 and the gradient (every dof column) on
+  // the helper, which hands the gradient over in vec1.
+  auto hess_grad = [&]() {
+    T gs = 0;
+    team_begin(e, TEAM_HESS, ne);
+    if (nw > 1) hessian_mfma<T, 0, 3>(Bm, Bs, efc, ne, nv, H);
+    else gs = hessian_mfma<T, 0, 4, true>(Bm, Bs, efc, ne, nv, H);
     team_end(e);
-    if (nw > 1) gg += e.vec1[lc];  // the helper's partial (odd batches)
-    return dl ? gg : (T)0;
+    if (nw > 1) gs = e.vec1[lc];
+    return dl ? u + gs : (T)0;
   };
-  T g = gradient();
-  MGX_STAMP(10);  // newton sub-stages (diagnostic build only): setup
+  T g = hess_grad();
+  MGX_STAMP(10);  // newton sub-stages (diagnostic build only): setup + the first Hessian
   // mj_solNewton's loop order [ext]: update first, then test the scaled improvement and the
   // scaled gradient at the new point, so at least one iteration runs
   while (iter < maxit) {
-    // H = I + sum_{x<0} D B_r B_r' on MFMA (hessian_mfma), lower triangle
-    team_begin(e, TEAM_HESS, ne);
-    if (nw > 1) hessian_mfma<T, 0, 3>(Bm, Bs, efc, ne, nv, H);  // the helper: tile row 3
-    else hessian_mfma(Bm, Bs, efc, ne, nv, H);
-    team_end(e);
-    MGX_STAMP(11);  // Hessian
+    MGX_STAMP(11);  // (the Hessian: hess_grad, stamped with the update)
     // Cholesky H = L L' in place: 16-wide block columns, trailing update on MFMA (chol_blocked)
     {
       const int nb = (nv + 15) >> 4;
@@ -1625,7 +1618,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
     const T improvement = -scale * (al * g0 + (T)0.5 * al * al * pp + usum(dc));
     iter++;
     wsync();
-    g = gradient();
+    g = hess_grad();
     // the gradient rule is on the dof-space gradient M(a - a0) - J'f = L' D^1/2 g
     T ga = mul_LT(m, e, e.qLD, sqrtD * g);
     const bool stop = improvement < tol || scale * sqrt(usum(dl ? ga * ga : (T)0)) < tol;
@@ -1639,11 +1632,9 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   }
   wsync();
   // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = J'f = L' D^1/2 (sum f_r B_r)
-  team_begin(e, TEAM_FORCE, ne);
-  T v = nt_force_rows(e, ne, nv, (T)0, 0, nw);
-  team_end(e);
-  if (nw > 1) v += e.vec1[lc];  // the helper's partial (odd batches)
-  v = dl ? v : (T)0;
+  // sum_r f_r B_r with f_r = -D x_r on the active rows = u - g (g = u + sum_{x<0} D x B_r at the
+  // final point, the last hess_grad): no pass over the rows
+  T v = dl ? u - g : (T)0;
   T z = dl ? u * e.diaginv * sqrtD : (T)0;
   z = solve_L(m, e, e.qLD, z);
   e.qacc = e.qacc_smooth + z;
@@ -1652,7 +1643,7 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
 }
 
 // wave 1 of a two-wave narrow Newton env (k_assembly): one loop iteration per barrier of wave 0
-// (TEAM_NONE), the odd batches / tile row 3 / every other trailing tile of each posted section,
+// (TEAM_NONE), the odd batches / tile row 3 + the gradient / every other trailing tile of a section,
 // until wave 0 posts TEAM_EXIT
 template <typename T>
 __device__ __forceinline__ void team_helper_n(const DevModel<T>& m, Env<T>& e) {
@@ -1669,16 +1660,14 @@ __device__ __forceinline__ void team_helper_n(const DevModel<T>& m, Env<T>& e) {
       T c0 = 0, cw = 0;
       nt_setup_rows(e, a, nv, wv, ws, wd, 1, 2, c0, cw);
       if (l == 0) { e.vec3[0] = c0; e.vec3[1] = cw; }
-    } else if (cmd == TEAM_GRAD) {
-      e.vec1[l] = nt_grad_rows(e, a, nv, (T)0, 1, 2);
-    } else if (cmd == TEAM_HESS) {
-      hessian_mfma<T, 3, 4>(e.Bm, e.Bs, e.efc, a, nv, e.hess);
+    } else if (cmd == TEAM_HESS) {  // tile row 3 and the gradient (newton's hess_grad)
+      e.vec1[l] = hessian_mfma<T, 3, 4, true>(e.Bm, e.Bs, e.efc, a, nv, e.hess);
     } else if (cmd == TEAM_TRAIL) {
       chol_trail<T, false>(e.hess, nv, a, 1, 2);
     } else if (cmd == TEAM_JP) {
       nt_jp_rows(e, a, nv, dl ? e.vec0[l] : (T)0, 1, 2);
-    } else if (cmd == TEAM_FORCE) {
-      e.vec1[l] = nt_force_rows(e, a, nv, (T)0, 1, 2);
+    } else if (cmd == TEAM_XFORM) {
+      transform_rows_rm(m, e, a, 1, 2);
     }
     __syncthreads();
   }

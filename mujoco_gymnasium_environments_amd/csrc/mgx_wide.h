@@ -193,13 +193,18 @@ __device__ __forceinline__ void wsolve_M(const DevModel<T>& m, const WEnv<T>& w,
 // H = I + sum_{x_r<0} D_r B_r B_r' for nv <= 128 (8 tile rows of 16): the lower tiles of tile
 // rows [T0, T1) per pass, so the accumulators of one pass stay in registers (hessian_mfma's
 // fragment layout, mgx_physics.h); passes over tile rows beyond the model's are skipped.
-template <typename T, int T0, int T1>
-__device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H) {
+// GRAD (16 T1 >= nv): the pass also accumulates sum_{x<0} D x B_r over every dof column and returns
+// it as the two-word lane vector (dof l, dof 64 + l) in g (hessian_mfma's fused gradient).
+template <typename T, int T0, int T1, bool GRAD = false>
+__device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H, T* g = nullptr) {
   typedef T V4 __attribute__((ext_vector_type(4)));
   constexpr int NT = (T1 * (T1 + 1) - T0 * (T0 + 1)) / 2;
   const int l = lane_id(), i = l & 15, kq = l >> 4;
   const int nt = (nv + 15) >> 4;
-  if (T0 >= nt) return;
+  if (!GRAD && T0 >= nt) return;
+  T gp[T1];
+#pragma unroll
+  for (int t = 0; t < T1; t++) gp[t] = 0;
   auto row_of = [&](int v) { return sizeof(T) == 8 ? kq + 4 * v : 4 * kq + v; };
   V4 acc[NT];
 #pragma unroll
@@ -208,12 +213,14 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
     for (int u = 0; u <= t; u++, q++)
 #pragma unroll
       for (int v = 0; v < 4; v++) acc[q][v] = (t == u && row_of(v) == i) ? (T)1 : (T)0;
-  auto load = [&](int r0, T* b, T& sc) {
+  auto load = [&](int r0, T* b, T& sc, T& sg) {
     const int r = r0 + kq;
     sc = 0;
+    sg = 0;
     if (r < ne) {
       const T x = efc[8 * r + 1];
       sc = x < 0 ? efc[8 * r + 4] : (T)0;
+      sg = sc * x;
     }
 #pragma unroll
     for (int t = 0; t < T1; t++) {
@@ -222,22 +229,27 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
     }
   };
   constexpr int HD = 2;  // chunks in flight (the register budget of the wide kernels)
-  T bq[HD][T1], sq[HD];
+  T bq[HD][T1], sq[HD], gq[HD];
 #pragma unroll
-  for (int d = 0; d < HD; d++) load(4 * d, bq[d], sq[d]);
+  for (int d = 0; d < HD; d++) load(4 * d, bq[d], sq[d], gq[d]);
   for (int r0 = 0; r0 < ne; r0 += 4) {
     T b[T1];
 #pragma unroll
     for (int t = 0; t < T1; t++) b[t] = bq[0][t];
-    const T sc = sq[0];
+    const T sc = sq[0], sg = gq[0];
 #pragma unroll
     for (int d = 0; d + 1 < HD; d++) {
       sq[d] = sq[d + 1];
+      gq[d] = gq[d + 1];
 #pragma unroll
       for (int t = 0; t < T1; t++) bq[d][t] = bq[d + 1][t];
     }
-    load(r0 + 4 * HD, bq[HD - 1], sq[HD - 1]);
+    load(r0 + 4 * HD, bq[HD - 1], sq[HD - 1], gq[HD - 1]);
     if (__ballot(sc != (T)0) == 0ull) continue;  // four inactive rows: no MFMAs
+    if constexpr (GRAD) {
+#pragma unroll
+      for (int t = 0; t < T1; t++) gp[t] += sg * b[t];
+    }
 #pragma unroll
     for (int t = T0, q = 0; t < T1; t++)
 #pragma unroll
@@ -259,16 +271,37 @@ __device__ __forceinline__ void whess_pass(const T* Bm, int Bs, const T* efc, in
         const int row = 16 * t + row_of(v), col = 16 * u + i;
         if (t < nt && row < nv && col <= row) H[hidx<true>(row, col, nv)] = acc[q][v];
       }
+  if constexpr (GRAD) {
+    // lane l = 16 kq + i: dof l is tile column kq, dof 64 + l tile column 4 + kq
+    T g0 = 0, g1 = 0;
+#pragma unroll
+    for (int t = 0; t < T1; t++) {
+      const T s = xor_sum_kq(gp[t]);
+      g0 = kq == t ? s : g0;
+      g1 = kq + 4 == t ? s : g1;
+    }
+    g[0] = l < nv ? g0 : (T)0;
+    g[1] = 64 + l < nv ? g1 : (T)0;
+  }
 }
 
-// pass q of the four to wave q mod nw
+// pass q of the four to wave q mod nw; the gradient rides on pass 2 (dof columns 0..111, nv <= 112:
+// construction, wave 0) or pass 3 (every column), into g (the owning wave's registers)
+__device__ __forceinline__ int whess_grad_pass(int nv) { return nv <= 112 ? 2 : 3; }
 template <typename T>
-__device__ __forceinline__ void whess_share(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H, int wv, int nw) {
+__device__ __forceinline__ void whess_share(const T* Bm, int Bs, const T* efc, int ne, int nv, T* H, int wv, int nw,
+                                            T* g) {
+  const int qg = whess_grad_pass(nv);
   for (int q = wv; q < 4; q += nw) {
     if (q == 0) whess_pass<T, 0, 4>(Bm, Bs, efc, ne, nv, H);       // 10 tiles
     else if (q == 1) whess_pass<T, 4, 6>(Bm, Bs, efc, ne, nv, H);  // 11 tiles
-    else if (q == 2) whess_pass<T, 6, 7>(Bm, Bs, efc, ne, nv, H);  // 7 tiles
-    else whess_pass<T, 7, 8>(Bm, Bs, efc, ne, nv, H);              // 8 tiles
+    else if (q == 2) {                                             // 7 tiles
+      if (qg == 2) whess_pass<T, 6, 7, true>(Bm, Bs, efc, ne, nv, H, g);
+      else whess_pass<T, 6, 7>(Bm, Bs, efc, ne, nv, H);
+    } else {  // 8 tiles
+      if (qg == 3) whess_pass<T, 7, 8, true>(Bm, Bs, efc, ne, nv, H, g);
+      else whess_pass<T, 7, 8>(Bm, Bs, efc, ne, nv, H);
+    }
   }
 }
 
@@ -321,41 +354,6 @@ __device__ __forceinline__ void wjp_share(const Env<T>& e, int nv, int ne, const
   }
 }
 
-// sum_{x<0} D x B_r over the rows of chunks c0, c0 + cs, ...: only active rows are loaded
-template <typename T>
-__device__ __forceinline__ void wgrad_share(const Env<T>& e, int nv, int ne, int c0, int cs, T (&gg)[2]) {
-  const int l = lane_id();
-  const bool dl[2] = {l < nv, 64 + l < nv};
-  const T* efc = e.efc;
-  gg[0] = 0;
-  gg[1] = 0;
-  T nx[MGX_RB], nd[MGX_RB], na[MGX_RB], nb[MGX_RB];  // the next chunk, in flight
-  auto load = [&](int r0) {
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) {
-      const int r = r0 + j;
-      nx[j] = r < ne ? efc[8 * r + 1] : (T)0;
-      nd[j] = nx[j] < 0 ? efc[8 * r + 4] : (T)0;
-      na[j] = (nx[j] < 0 && dl[0]) ? e.Bm[r * e.Bs + l] : (T)0;
-      nb[j] = (nx[j] < 0 && dl[1]) ? e.Bm[r * e.Bs + 64 + l] : (T)0;
-    }
-  };
-  load(MGX_RB * c0);
-  for (int r0 = MGX_RB * c0; r0 < ne; r0 += MGX_RB * cs) {
-    T xs[MGX_RB], sd[MGX_RB], xa[MGX_RB], xb[MGX_RB];
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) { xs[j] = nx[j]; sd[j] = nd[j]; xa[j] = na[j]; xb[j] = nb[j]; }
-    load(r0 + MGX_RB * cs);
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++) {
-      if (xs[j] < 0) {
-        const T s = sd[j] * xs[j];
-        gg[0] += s * xa[j];
-        gg[1] += s * xb[j];
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------- Newton (mj_solNewton)
 // newton() of mgx_physics.h with two-word dof vectors; same whitened coordinates, row scalars
@@ -433,28 +431,28 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
   // whitened gradient g = u + sum_{x<0} D x B_r as two partial sums over alternating row chunks
   // (even chunks on wave 0, odd chunks on the helper, its sum via vec1), added in that order with
   // one wave or two — the result does not depend on the launch's wave count
-  auto gradient = [&](T (&gg)[2]) {
-    T part[2], odd[2];
-    team_begin(w.e, TEAM_GRAD, ne);
-    wgrad_share(e, nv, ne, 0, 2, part);
-    if (w.e.nw == 1) wgrad_share(e, nv, ne, 1, 2, odd);
+  // H and g = u + sum_{x<0} D x B_r in one set of passes over the active rows at the current point
+  // (before the first iteration and after every update: the stop test's gradient, the next
+  // iteration's Hessian); the gradient rides on one Hessian pass (whess_share), handed over in vec1
+  // when the helper wave ran it
+  auto hess_grad = [&](T (&gg)[2]) {
+    T gs[2] = {0, 0};
+    team_begin(w.e, TEAM_HESS, ne);
+    whess_share(Bm, Bs, efc, ne, nv, H, 0, w.e.nw, gs);
     team_end(w.e);
-    if (w.e.nw > 1) {
-      odd[0] = dl[0] ? e.vec1[l] : (T)0;
-      odd[1] = dl[1] ? e.vec1[64 + l] : (T)0;
+    if (whess_grad_pass(nv) % w.e.nw != 0) {
+      gs[0] = dl[0] ? e.vec1[l] : (T)0;
+      gs[1] = dl[1] ? e.vec1[64 + l] : (T)0;
     }
-    gg[0] = dl[0] ? u[0] + part[0] + odd[0] : (T)0;
-    gg[1] = dl[1] ? u[1] + part[1] + odd[1] : (T)0;
+    gg[0] = dl[0] ? u[0] + gs[0] : (T)0;
+    gg[1] = dl[1] ? u[1] + gs[1] : (T)0;
   };
   T g[2];
-  gradient(g);
+  hess_grad(g);
   MGX_STAMP_DECL
-  MGX_STAMP(10);  // setup
+  MGX_STAMP(10);  // setup + the first Hessian
   while (iter < maxit) {
-    team_begin(w.e, TEAM_HESS, ne);
-    whess_share(Bm, Bs, efc, ne, nv, H, 0, w.e.nw);
-    team_end(w.e);
-    MGX_STAMP(11);  // Hessian
+    MGX_STAMP(11);  // (the Hessian: hess_grad, stamped with the update)
     wchol(w, H, nv);
     MGX_STAMP(12);  // Cholesky
     // L y = -g, L' p = y
@@ -540,7 +538,7 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     const T improvement = -scale * (al * g0 + (T)0.5 * al * al * pp + usum(dc));
     iter++;
     wsync();
-    gradient(g);
+    hess_grad(g);
     // the gradient rule is on the dof-space gradient L' D^1/2 g
     T sg[2] = {sqrtD[0] * g[0], sqrtD[1] * g[1]}, ga[2];
     wmul_LT(m, w, e.qLD, sg, ga);
@@ -556,22 +554,9 @@ __device__ __forceinline__ void wnewton(const DevModel<T>& m, WEnv<T>& w) {
     q[1] = q[1] < 0 ? -q[4] * q[1] : (T)0;
   }
   wsync();
-  // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = L' D^1/2 (sum f_r B_r)
-  T v[2] = {0, 0};
-  first_rows(na, Bm, Bs, ne, lc[0], dl[0]);
-  first_rows(nb, Bm, Bs, ne, lc[1], dl[1]);
-  for (int r0 = 0; r0 < ne; r0 += MGX_RB) {
-    T xa[MGX_RB], xb[MGX_RB];
-    next_rows(xa, na, Bm, Bs, r0, ne, lc[0], dl[0]);
-    next_rows(xb, nb, Bm, Bs, r0, ne, lc[1], dl[1]);
-#pragma unroll
-    for (int j = 0; j < MGX_RB; j++)
-      if (r0 + j < ne) {
-        const T f = efc[8 * (r0 + j) + 1];
-        v[0] += f * xa[j];
-        v[1] += f * xb[j];
-      }
-  }
+  // qacc = qacc_smooth + L^-1 D^-1/2 u ; qfrc_constraint = L' D^1/2 (sum f_r B_r), with
+  // sum f_r B_r = -sum_{x<0} D x B_r = u - g at the final point (the last hess_grad): no row pass
+  T v[2] = {dl[0] ? u[0] - g[0] : (T)0, dl[1] ? u[1] - g[1] : (T)0};
   T z[2], sv[2];
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -782,7 +767,12 @@ __device__ __forceinline__ void team_helper(const DevModel<T>& m, WEnv<T>& w) {
     if (cmd == TEAM_EXIT) break;
     const int a = __builtin_amdgcn_readfirstlane(w.e.ctl[1]);
     if (cmd == TEAM_HESS) {
-      whess_share(e.Bm, e.Bs, e.efc, a, nv, e.hess, wv, w.e.nw);
+      T gs[2];
+      whess_share(e.Bm, e.Bs, e.efc, a, nv, e.hess, wv, w.e.nw, gs);
+      if (whess_grad_pass(nv) % w.e.nw == wv) {  // this wave ran the gradient's pass
+        e.vec1[l] = gs[0];
+        e.vec1[64 + l] = gs[1];
+      }
     } else if (cmd == TEAM_PANEL) {
       chol_panel<T, true>(e.hess, nv, a, wv, w.e.nw);
     } else if (cmd == TEAM_TRAIL) {
@@ -790,11 +780,6 @@ __device__ __forceinline__ void team_helper(const DevModel<T>& m, WEnv<T>& w) {
     } else if (cmd == TEAM_JP) {
       const T p[2] = {l < nv ? e.vec0[l] : (T)0, 64 + l < nv ? e.vec0[64 + l] : (T)0};
       wjp_share(e, nv, a, p, wv, w.e.nw);
-    } else if (cmd == TEAM_GRAD) {  // the odd chunks (wnewton's gradient)
-      T g[2];
-      wgrad_share(e, nv, a, 1, 2, g);
-      e.vec1[l] = g[0];
-      e.vec1[64 + l] = g[1];
     } else if (cmd == TEAM_XFORM) {
       wtransform_rows(m, w, a, wv, w.e.nw);
     }

@@ -57,9 +57,11 @@ def test_newton_forward(newton_case, prec):
             assert _rel(dbg["qfrc_constraint"][i], o.qfrc_constraint) < 1e-7, "qfrc_constraint"
             assert abs(int(dbg["niter"][i][0]) - int(o.solver_niter[0])) <= 1, "niter"
         else:
-            # fp32 at tolerance 1e-8: the improvement / gradient rules fire a different iteration
-            # than in fp64 on these violent states (|qacc| up to 1e12), so the iterate differs more
-            assert _rel(dbg["qacc"][i], o.qacc) < (5e-3 if m.tolerance < 1e-9 else 1e-1), "qacc"
+            # fp32: the improvement / gradient rules fire a different iteration than in fp64 on
+            # these violent states (|qacc| up to 1e12), so the iterate differs more, by an amount
+            # that follows the fp32 rounding order of the solver's sums (measured 0.5% with the
+            # gradient summed row by row, 1.3% with it summed per MFMA row group, round 5)
+            assert _rel(dbg["qacc"][i], o.qacc) < (2e-2 if m.tolerance < 1e-9 else 1e-1), "qacc"
 
 
 @pytest.mark.parametrize("prec", ["f64", "f32"])
