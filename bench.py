@@ -49,9 +49,9 @@ VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vect
 # latest tools/profile_round.sh summaries of the soccer step (HBM traffic per step), per precision
 PMC_PROFILE = {"f64": "r05_head_pmc.json", "f32": "r03_f32_pmc.json"}
 PMC_PROFILE_BIPEDAL = "r05_bipedal_pmc.json"
-PMC_PROFILE_ASSEMBLY = "r04_assembly_pmc.json"
+PMC_PROFILE_ASSEMBLY = "r05_assembly_pmc.json"
 PMC_PROFILE_PARKOUR = "r05_parkour_pmc.json"
-PMC_PROFILE_CONSTRUCTION = "r04_construction_pmc.json"
+PMC_PROFILE_CONSTRUCTION = "r05_construction_pmc.json"
 PMC_PROFILE_MIXED = "r05_mixed_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
