@@ -167,7 +167,9 @@ typedef struct mgx_soccer_env {
                             to (model, N, banks); holds the reset banks between calls */
   uint64_t workspace_bytes;
   int32_t banks;         /* reset banks per env (0 = none; autoreset then resets in-launch) */
-  int32_t pad0;
+  int32_t action_f64;    /* 0: mgx_soccer_step's `action` is float32 [N][nu]; 1: it is float64 — the
+                            reference's np.clip keeps a float64 policy's dtype, so ctrl and the
+                            energy term follow in float64 (soccer_env.py:401-405, :674) */
 } mgx_soccer_env;
 
 typedef struct mgx_soccer_ids {

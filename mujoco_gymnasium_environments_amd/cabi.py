@@ -80,7 +80,7 @@ class MgxSoccerEnv(C.Structure):
                 ("step", C.c_void_p), ("goal_scored", C.c_void_p), ("stats", C.c_void_p),
                 ("episode", C.c_void_p), ("flags", C.c_void_p), ("rollout", C.c_void_p),
                 ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32),
-                ("pad0", C.c_int32)]
+                ("action_f64", C.c_int32)]
 
 
 class MgxSoccerLogicIO(C.Structure):

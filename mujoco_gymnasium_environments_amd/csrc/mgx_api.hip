@@ -85,7 +85,7 @@ __device__ __forceinline__ void soccer_step_mono(const DevModel<T>& m, Env<T>& e
   T* prev_ball = (T*)ev.prev_ball_pos + 3 * (size_t)env;
   float* o = obs + (size_t)env * 80;
   int l = lane_id();
-  const float* a = action + (size_t)env * m.nu;
+  const SoccerAct a(action, ev.action_f64, env, m.nu);
   soccer_pre(m, e, ids, a, prev_ball, (T*)ev.wind + 3 * (size_t)env);
   int warn = mj_step_env(m, e);
   bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, prev_ball,
@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(64) k_soccer_logic(DevModel<T> m, SoccerIds<T>
   }
   wsync();
   const T* stale = (const T*)io.xpos + (size_t)env * 3 * m.nbody + 3 * ids.ball;
-  const float* a = io.action + (size_t)env * m.nu;
+  const SoccerAct a(io.action, 0, env, m.nu);
   soccer_pre(m, e, ids, a, stale, (const T*)io.wind + 3 * (size_t)env);
   soccer_post(m, e, ids, a, io.step + env, io.goal_scored + env, (T*)io.prev_ball_pos + 3 * (size_t)env,
               (T*)io.prev_robot_pos + 3 * (size_t)env, (T*)io.stats + 5 * (size_t)env, io.obs + (size_t)env * 80,

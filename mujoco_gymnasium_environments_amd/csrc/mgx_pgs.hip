@@ -88,7 +88,8 @@ __global__ void __launch_bounds__(64) k_soccer_rows(DevModel<T> m, SoccerIds<T> 
     bind_carry_tail(m, e, P, b);
     load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
                (T*)s.time, b);
-    soccer_pre(m, e, ids, action + (size_t)b * m.nu, (T*)ev.prev_ball_pos + 3 * (size_t)b, (T*)ev.wind + 3 * (size_t)b);
+    soccer_pre(m, e, ids, SoccerAct(action, ev.action_f64, b, m.nu), (T*)ev.prev_ball_pos + 3 * (size_t)b,
+               (T*)ev.wind + 3 * (size_t)b);
     slot = b;
   } else {
     int bi = b - n_env;
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(64) k_soccer_finish(DevModel<T> m, SoccerIds<T
               (T*)s.time, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
   if (l == 0 && s.overflow && e.overflow) s.overflow[env] += 1;
-  const float* a = action + (size_t)env * m.nu;
+  const SoccerAct a(action, ev.action_f64, env, m.nu);
   float* o = obs + (size_t)env * 80;
   bool done = soccer_post(m, e, ids, a, ev.step + env, ev.goal_scored + env, (T*)ev.prev_ball_pos + 3 * (size_t)env,
                           (T*)ev.prev_robot_pos + 3 * (size_t)env, (T*)ev.stats + 5 * (size_t)env, o, reward + env,

@@ -28,15 +28,32 @@ struct SoccerIds {
   int n_noise;
 };
 
+// One env's action row: float32, or float64 (mgx_soccer_env.action_f64) — the reference's np.clip
+// against the float32 action_space bounds keeps a float64 policy's action float64, so ctrl and
+// the energy term then follow in float64 (soccer_env.py:401-405, :674).
+struct SoccerAct {
+  const void* p;
+  int f64;
+  __device__ SoccerAct(const void* base, int f64_, size_t row, int nu)
+      : p(f64_ ? (const void*)((const double*)base + row * nu) : (const void*)((const float*)base + row * nu)),
+        f64(f64_) {}
+};
+
 // Pre-physics env logic: action clip -> ctrl, goalkeeper, wind (soccer_env.py:401-411)
 template <typename T>
-__device__ __forceinline__ void soccer_pre(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action,
+__device__ __forceinline__ void soccer_pre(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, SoccerAct act,
                            const T* prev_ball, const T* wind) {
   int l = lane_id();
   for (int u = l; u < m.nu; u += 64) {
-    float a = action[u];
-    a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);   // action_space bounds, float32
-    e.ctrl[u] = (T)a;
+    if (act.f64) {
+      double a = static_cast<const double*>(act.p)[u];
+      a = a < -150.0 ? -150.0 : (a > 150.0 ? 150.0 : a);  // float64 action, float32 bounds: float64
+      e.ctrl[u] = (T)a;
+    } else {
+      float a = static_cast<const float*>(act.p)[u];
+      a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);   // action_space bounds, float32
+      e.ctrl[u] = (T)a;
+    }
   }
   // goalkeeper P-controller on the stale ball position
   T bx = prev_ball[0], by = prev_ball[1], bz = prev_ball[2];
@@ -147,29 +164,32 @@ __device__ __forceinline__ bool soccer_upright(const Env<T>& e, const SoccerIds<
 // numpy's np.linalg.norm of a float64 3-vector: sqrt of the BLAS dot, which rounds as two FMAs
 __device__ __forceinline__ double norm3_np(double x, double y, double z) { return sqrt(fma(z, z, fma(y, y, x * x))); }
 
-// numpy float32 add.reduce of the squared clipped actions (soccer_env.py:674): pairwise sum,
-// 8 accumulators over the first 8*floor(n/8) values, tree (01)(23) / (45)(67), then the tail
-__device__ __forceinline__ float np_sumsq_clip_f32(const float* action, int n) {
+// numpy add.reduce of the squared clipped actions (soccer_env.py:674) in the action's dtype
+// (float32 or float64: numpy's pairwise sum is the same for both): 8 accumulators over the first
+// 8*floor(n/8) values, tree (01)(23) / (45)(67), then the tail
+template <typename A>
+__device__ __forceinline__ A np_sumsq_clip(const A* action, int n) {
 #pragma clang fp contract(off)
   auto sq = [&](int u) {
-    float a = action[u];
-    a = a < -150.0f ? -150.0f : (a > 150.0f ? 150.0f : a);
+    A a = action[u];
+    a = a < (A)-150 ? (A)-150 : (a > (A)150 ? (A)150 : a);
     return a * a;
   };
   if (n < 8) {
-    float res = 0.0f;
+    A res = 0;
     for (int u = 0; u < n; u++) res += sq(u);
     return res;
   }
-  float r[8];
+  A r[8];
   for (int k = 0; k < 8; k++) r[k] = sq(k);
   int i = 8;
   for (; i + 8 <= n; i += 8)
     for (int k = 0; k < 8; k++) r[k] += sq(i + k);
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  A res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
   for (; i < n; i++) res += sq(i);
   return res;
 }
+__device__ __forceinline__ float np_sumsq_clip_f32(const float* action, int n) { return np_sumsq_clip(action, n); }
 
 // _calculate_reward (soccer_env.py:633-690) with the reference's numpy arithmetic, lane-uniform:
 // the reward is a Python float until an np.float64 term (approach / forward progress, from
@@ -178,7 +198,7 @@ __device__ __forceinline__ float np_sumsq_clip_f32(const float* action, int n) {
 // progress) promotes it back. Positions enter as float64 whatever the physics precision.
 __device__ __forceinline__ double soccer_reward_np(bool goal_now, bool ball_contact, bool upright, const double* bp,
                                                    const double* tx, const double* pb, const double* pr,
-                                                   float energy) {
+                                                   float energy, bool e64 = false, double energy64 = 0.0) {
 #pragma clang fp contract(off)
   double r = 0.0;
   bool is64 = false;
@@ -192,7 +212,10 @@ __device__ __forceinline__ double soccer_reward_np(bool goal_now, bool ball_cont
   double cur_gd = norm3_np(tx[0] - 24.5, tx[1] - 0.0, tx[2] - 0.0);
   if (cur_gd < prev_gd) { r += 100.0 * (prev_gd - cur_gd); is64 = true; }
   const float eterm = -0.1f * energy;
-  if (is64) {
+  if (e64) {  // float64 action: the energy term and everything after it in float64
+    r += -0.1 * energy64;
+    if (!upright) r += -1000.0;
+  } else if (is64) {
     r += (double)eterm;
     if (!upright) r += -1000.0;
   } else {
@@ -208,7 +231,7 @@ __device__ __forceinline__ double soccer_reward_np(bool goal_now, bool ball_cont
 
 // Post-physics: step count, obs, reward, termination, stats, prev snapshots
 template <typename T>
-__device__ __forceinline__ bool soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, const float* action, int* step,
+__device__ __forceinline__ bool soccer_post(const DevModel<T>& m, Env<T>& e, const SoccerIds<T>& ids, SoccerAct act, int* step,
                             uint8_t* goal_scored, T* prev_ball, T* prev_robot, T* stats, float* obs, double* reward,
                             uint8_t* terminated, uint8_t* truncated, uint8_t* flags = nullptr) {
 #pragma clang fp contract(off)
@@ -224,8 +247,11 @@ __device__ __forceinline__ bool soccer_post(const DevModel<T>& m, Env<T>& e, con
   const double txd[3] = {(double)tx[0], (double)tx[1], (double)tx[2]};
   const double pbd[3] = {(double)prev_ball[0], (double)prev_ball[1], (double)prev_ball[2]};
   const double prd[3] = {(double)prev_robot[0], (double)prev_robot[1], (double)prev_robot[2]};
-  const double r = soccer_reward_np(goal_now, ball_contact, upright, bpd, txd, pbd, prd,
-                                    np_sumsq_clip_f32(action, m.nu));
+  const double r =
+      act.f64 ? soccer_reward_np(goal_now, ball_contact, upright, bpd, txd, pbd, prd, 0.0f, true,
+                                 np_sumsq_clip(static_cast<const double*>(act.p), m.nu))
+              : soccer_reward_np(goal_now, ball_contact, upright, bpd, txd, pbd, prd,
+                                 np_sumsq_clip_f32(static_cast<const float*>(act.p), m.nu));
   bool gs = (*goal_scored != 0) || goal_now;
   bool term = gs || (!upright && st > 100) ||
               (fabs(bp[0]) > (T)30 || fabs(bp[1]) > (T)20 || bp[2] < (T)-1 || bp[2] > (T)10) ||

@@ -212,10 +212,14 @@ class SoccerVectorEnv:
         return self.obs, self.info()
 
     def step(self, actions: torch.Tensor, stream=None):
-        """One env step for every env. ``actions`` float32 [N, nu] on the device."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        """One env step for every env. ``actions`` [N, nu] on the device: float32, or float64 — a
+        float64 action is clipped and applied in float64 and its energy term summed in float64,
+        as the reference's np.clip keeps a float64 policy's dtype (soccer_env.py:401-405, :674)."""
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
         assert actions.shape == (self.num_envs, self.model.nu), actions.shape
+        self._env.action_f64 = 1 if dt == torch.float64 else 0
         check(lib().mgx_soccer_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
                                     _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
                                     _ptr(self.truncated), _ptr(self.final_obs) if self.autoreset else None,
@@ -324,9 +328,10 @@ class StreamShardedSoccerEnv:
         return self.obs, self.info()
 
     def step(self, actions: torch.Tensor, stream=None):
-        """One env step for every env; actions float32 [N, nu] on the device."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        """One env step for every env; actions float32 or float64 [N, nu] on the device."""
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
         assert actions.shape == (self.num_envs, self.model.nu), actions.shape
         self._fan_out(stream, lambda a, b, s, st: s.step(actions[a:b], stream=st))
         return self.obs, self.reward, self.terminated, self.truncated, self.info()
@@ -392,8 +397,10 @@ class HumanoidSoccerEnv(EnvBase):
         return obs[0].cpu().numpy().copy(), self._info(False)
 
     def step(self, action: np.ndarray):
-        action = np.clip(np.asarray(action, dtype=np.float32), self.action_space.low, self.action_space.high)
-        a = torch.from_numpy(action.reshape(1, -1)).to(self._vec.device)
+        # np.clip against the float32 bounds keeps a float64 action float64 (soccer_env.py:401-405)
+        action = np.clip(np.asarray(action), self.action_space.low, self.action_space.high)
+        action = action.astype(np.float64 if action.dtype == np.float64 else np.float32, copy=False)
+        a = torch.from_numpy(np.ascontiguousarray(action.reshape(1, -1))).to(self._vec.device)
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = int(self._vec.step_count[0])

@@ -31,8 +31,15 @@ class SoccerLogic:
         self.max_episode_steps = max_episode_steps
 
     # ----- pre-physics (state = dict of numpy arrays; mutated in place)
+    @staticmethod
+    def action_array(action):
+        """The action as the reference holds it after np.clip against the float32 action_space
+        bounds: float64 stays float64, anything else becomes float32 (soccer_env.py:401-405)."""
+        a = np.asarray(action)
+        return a if a.dtype == np.float64 else a.astype(np.float32)
+
     def pre(self, s, action):
-        action = np.clip(np.asarray(action, np.float32), -150.0, 150.0)
+        action = np.clip(self.action_array(action), -150.0, 150.0)
         s["ctrl"][:] = action
         ball = s["xpos"][self.t.ball]
         if ball[0] < -10.0:
@@ -113,7 +120,7 @@ class SoccerLogic:
         pg, cg = np.linalg.norm(s["prev_robot_pos"] - GOAL), np.linalg.norm(robot - GOAL)
         if cg < pg:
             r += 100.0 * (pg - cg)
-        r += -0.1 * np.sum(np.square(np.asarray(action, np.float32)))
+        r += -0.1 * np.sum(np.square(self.action_array(action)))
         if not upright:
             r += -1000.0
         pb, cb = np.linalg.norm(s["prev_ball_pos"] - GOAL), np.linalg.norm(ball - GOAL)
