@@ -1,6 +1,6 @@
 """Print the per-env LDS footprint and capacities the library chose for a task model (GPU box).
 
-usage: python tools/lds_info.py [assembly|bipedal|soccer|soccer_full] [f32|f64]
+usage: python tools/lds_info.py [assembly|bipedal|soccer|soccer_full|martial|dancing] [f32|f64]
        (MGX_MAX_NEFC / MGX_MAX_NCON override)
 Monolithic kernels: envs per CU = floor(160 KiB / lds_bytes_per_env). Staged tasks also print
 the row builder's and the finisher's per-wave LDS (lds_bytes_rows / lds_bytes_finish).
@@ -19,6 +19,14 @@ def main(task: str, prec: str) -> None:
         from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
         e = SoccerVectorEnv(2, precision=prec, full_capacity=task == "soccer_full")
         nat = e.native
+    elif task == "martial":
+        from mujoco_gymnasium_environments_amd.envs.martial import MartialArtsVectorEnv
+        e = MartialArtsVectorEnv(2, precision=prec)
+        nat = e.batch.native if hasattr(e, "batch") else e.native
+    elif task == "dancing":
+        from mujoco_gymnasium_environments_amd.envs.dancing import DancingVectorEnv
+        e = DancingVectorEnv(2, precision=prec)
+        nat = e.batch.native if hasattr(e, "batch") else e.native
     else:
         from mujoco_gymnasium_environments_amd.envs.assembly import AssemblyVectorEnv
         e = AssemblyVectorEnv(2, precision=prec)
