@@ -401,11 +401,11 @@ __device__ __forceinline__ void next_rows(T* x, T (*xn)[MGX_RB], const T* Bm, in
 // share (no barriers inside) -> barrier -> wave 0 clears the command. With one wave (nw = 1, every
 // other kernel) the sections are plain wave barriers and wave 0 runs every share itself.
 enum { TEAM_NONE = 0, TEAM_EXIT = 1, TEAM_HESS, TEAM_PANEL, TEAM_TRAIL, TEAM_JP, TEAM_GRAD, TEAM_XFORM, TEAM_SETUP,
-       TEAM_FORCE };
+       TEAM_FORCE, TEAM_CONTACT };
 
 template <typename T>
-__device__ __forceinline__ void team_begin(Env<T>& e, int cmd, int arg) {
-  if (e.nw > 1 && lane_id() == 0) { e.ctl[0] = cmd; e.ctl[1] = arg; }
+__device__ __forceinline__ void team_begin(Env<T>& e, int cmd, int arg, int arg2 = 0) {
+  if (e.nw > 1 && lane_id() == 0) { e.ctl[0] = cmd; e.ctl[1] = arg; e.ctl[2] = arg2; }
   wsync();
 }
 template <typename T>
@@ -603,6 +603,105 @@ __device__ __forceinline__ T impedance(const T* solimp, T pos, T margin) {
   return d0 + y * (d1 - d0);
 }
 
+// The rows of contact c from row r0 (lane = dof): J_n +- mu_k J_k, then the rows' type / id /
+// pos / margin / diagApprox (lane = row)
+template <typename T>
+__device__ __forceinline__ void contact_rows(const DevModel<T>& m, Env<T>& e, int c, int r0) {
+  const int l = lane_id();
+  int p = e.con_pair[c];
+  int dim = m.pair_condim[p];
+  int nrow = dim == 1 ? 1 : 2 * (dim - 1);
+  int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
+  int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+  const T* fr = e.con_frame + 9 * c;
+  const T* pos = e.con_pos + 3 * c;
+  for (int d = l; d < m.nv; d += 64) {  // lane = dof (l, l + 64 when nv > 64)
+    T j1[3] = {0, 0, 0}, j2[3] = {0, 0, 0};
+    const T* cd = e.cdof + 6 * d;
+    if (b2 > 0 && body_has_dof(m, b2, d)) {
+      int r2 = m.body_rootid[b2];
+      T off[3] = {pos[0] - e.subtree_com[3 * r2], pos[1] - e.subtree_com[3 * r2 + 1], pos[2] - e.subtree_com[3 * r2 + 2]}, t[3];
+      cross3(t, cd, off);
+      j2[0] = cd[3] + t[0]; j2[1] = cd[4] + t[1]; j2[2] = cd[5] + t[2];
+    }
+    if (b1 > 0 && body_has_dof(m, b1, d)) {
+      int r1 = m.body_rootid[b1];
+      T off[3] = {pos[0] - e.subtree_com[3 * r1], pos[1] - e.subtree_com[3 * r1 + 1], pos[2] - e.subtree_com[3 * r1 + 2]}, t[3];
+      cross3(t, cd, off);
+      j1[0] = cd[3] + t[0]; j1[1] = cd[4] + t[1]; j1[2] = cd[5] + t[2];
+    }
+    T jd[3] = {j2[0] - j1[0], j2[1] - j1[1], j2[2] - j1[2]};
+    T cj0 = fr[0] * jd[0] + fr[1] * jd[1] + fr[2] * jd[2];
+    if (dim == 1) {
+      e.Bm[r0 * e.Bs + d] = cj0;
+    } else {
+      T cj[6];
+      cj[1] = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
+      cj[2] = fr[6] * jd[0] + fr[7] * jd[1] + fr[8] * jd[2];
+      if (dim > 3) {
+        // relative angular motion: the rotational parts of the dof's motion subspace
+        T jr[3] = {0, 0, 0};
+        if (b2 > 0 && body_has_dof(m, b2, d)) { jr[0] += cd[0]; jr[1] += cd[1]; jr[2] += cd[2]; }
+        if (b1 > 0 && body_has_dof(m, b1, d)) { jr[0] -= cd[0]; jr[1] -= cd[1]; jr[2] -= cd[2]; }
+        cj[3] = fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2];
+        cj[4] = fr[3] * jr[0] + fr[4] * jr[1] + fr[5] * jr[2];
+        cj[5] = fr[6] * jr[0] + fr[7] * jr[1] + fr[8] * jr[2];
+      }
+      for (int k = 1; k < dim; k++) {
+        T mu = m.pair_friction[5 * p + k - 1];
+        e.Bm[(r0 + 2 * (k - 1)) * e.Bs + d] = cj0 + mu * cj[k];
+        e.Bm[(r0 + 2 * (k - 1) + 1) * e.Bs + d] = cj0 - mu * cj[k];
+      }
+    }
+  }
+  if (l < nrow) {
+    int r = r0 + l;
+    T tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+    T rot = m.body_invweight0[2 * b1 + 1] + m.body_invweight0[2 * b2 + 1];
+    T f = dim == 1 ? (T)0 : m.pair_friction[5 * p + (l >> 1)];
+    e.efc_type[r] = dim == 1 ? C_CONTACT_FRICTIONLESS : C_CONTACT_PYRAMIDAL;
+    e.efc_id[r] = c;
+    e.efc[8 * r + 7] = e.con_dist[c];
+    e.efc_margin[r] = m.pair_margin[p] - m.pair_gap[p];
+    e.efc[8 * r + 2] = tran + f * f * ((l >> 1) < 2 ? tran : rot);  // mj_diagApprox [ext]
+  }
+}
+
+// The contacts' rows over contacts w0, w0 + ws, ... (a helper wave takes every other contact):
+// each contact's first row from a wave scan of the row counts, and the rows end at the first
+// contact that does not fit (the serial loop's break). Returns the row count after the contacts
+// (every wave computes the same) and flags an overflow.
+template <typename T>
+__device__ __forceinline__ int contact_rows_share(const DevModel<T>& m, Env<T>& e, int ncon, int nefc0, int w0, int ws,
+                                                  bool& ovf) {
+  const int l = lane_id();
+  int total = nefc0;
+  ovf = false;
+  for (int cb = 0; cb < ncon; cb += 64) {
+    const int c = cb + l;
+    int nr = 0;
+    if (c < ncon) {
+      const int dim = m.pair_condim[e.con_pair[c]];
+      nr = dim == 1 ? 1 : 2 * (dim - 1);
+    }
+    int bt;
+    const int off = wave_excl_scan(nr, &bt);
+    const int nb = ncon - cb < 64 ? ncon - cb : 64;
+    const uint64_t valid = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+    const uint64_t fit = ballot(c < ncon && total + off + nr <= m.L.max_nefc);
+    const uint64_t bad = valid & ~fit;
+    const int kend = bad ? __builtin_ctzll(bad) : nb;
+    for (int k = w0; k < kend; k += ws) contact_rows(m, e, cb + k, total + readlane(off, k));
+    if (kend < nb) {
+      ovf = true;
+      total += readlane(off, kend);
+      break;
+    }
+    total += bt;
+  }
+  return total;
+}
+
 // joint limits then pyramidal contacts; rows are written as J and transformed in place
 template <typename T>
 __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e) {
@@ -652,66 +751,12 @@ __device__ __forceinline__ void make_constraint(const DevModel<T>& m, Env<T>& e)
   // Edge k (k = 1 .. condim-1) is J_n +- mu_k J_k with J_1, J_2 the sliding directions
   // (translational Jacobian on the tangents), J_3 torsion (rotational on the normal), J_4, J_5
   // rolling (rotational on the tangents), in MuJoCo's order [ext]
-  for (int c = 0; c < e.ncon; c++) {
-    int p = e.con_pair[c];
-    int dim = m.pair_condim[p];
-    int nrow = dim == 1 ? 1 : 2 * (dim - 1);
-    if (nefc + nrow > L.max_nefc) { e.overflow |= 4; break; }
-    int g1 = e.con_geom[2 * c], g2 = e.con_geom[2 * c + 1];
-    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-    const T* fr = e.con_frame + 9 * c;
-    const T* pos = e.con_pos + 3 * c;
-    for (int d = l; d < m.nv; d += 64) {  // lane = dof (l, l + 64 when nv > 64)
-      T j1[3] = {0, 0, 0}, j2[3] = {0, 0, 0};
-      const T* cd = e.cdof + 6 * d;
-      if (b2 > 0 && body_has_dof(m, b2, d)) {
-        int r2 = m.body_rootid[b2];
-        T off[3] = {pos[0] - e.subtree_com[3 * r2], pos[1] - e.subtree_com[3 * r2 + 1], pos[2] - e.subtree_com[3 * r2 + 2]}, t[3];
-        cross3(t, cd, off);
-        j2[0] = cd[3] + t[0]; j2[1] = cd[4] + t[1]; j2[2] = cd[5] + t[2];
-      }
-      if (b1 > 0 && body_has_dof(m, b1, d)) {
-        int r1 = m.body_rootid[b1];
-        T off[3] = {pos[0] - e.subtree_com[3 * r1], pos[1] - e.subtree_com[3 * r1 + 1], pos[2] - e.subtree_com[3 * r1 + 2]}, t[3];
-        cross3(t, cd, off);
-        j1[0] = cd[3] + t[0]; j1[1] = cd[4] + t[1]; j1[2] = cd[5] + t[2];
-      }
-      T jd[3] = {j2[0] - j1[0], j2[1] - j1[1], j2[2] - j1[2]};
-      T cj0 = fr[0] * jd[0] + fr[1] * jd[1] + fr[2] * jd[2];
-      if (dim == 1) {
-        e.Bm[nefc * e.Bs + d] = cj0;
-      } else {
-        T cj[6];
-        cj[1] = fr[3] * jd[0] + fr[4] * jd[1] + fr[5] * jd[2];
-        cj[2] = fr[6] * jd[0] + fr[7] * jd[1] + fr[8] * jd[2];
-        if (dim > 3) {
-          // relative angular motion: the rotational parts of the dof's motion subspace
-          T jr[3] = {0, 0, 0};
-          if (b2 > 0 && body_has_dof(m, b2, d)) { jr[0] += cd[0]; jr[1] += cd[1]; jr[2] += cd[2]; }
-          if (b1 > 0 && body_has_dof(m, b1, d)) { jr[0] -= cd[0]; jr[1] -= cd[1]; jr[2] -= cd[2]; }
-          cj[3] = fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2];
-          cj[4] = fr[3] * jr[0] + fr[4] * jr[1] + fr[5] * jr[2];
-          cj[5] = fr[6] * jr[0] + fr[7] * jr[1] + fr[8] * jr[2];
-        }
-        for (int k = 1; k < dim; k++) {
-          T mu = m.pair_friction[5 * p + k - 1];
-          e.Bm[(nefc + 2 * (k - 1)) * e.Bs + d] = cj0 + mu * cj[k];
-          e.Bm[(nefc + 2 * (k - 1) + 1) * e.Bs + d] = cj0 - mu * cj[k];
-        }
-      }
-    }
-    if (l < nrow) {
-      int r = nefc + l;
-      T tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-      T rot = m.body_invweight0[2 * b1 + 1] + m.body_invweight0[2 * b2 + 1];
-      T f = dim == 1 ? (T)0 : m.pair_friction[5 * p + (l >> 1)];
-      e.efc_type[r] = dim == 1 ? C_CONTACT_FRICTIONLESS : C_CONTACT_PYRAMIDAL;
-      e.efc_id[r] = c;
-      e.efc[8 * r + 7] = e.con_dist[c];
-      e.efc_margin[r] = m.pair_margin[p] - m.pair_gap[p];
-      e.efc[8 * r + 2] = tran + f * f * ((l >> 1) < 2 ? tran : rot);  // mj_diagApprox [ext]
-    }
-    nefc += nrow;
+  {
+    bool ovf;
+    team_begin(e, TEAM_CONTACT, e.ncon, nefc);
+    nefc = contact_rows_share(m, e, e.ncon, nefc, 0, e.nw, ovf);
+    team_end(e);
+    if (ovf) e.overflow |= 4;
   }
   e.nefc = __builtin_amdgcn_readfirstlane(nefc);
   wsync();
@@ -1668,6 +1713,9 @@ __device__ __forceinline__ void team_helper_n(const DevModel<T>& m, Env<T>& e) {
       nt_jp_rows(e, a, nv, dl ? e.vec0[l] : (T)0, 1, 2);
     } else if (cmd == TEAM_XFORM) {
       transform_rows_rm(m, e, a, 1, 2);
+    } else if (cmd == TEAM_CONTACT) {  // every other contact's rows (make_constraint)
+      bool ovf;
+      contact_rows_share(m, e, a, __builtin_amdgcn_readfirstlane(e.ctl[2]), 1, 2, ovf);
     }
     __syncthreads();
   }

@@ -782,6 +782,9 @@ __device__ __forceinline__ void team_helper(const DevModel<T>& m, WEnv<T>& w) {
       wjp_share(e, nv, a, p, wv, w.e.nw);
     } else if (cmd == TEAM_XFORM) {
       wtransform_rows(m, w, a, wv, w.e.nw);
+    } else if (cmd == TEAM_CONTACT) {  // every other contact's rows (make_constraint)
+      bool ovf;
+      contact_rows_share(m, e, a, __builtin_amdgcn_readfirstlane(w.e.ctl[2]), wv, w.e.nw, ovf);
     }
     __syncthreads();
   }
