@@ -358,8 +358,15 @@ def cpu_baseline_assembly(n_envs: int, n_steps: int, seed: int = 0) -> dict:
             "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
 
 
-MIXED_GROUPS = [["humanoid_construction"], ["robotic_arm_assembly"],
-                ["bipedal_rescue", "humanoid_soccer"], ["quadruped_parkour", "humanoid_martial_arts", "humanoid_dancing"]]
+# round 5 (assembly now the longest stream): soccer beside construction, dancing beside bipedal —
+# 125.8k / 126.0k / 126.5k against 125.0k / 124.5k / 124.6k env-steps/s for the round-4 grouping
+# (construction alone; bipedal + soccer; parkour + martial arts + dancing), alternating runs on one box
+MIXED_GROUPS = [["humanoid_construction", "humanoid_soccer"], ["robotic_arm_assembly"],
+                ["bipedal_rescue", "humanoid_dancing"], ["quadruped_parkour", "humanoid_martial_arts"]]
+# MGX_MIX_GROUPS (A/B hook): another grouping, groups separated by ';', tasks by ',' (group 0 is
+# the high-priority one)
+if os.environ.get("MGX_MIX_GROUPS"):
+    MIXED_GROUPS = [g.split(",") for g in os.environ["MGX_MIX_GROUPS"].split(";")]
 
 
 def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
@@ -367,10 +374,11 @@ def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
 
     HIP streams map onto GPU_MAX_HW_QUEUES hardware queues (4 on the box): with a stream per
     task (7, plus the staged tasks' side streams) unrelated tasks share queues and wait on each
-    other's kernels. Four streams instead: construction and assembly (the long Newton steps)
-    each on its own, the five PGS tasks split over two; no side streams (MGX_SIDE_STREAM=0).
-    Construction's stream (the longest) runs at high priority (mix_priority 1, measured 73.2k ->
-    75.5k env-steps/s). mix_streams 7: the old one-stream-per-task layout (67.3k)."""
+    other's kernels. Four streams instead: construction (with soccer) and assembly, the long Newton
+    steps, each on a stream of their own, the other PGS tasks in two pairs; no side streams
+    (MGX_SIDE_STREAM=0). Construction's stream runs at high priority (mix_priority 1, measured
+    73.2k -> 75.5k env-steps/s in round 4; in round 5 group 0 alone is still best: 122.7k against
+    119.4k with assembly's group, 118.9k with both). mix_streams 7: one stream per task (67.3k)."""
     if mix_streams >= len(tasks):
         return {k: torch.cuda.Stream(device=dev) for k in tasks}
     os.environ["MGX_SIDE_STREAM"] = "0"
