@@ -4,6 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N` alone (no WORLD_SIZE in the environment) starts the N rank processes itself, one per
+GPU, before any GPU call (spawn_ranks); under a launcher, --gpus must equal WORLD_SIZE.
+
 One "step" = one SoccerVectorEnv.step over all envs of a rank: action clip, goalkeeper, wind,
 mj_step (kinematics .. PGS .. Euler) and observation/reward/termination for every env, with
 same-step autoreset — mgx_soccer_step, the staged kernels k_soccer_rows -> k_pgs_groups ->
@@ -571,9 +574,70 @@ def other_precision_line(args, dev, N, g, precision: str) -> dict:
             "launch_ms": round(a.elapsed_time(b) / steps, 4), "steps": steps, "dtype": precision, "note": note}
 
 
+def spawn_ranks(n: int, argv) -> int:
+    """``--gpus N`` without an outer launcher: start N rank processes of this script, one per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), the way
+    ``torch.distributed.run --nproc-per-node N`` would, and wait for them. Called before anything
+    touches the GPU (the parent never initialises HIP); rank 0 prints the one JSON line. Returns
+    the first non-zero exit status of the ranks (0 when every rank succeeded)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def cpu_harness(args, world: int, rank: int, dist) -> None:
+    """``--harness cpu``: bench.py's multi-rank machinery (spawn, rendezvous, env shards, timed
+    region, SUM / MAX reduction, rank-0 JSON line) with gloo and the oracle soccer env standing in
+    for RCCL and the GPU step, so the N-rank path is testable on a CPU-only host
+    (tests/test_distributed_cpu.py). Not a benchmark: the line says so in its `data` field."""
+    from mujoco_gymnasium_environments_amd.distributed import env_offset
+    n = args.envs
+    envs = [OracleSoccerEnv(env_offset(rank, n) + i, seed=5) for i in range(n)]
+    acts = np.random.default_rng(0).uniform(-150, 150, (max(1, args.steps + args.warmup), envs[0].m.nu))
+    acts = acts.astype(np.float32)
+    acc = torch.zeros(6, dtype=torch.float64)
+
+    def step(k):
+        for e in envs:
+            r, term, trunc = e.step(acts[k])
+            acc[0] += 1
+            acc[2] += r
+            acc[3] += term
+            acc[4] += trunc
+    for k in range(args.warmup):
+        step(k)
+    acc.zero_()
+    elapsed = timed_region(lambda k: step(args.warmup + k), args.steps, lambda: None, dist)
+    acc, elapsed, value = whole_job_value(acc, elapsed)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 3), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "cpu harness: oracle soccer env, gloo (tests only, not a measurement)",
+            "config": {"workload": "harness", "envs_per_gpu": n, "global_batch": n * world,
+                       "parallelism": f"dp{world} (env shards)", "env_steps_total": int(acc[0].item())}}))
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without an outer torch.distributed.run, bench.py starts them itself")
+    ap.add_argument("--harness", default="gpu", choices=["gpu", "cpu"], help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default 4096; 8192 for bipedal)")
@@ -601,6 +665,21 @@ def main():
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
                                                           "construction"])
     args = ap.parse_args()
+    from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # no outer launcher: one child process per GPU, started before any GPU call
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = world_from_env()
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
+    if args.harness == "cpu":
+        dist = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+        args.envs = args.envs if args.envs > 0 else 2
+        return cpu_harness(args, world, rank, dist)
     if args.task not in ("soccer", "bipedal", "parkour"):
         args.mono = True  # one fused wave-per-env launch per step
     if args.precision is None:
@@ -608,8 +687,6 @@ def main():
     if args.envs <= 0:
         args.envs = {"bipedal": 8192, "mixed": 1024, "assembly": 1024, "construction": 1024}.get(args.task, 4096)
 
-    from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
-    world, rank, local = world_from_env()
     dist = None
     if world > 1:
         import torch.distributed as dist

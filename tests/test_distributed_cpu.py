@@ -53,6 +53,36 @@ def test_single_process_noop():
     assert m.tolist() == [1.0] * 6 and t == 3.5
 
 
+def test_bench_gpus2_spawns_its_own_ranks():
+    """`bench.py --gpus 2` with no outer launcher starts two rank processes itself (the CPU
+    harness: gloo + the oracle soccer env in place of RCCL + the GPU step) and rank 0 prints one
+    JSON line covering both shards."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--harness", "cpu",
+                        "--envs", "2", "--steps", "3", "--warmup", "1"], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2 * 2
+    assert out["config"]["env_steps_total"] == 2 * 2 * 3 and out["value"] > 0
+
+
+def test_bench_gpus_must_match_world():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--harness", "cpu"],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
 def _bench_worker(rank, world, port, q):
     """One rank of bench.py's harness (timed_region + whole_job_value, the code every bench line
     runs) over its env shard of the oracle soccer env, gloo standing in for RCCL."""
