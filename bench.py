@@ -203,118 +203,50 @@ class OracleSoccerEnv:
         return float(reward), bool(term), bool(trunc)
 
 
-def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
-    """Oracle port on one host core: mjref (C, fp64) physics + numpy env logic."""
-    from mujoco_gymnasium_environments_amd.envs.soccer import soccer_model
-    rng = np.random.default_rng(seed)
-    acts = rng.uniform(-150, 150, (64, soccer_model().nu)).astype(np.float32)
-    total = 0
+def cpu_baseline_task(task: str, n_envs: int, n_steps: int, seed: int = 0) -> dict:
+    """Oracle port on one host core (oracle/envs.py: mjref C fp64 physics + the task's numpy
+    logic), n_envs envs one after another, n_steps env steps each with autoreset, at the bench's
+    action distribution. Besides the rate it reports the oracle's own termination and bad-state
+    (MuJoCo's auto-reset) rates at these actions, to read next to the device line's."""
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.envs import ORACLES, task_setup
+    packed, tb, draws_fn, acts_fn = task_setup(task)
+    acts = acts_fn(np.random.default_rng(seed), 64)
+    total = terms = bad = 0
     t0 = time.perf_counter()
     for e in range(n_envs):
-        env = OracleSoccerEnv(e, seed)
+        rng = np_random(seed + e)[0]
+        env = ORACLES[task](packed, tb)
+        env.reset(draws_fn(rng))
         for k in range(n_steps):
-            env.step(acts[k % 64])
+            _, _, te, tr = env.step(acts[k % 64])
             total += 1
+            terms += te
+            if te or tr:
+                env.reset(draws_fn(rng))
+        bad += env.bad_states
     dt = time.perf_counter() - t0
+    what = {"soccer": "humanoid_soccer, U(-150,150) actions",
+            "parkour": "quadruped_parkour (10 substeps each), U(-lim, lim) actions",
+            "bipedal": "bipedal_rescue (RK4), U(-100,100) actions"}[task]
     return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of humanoid_soccer, U(-150,150) actions, "
-                      f"oracle/mjref.c fp64 physics + oracle/soccer_logic.py; CPU MuJoCo unavailable (not installed)",
-            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+            "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of {what}, oracle/mjref.c fp64 physics + "
+                      f"oracle/{task}_logic.py; CPU MuJoCo unavailable (not installed)",
+            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine(),
+            "oracle_termination_rate": round(terms / max(total, 1), 5),
+            "oracle_bad_state_rate": round(bad / max(total, 1), 5)}
+
+
+def cpu_baseline(n_envs: int, n_steps: int, seed: int = 0) -> dict:
+    return cpu_baseline_task("soccer", n_envs, n_steps, seed)
 
 
 def cpu_baseline_parkour(n_envs: int, n_steps: int, seed: int = 0) -> dict:
-    """Oracle port on one host core: mjref (C, fp64) physics x 10 substeps + numpy env logic."""
-    from mujoco_gymnasium_environments_amd import cabi
-    from mujoco_gymnasium_environments_amd.envs.parkour import action_limits, parkour_model
-    from mujoco_gymnasium_environments_amd.seeding import np_random
-    from oracle.mjref import RefSim
-    from oracle.parkour_logic import ParkourLogic, ParkourTables
-    m = parkour_model()
-    pk = cabi.pack_model(m)
-    L = ParkourLogic(ParkourTables(m))
-    rng = np.random.default_rng(seed)
-    acts = (rng.uniform(-1, 1, (64, 16)) * action_limits()).astype(np.float32)
-    total = 0
-    t0 = time.perf_counter()
-    for e in range(n_envs):
-        sim = RefSim(pk)
-        er = np_random(seed + e)[0]
-        s = {}
-
-        def view():
-            c = sim.contacts()
-            s.update(qpos=sim.qpos, qvel=sim.qvel, ctrl=sim.ctrl, xpos=sim.xpos.reshape(-1, 3), con_geom=c["geom"],
-                     ncon=int(sim.ncon[0]))
-
-        def reset():
-            sim.reset()
-            view()
-            L.apply_reset(s, L.t.reset_draws(er))
-            sim.step(10)
-            view()
-        reset()
-        for k in range(n_steps):
-            a = L.pre(s, acts[k % 64])
-            sim.step(10)
-            view()
-            _, _, term, trunc = L.post(s, a)
-            total += 1
-            if term or trunc:
-                reset()
-    dt = time.perf_counter() - t0
-    return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_envs} envs x {n_steps} steps (10 substeps each, autoreset) of quadruped_parkour, "
-                      f"U(-lim, lim) actions, oracle/mjref.c fp64 physics + oracle/parkour_logic.py; CPU MuJoCo "
-                      f"unavailable (not installed)",
-            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+    return cpu_baseline_task("parkour", n_envs, n_steps, seed)
 
 
 def cpu_baseline_bipedal(n_envs: int, n_steps: int, seed: int = 0) -> dict:
-    """Oracle port on one host core: mjref (C, fp64) RK4 physics + numpy env logic."""
-    from mujoco_gymnasium_environments_amd import cabi
-    from mujoco_gymnasium_environments_amd.envs.bipedal import bipedal_model
-    from mujoco_gymnasium_environments_amd.seeding import np_random
-    from oracle.bipedal_logic import BipedalLogic, BipedalTables
-    from oracle.mjref import RefSim
-    m = bipedal_model()
-    pk = cabi.pack_model(m)
-    L = BipedalLogic(BipedalTables(m))
-    rng = np.random.default_rng(seed)
-    acts = rng.uniform(-100, 100, (64, 26)).astype(np.float32)
-    total = 0
-    t0 = time.perf_counter()
-    for e in range(n_envs):
-        sim = RefSim(pk)
-        er = np_random(seed + e)[0]
-        s = dict(prev_rescued=-1, prev_carried=-1, prev_sz=float("nan"), fall_timer=-1)
-
-        def view():
-            s.update(qpos=sim.qpos, qvel=sim.qvel, ctrl=sim.ctrl, xpos=sim.xpos.reshape(-1, 3),
-                     xquat=sim.xquat.reshape(-1, 4), con_dist=sim.contacts()["dist"])
-
-        def reset():
-            sim.reset()
-            view()
-            L.apply_reset(s, L.t.reset_draws(er))
-            sim.step(10)
-            view()
-            L.after_reset(s)
-            L.obs(s)
-        reset()
-        for k in range(n_steps):
-            a = L.pre(s, acts[k % 64])
-            sim.step()
-            view()
-            _, _, term, trunc = L.post(s, a)
-            total += 1
-            if term or trunc:
-                reset()
-    dt = time.perf_counter() - t0
-    return {"value": total / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_envs} envs x {n_steps} steps (autoreset) of bipedal_rescue, U(-100,100) actions, "
-                      f"oracle/mjref.c fp64 RK4 physics + oracle/bipedal_logic.py; CPU MuJoCo unavailable "
-                      f"(not installed)",
-            "seconds": round(dt, 2), "host_cpu": platform.processor() or platform.machine()}
+    return cpu_baseline_task("bipedal", n_envs, n_steps, seed)
 
 
 def cpu_baseline_assembly(n_envs: int, n_steps: int, seed: int = 0) -> dict:
@@ -372,6 +304,13 @@ if os.environ.get("MGX_MIX_GROUPS"):
     MIXED_GROUPS = [g.split(",") for g in os.environ["MGX_MIX_GROUPS"].split(";")]
 
 
+def mixed_side_streams(n_tasks: int, mix_streams: int) -> None:
+    """The grouped layout runs without the staged tasks' side streams (MGX_SIDE_STREAM=0, a hook
+    libmgx reads when a model is created: call this before the envs are built)."""
+    if mix_streams < n_tasks:
+        os.environ["MGX_SIDE_STREAM"] = "0"
+
+
 def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
     """The mixed run's HIP streams per task (tests/test_gpu_mixed.py steps the same layout).
 
@@ -379,12 +318,12 @@ def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
     task (7, plus the staged tasks' side streams) unrelated tasks share queues and wait on each
     other's kernels. Four streams instead: construction (with soccer) and assembly, the long Newton
     steps, each on a stream of their own, the other PGS tasks in two pairs; no side streams
-    (MGX_SIDE_STREAM=0). Construction's stream runs at high priority (mix_priority 1, measured
-    73.2k -> 75.5k env-steps/s in round 4; in round 5 group 0 alone is still best: 122.7k against
-    119.4k with assembly's group, 118.9k with both). mix_streams 7: one stream per task (67.3k)."""
+    (MGX_SIDE_STREAM=0, mixed_side_streams). Construction's stream runs at high priority
+    (mix_priority 1, measured 73.2k -> 75.5k env-steps/s in round 4; in round 5 group 0 alone is
+    still best: 122.7k against 119.4k with assembly's group, 118.9k with both). mix_streams 7: one
+    stream per task (67.3k)."""
     if mix_streams >= len(tasks):
         return {k: torch.cuda.Stream(device=dev) for k in tasks}
-    os.environ["MGX_SIDE_STREAM"] = "0"
     # (dancing with parkour and martial arts: 75.5 / 76.7k against 74.9 / 75.0k with dancing
     # beside bipedal and soccer, two A/B pairs on one box)
     # MGX_MIX_PRIO_GROUPS (A/B hook): which groups run at high priority; 0 / 0,1 / 1 measured
@@ -413,6 +352,7 @@ def bench_mixed(args, dev, world, rank, dist):
     # assembly action_space: [-2, 2]^7 joint commands, [0, 100] opening, [0, 50] force (:150-151)
     alo = torch.tensor([-2.0] * 7 + [0.0, 0.0], device=dev)
     alim = torch.tensor([4.0] * 7 + [100.0, 50.0], device=dev)
+    mixed_side_streams(7, args.mix_streams)
     tasks = {
         "humanoid_soccer": (SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=11, env_offset=off,
                                             banks=args.banks), lambda: torch.rand(N, 33, device=dev, generator=g) * 300 - 150,
@@ -461,18 +401,24 @@ def bench_mixed(args, dev, world, rank, dist):
     torch.cuda.synchronize(dev)
     for env, _, _ in tasks.values():
         env.rollout.zero_()
+        env.batch.overflow.zero_()
+    warn0 = {k: int(env.batch.warning.sum().item()) for k, (env, _, _) in tasks.items()}
     evs = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in tasks}
            for _ in range(args.steps)]
     elapsed = timed_region(lambda i: one_step(i, evs[i]), args.steps, lambda: torch.cuda.synchronize(dev), dist)
     per = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in tasks}
     acc = torch.zeros(6, dtype=torch.float64, device=dev)
-    for env, _, _ in tasks.values():
+    # per task, over the timed region: MuJoCo's bad-state auto-resets and the env steps whose
+    # contacts / rows exceeded the task's capacity (0 when every row MuJoCo keeps was kept)
+    bad = {k: int(env.batch.warning.sum().item()) - warn0[k] for k, (env, _, _) in tasks.items()}
+    ovf = {k: int(env.batch.overflow.sum().item()) for k, (env, _, _) in tasks.items()}
+    for k, (env, _, _) in tasks.items():
         ro = env.rollout.double().sum(0)
         acc[0] += ro[3]
         acc[2] += ro[0] if torch.isfinite(ro[0]) else 0.0
         acc[3] += ro[1]
         acc[4] += ro[2]
-        acc[5] += float(env.batch.warning.sum().item())
+        acc[5] += bad[k]
     acc, elapsed, _ = whole_job_value(acc, elapsed)
     total = acc[0].item()
     if rank == 0:
@@ -495,7 +441,8 @@ def bench_mixed(args, dev, world, rank, dist):
                        "autoreset": "same-step", "task_launch_ms": {k: round(v, 4) for k, v in per.items()},
                        "task_dtype": {k: ("f64" if k in ("robotic_arm_assembly", "humanoid_construction")
                                           else args.precision) for k in tasks},
-                       "bad_state_resets": int(acc[5].item())},
+                       "bad_state_resets": int(acc[5].item()), "bad_state_resets_per_task": bad,
+                       "capacity_overflow_steps": sum(ovf.values()), "capacity_overflow_steps_per_task": ovf},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": _pmc_traffic(PMC_PROFILE_MIXED, N, args.precision, "mixed"),
@@ -746,6 +693,7 @@ def main():
         e.rollout.zero_()
         e.batch.overflow.zero_()
     ep0 = sum(int(e.episode.sum().item()) for e in shards)
+    warn0 = sum(int(e.batch.warning.sum().item()) for e in shards)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def one_step(k):
@@ -758,7 +706,7 @@ def main():
     acc[0] = ro[3]
     acc[1] = float(sum(int(e.episode.sum().item()) for e in shards) - ep0)
     acc[2], acc[3], acc[4] = ro[0], ro[1], ro[2]
-    acc[5] = float(sum(float(e.batch.warning.sum().item()) for e in shards))
+    acc[5] = float(sum(int(e.batch.warning.sum().item()) for e in shards) - warn0)  # over the timed region
     overflow_steps = sum(int(e.batch.overflow.sum().item()) for e in shards)
     acc, elapsed, value = whole_job_value(acc, elapsed)  # end-of-rollout metric all-reduce (RCCL), max time
     total_steps = acc[0].item()
@@ -775,6 +723,8 @@ def main():
                        "global_batch": N * world, "parallelism": f"dp{world} (env shards)", "autoreset": "same-step",
                        "integrator": "RK4", "step_kernels": bmode, "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "termination_rate": round(acc[3].item() / total_steps, 5),
+                       "bad_state_rate": round(acc[5].item() / total_steps, 5),
                        "capacity_overflow_steps": overflow_steps,
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -851,6 +801,9 @@ def main():
                        "substeps_per_step": 10, "step_kernels": "mono" if args.mono else "staged",
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "termination_rate": round(acc[3].item() / total_steps, 5),
+                       "bad_state_rate": round(acc[5].item() / total_steps, 5),
+                       "capacity": "96 contacts / 384 rows", "capacity_overflow_steps": overflow_steps,
                        "mean_reward": _finite(acc[2].item() / total_steps)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -881,6 +834,8 @@ def main():
                        "stream_shards": args.streams,
                        "episodes_started": int(acc[1].item()),
                        "terminated_total": int(acc[3].item()), "bad_state_resets": int(acc[5].item()),
+                       "termination_rate": round(acc[3].item() / total_steps, 5),
+                       "bad_state_rate": round(acc[5].item() / total_steps, 5),
                        "capacity_overflow_steps": overflow_steps,
                        "capacity": "64 contacts / 192 rows" if (args.reduced_capacity or args.mono) else "96 contacts / 384 rows",
                        "mean_reward": _finite(acc[2].item() / total_steps)},

@@ -45,6 +45,8 @@ _PTR = {"i": P_I32, "u": P_U32, "d": P_F64}
 _NP = {"i": np.int32, "u": np.uint32, "d": np.float64}
 
 
+MGX_ABI_VERSION = 6  # include/mgx.h: the struct layouts below
+MGX_E_ARG, MGX_E_CAPACITY, MGX_E_HIP, MGX_E_UNSUPPORTED = -1, -2, -3, -4  # include/mgx.h error codes
 MGX_KEEP_CVEL = 1  # mgx_model_desc.layout_flags (include/mgx.h)
 MGX_ROWS_IN_SCRATCH = 2  # layout_flags: constraint rows in per-env global scratch (include/mgx.h)
 
@@ -104,7 +106,8 @@ class MgxParkourEnv(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ["last_position", "max_progress", "episode_reward", "er_kind", "reached", "fall_count", "stuck",
                  "step", "episode", "rollout"]] + \
-               [("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32), ("pad0", C.c_int32)]
+               [("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32),
+                ("action_f64", C.c_int32)]
 
 
 class MgxParkourLogicIO(C.Structure):
@@ -121,7 +124,8 @@ class MgxMartialIds(C.Structure):
 
 
 class MgxMartialEnv(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["scal", "ints", "episode", "rollout"]]
+    _fields_ = [(n, C.c_void_p) for n in ["scal", "ints", "episode", "rollout"]] + \
+               [("action_f64", C.c_int32), ("pad0", C.c_int32)]
 
 
 class MgxMartialLogicIO(C.Structure):
@@ -143,7 +147,8 @@ class MgxAssemblyIds(C.Structure):
 
 
 class MgxAssemblyEnv(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["ints", "cumulative", "episode", "rollout", "reset_qpos"]]
+    _fields_ = [(n, C.c_void_p) for n in ["ints", "cumulative", "episode", "rollout", "reset_qpos"]] + \
+               [("action_f64", C.c_int32), ("pad0", C.c_int32)]
 
 
 class MgxAssemblyLogicIO(C.Structure):
@@ -165,7 +170,8 @@ class MgxBipedalEnv(C.Structure):
                 ["step", "energy", "energy_used", "rescued", "carried", "carrying", "closest", "prev_rescued",
                  "prev_carried", "prev_sz", "fall_timer", "victims_rescued", "distance", "ttfr", "falls", "collisions",
                  "prev_robot_pos", "episode", "rollout"]] + \
-               [("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32)]
+               [("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64), ("banks", C.c_int32),
+                ("action_f64", C.c_int32), ("energy_kind", C.c_void_p)]
 
 
 class MgxBipedalLogicIO(C.Structure):
@@ -183,7 +189,8 @@ class MgxDancingIds(C.Structure):
 
 class MgxDancingEnv(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
-                ["scal", "ints", "hist", "moves", "durations", "prev_jvel", "episode", "rollout"]]
+                ["scal", "ints", "hist", "moves", "durations", "prev_jvel", "episode", "rollout"]] + \
+               [("action_f64", C.c_int32), ("pad0", C.c_int32)]
 
 
 class MgxDancingLogicIO(C.Structure):
@@ -199,7 +206,8 @@ class MgxConstructionIds(C.Structure):
 
 
 class MgxConstructionEnv(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["scal", "ints", "total_reward", "episode", "rollout"]]
+    _fields_ = [(n, C.c_void_p) for n in ["scal", "ints", "total_reward", "episode", "rollout"]] + \
+               [("action_f64", C.c_int32), ("pad0", C.c_int32), ("total_kind", C.c_void_p)]
 
 
 class MgxConstructionLogicIO(C.Structure):

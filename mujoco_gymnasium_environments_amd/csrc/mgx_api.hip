@@ -341,7 +341,8 @@ Layout make_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int ma
 //          phase D (row blocks): cacc over the geom poses.
 // fp64 soccer, default capacity (64 contacts, 192 rows): 31.7 -> 19.7 KB per row-builder wave,
 // eight waves per CU instead of five (the VGPR limit of the row builder is also eight).
-Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active) {
+Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon, int max_nefc, int max_active,
+                          int gcon) {
   Layout L{};
   int p = 0;
   const int al = 16 / real_bytes;
@@ -378,8 +379,8 @@ Layout make_staged_layout(const mgx_model_desc* d, int real_bytes, int max_ncon,
   const int nlist = std::max(max_active, ecap);
   L.geom_xpos = R; L.geom_xmat = L.geom_xpos + a(3 * ng);
   L.con_frame = L.geom_xmat + a(9 * ng);
-  // the contact points live in the pipe (Pipe.o_cpos) unless MGX_GCON=0 (A/B: in phase C's LDS)
-  static const int gcon = getenv("MGX_GCON") ? atoi(getenv("MGX_GCON")) : 1;
+  // the contact points live in the pipe (Pipe.o_cpos) unless gcon = 0 (MGX_GCON=0, A/B: in phase
+  // C's LDS)
   L.gcon = gcon;
   L.con_pos = gcon ? 0 : L.con_frame + a(3 * max_ncon);
   L.act_union = L.con_frame + a(3 * max_ncon) + (gcon ? 0 : a(3 * max_ncon));
@@ -546,7 +547,7 @@ static int pgs_arena_bytes(int precision) {
 // ring turns of blocks plus the look-ahead, 16-byte rounded B) for the model's largest slot, or 0
 // when that exceeds 160 KiB or MGX_PGS_WIDE_LDS=0 (B from global memory, the A/B alternative)
 static int wide_arena_bytes(const mgx_model* m) {
-  static const int wide_lds = getenv("MGX_PGS_WIDE_LDS") ? atoi(getenv("MGX_PGS_WIDE_LDS")) : 1;
+  const int wide_lds = m->hooks.pgs_wide_lds;
   const int rb = m->precision == MGX_F32 ? 4 : 8;
   const int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
   const int maxE = m->Ls.max_nefc;
@@ -567,15 +568,15 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   p.base = (char*)ws;
   p.N = n_env; p.R = banks; p.S = n_env * (1 + banks);
   p.maxE = m->Ls.max_nefc; p.nv = nv; p.dpl = (nv + 7) / 8;  // solver: support entries per lane
-  // test hook: MGX_PGS_LDS_ROWS lowers the main launch's LDS rows (read per call), so ordinary
-  // states exercise the wide-LDS launch (tests/test_gpu_capacity.py)
-  const char* cap_env = getenv("MGX_PGS_LDS_ROWS");
-  int capE = cap_env ? (atoi(cap_env) + 3) / 4 * 4 : MGX_PGS_LDS_ROWS;
+  // test hook: MGX_PGS_LDS_ROWS (Hooks.pgs_lds_rows, read at model creation) lowers the main
+  // launch's LDS rows, so ordinary states exercise the wide-LDS launch (tests/test_gpu_capacity.py)
+  const Hooks& H = m->hooks;
+  const bool cap_env = H.pgs_lds_rows > 0;
+  int capE = cap_env ? (H.pgs_lds_rows + 3) / 4 * 4 : MGX_PGS_LDS_ROWS;
   if (capE < 4 || capE > p.maxE) capE = MGX_PGS_LDS_ROWS;
   if (rk) {
     // the RK4 pipeline's rows (bipedal: ~150 per forward, up to 512): MGX_RK_LDS_ROWS, default 256
-    const char* rk_env = getenv("MGX_RK_LDS_ROWS");
-    capE = rk_env ? (atoi(rk_env) + 3) / 4 * 4 : 256;
+    capE = H.rk_lds_rows > 0 ? (H.rk_lds_rows + 3) / 4 * 4 : 256;
     if (capE < 4) capE = 256;
   }
   p.capE = p.maxE < capE ? p.maxE : capE;
@@ -586,10 +587,9 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   // six waves per CU, 1.534M for that launch held to four; reduced capacity 1.647M).
   // MGX_PGS_SINGLE=1 selects the single main launch (A/B); the MGX_PGS_LDS_ROWS test hook sets the
   // main launch's rows directly.
-  static const int single = getenv("MGX_PGS_SINGLE") ? atoi(getenv("MGX_PGS_SINGLE")) : 0;
   p.sqg = 0;
-  if (!rk && !cap_env && !pgs_lds_b() && p.maxE > MGX_PGS_LDS_ROWS) {
-    if (single) {
+  if (!rk && !cap_env && !H.pgs_lds_b && p.maxE > MGX_PGS_LDS_ROWS) {
+    if (H.pgs_single) {
       p.capE = p.maxE;
       p.sqg = 1;
     } else {
@@ -604,11 +604,9 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   // turns of blocks plus the look-ahead, 16-byte rounded B.
   p.warena = !rk && p.maxE > p.capE ? wide_arena_bytes(m) : 0;
   // LDS arena of one main-launch solver wave (scalars + block table + B of its slots); the
-  // test / tuning hook MGX_PGS_ARENA overrides it (read per call; a small arena sends waves to
-  // the global-B launch)
-  const char* ar_env = getenv("MGX_PGS_ARENA");
+  // test / tuning hook MGX_PGS_ARENA overrides it (a small arena sends waves to the global-B launch)
   p.arena = pgs_arena_bytes(m->precision);
-  if (ar_env && atoi(ar_env) > 0 && atoi(ar_env) <= 96 * 1024) p.arena = atoi(ar_env);
+  if (H.pgs_arena > 0 && H.pgs_arena <= 96 * 1024) p.arena = H.pgs_arena;
   p.carry_stride = ((m->Ls.carry_reals + 63) & ~63) + 5 * 64;
   p.carryi_stride = m->Ls.carry_ints + 8;
   p.bcap = 32 + (p.maxE / 4) * (8 + 32 * ((nv + 7) / 8));
@@ -625,7 +623,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   // per-call hook changes those), so the workspace layout never depends on MGX_PGS_LDS_ROWS
   // heavy slots in the main launch (hmain, the full-capacity soccer default): when the SQG layout of
   // maxE rows fits the LDS of a capE-row wave. The MGX_PGS_LDS_ROWS test hook keeps the wide launch.
-  p.hmain = !rk && !cap_env && !p.sqg && !pgs_lds_b() && p.capE < p.maxE &&
+  p.hmain = !rk && !cap_env && !p.sqg && !H.pgs_lds_b && p.capE < p.maxE &&
             staged_pgs_lds_bytes(m, p.maxE, pgs_lanes(), 1, mgx_twl(false)) <=
                 staged_pgs_lds_bytes(m, p.capE, pgs_lanes(), 0, mgx_twl(false));
   if (p.hmain) p.warena = 0;
@@ -677,12 +675,28 @@ static int pgs_lds_bytes(const mgx_model* m, int rows, int sqg = 0) {
   return staged_pgs_lds_bytes(m, rows, pgs_lanes(), sqg, mgx_twl(false));
 }
 
-// MGX_SIDE_STREAM=0 (read per call) runs the wide solver launch after the main one on the caller's
-// stream: with more streams than hardware queues (several tasks on one GPU, each on its own stream)
-// a side stream can queue behind another task's long kernels.
-int mgx::side_streams() {
-  const char* v = getenv("MGX_SIDE_STREAM");
-  return v ? atoi(v) != 0 : 1;
+// Hooks (mgx_internal.h): the MGX_* A/B and test variables, read once per model
+mgx::Hooks mgx::read_hooks() {
+  Hooks h;
+  auto get = [](const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+  };
+  h.pgs_lds_rows = get("MGX_PGS_LDS_ROWS", 0);
+  h.rk_lds_rows = get("MGX_RK_LDS_ROWS", 0);
+  h.pgs_single = get("MGX_PGS_SINGLE", 0);
+  h.pgs_lds_b = get("MGX_PGS_LDS_B", MGX_PGS_LDS_B) != 0;
+  h.pgs_arena = get("MGX_PGS_ARENA", 0);
+  h.pgs_lds_pad = get("MGX_PGS_LDS_PAD", 0);
+  h.pgs_wide_lds = get("MGX_PGS_WIDE_LDS", 1);
+  h.pgs_spw = get("MGX_PGS_SPW", 0);
+  // MGX_SIDE_STREAM=0 runs the wide solver launch after the main one on the caller's stream: with
+  // more streams than hardware queues (several tasks on one GPU, each on its own stream) a side
+  // stream can queue behind another task's long kernels
+  h.side_stream = get("MGX_SIDE_STREAM", 1) != 0;
+  h.gcon = get("MGX_GCON", 1);
+  h.rows_lds = get("MGX_ROWS_LDS", 0);
+  return h;
 }
 
 // A side stream and two events per caller stream (created once, kept for the process): the wide
@@ -731,7 +745,10 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   size_t need = make_pipe(m, e->workspace, n_env, e->banks, &P);
   if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_soccer_workspace_bytes");
   int slots = n_env * (1 + banks);
-  launch_soccer_rows<T>(Ms, ids, *s, *e, action, n_env, mask, P, banks, slots, m->Ls.bytes, st);
+  const Hooks& H = m->hooks;
+  // occupancy probe: MGX_ROWS_LDS pads the row builder's LDS (fewer waves per CU; up to 64 KiB)
+  const int rlds = H.rows_lds > m->Ls.bytes && H.rows_lds <= 64 * 1024 ? H.rows_lds : m->Ls.bytes;
+  launch_soccer_rows<T>(Ms, ids, *s, *e, action, n_env, mask, P, banks, slots, rlds, st);
   T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
   // slots over the main launch's LDS rows (MuJoCo has no cap: the rows are kept, not dropped):
   // a small grid-stride global-B launch with maxE rows of LDS per slot, which exits at once when
@@ -740,23 +757,22 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   // main launch (MGX_PGS_LDS_B) it also takes the waves that did not fit their arena, so it
   // follows the main launch there.
   const int wgrid = 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, wlds = pgs_lds_bytes(m, P.maxE);
-  int mlds = pgs_lds_b() ? P.arena : pgs_lds_bytes(m, P.capE, P.sqg);
+  int mlds = H.pgs_lds_b ? P.arena : pgs_lds_bytes(m, P.capE, P.sqg);
   // occupancy probe: MGX_PGS_LDS_PAD pads the main solver launch's LDS (fewer waves per CU)
-  if (const char* pad = getenv("MGX_PGS_LDS_PAD"))
-    if (atoi(pad) > mlds && atoi(pad) <= 96 * 1024) mlds = atoi(pad);
-  if (!pgs_lds_b() && (P.maxE <= P.capE || P.hmain)) {
+  if (H.pgs_lds_pad > mlds && H.pgs_lds_pad <= 96 * 1024) mlds = H.pgs_lds_pad;
+  if (!H.pgs_lds_b && (P.maxE <= P.capE || P.hmain)) {
     // every slot fits the main launch (the default capacity): no wide launch at all
-    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
-  } else if (SideStream* side = (!pgs_lds_b() && side_streams()) ? side_stream(st) : nullptr) {
+    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0, H);
+  } else if (SideStream* side = (!H.pgs_lds_b && H.side_stream) ? side_stream(st) : nullptr) {
     HIPCHK(hipEventRecord(side->rows, st));
     HIPCHK(hipStreamWaitEvent(side->s, side->rows, 0));
-    launch_pgs<T>(P, wgrid, wlds, side->s, M.iterations, M.tolerance, scale, 1);
+    launch_pgs<T>(P, wgrid, wlds, side->s, M.iterations, M.tolerance, scale, 1, H);
     HIPCHK(hipEventRecord(side->big, side->s));
-    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
+    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0, H);
     HIPCHK(hipStreamWaitEvent(st, side->big, 0));
   } else {
-    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0);
-    launch_pgs<T>(P, wgrid, wlds, st, M.iterations, M.tolerance, scale, 1);
+    launch_pgs<T>(P, slots, mlds, st, M.iterations, M.tolerance, scale, 0, H);
+    launch_pgs<T>(P, wgrid, wlds, st, M.iterations, M.tolerance, scale, 1, H);
   }
   launch_soccer_finish<T>(Mf, ids, *s, *e, action, obs, reward, terminated, truncated, final_obs, autoreset, seed,
                           env_offset, n_env, mask, P, banks, m->Lf.bytes, st);
@@ -807,6 +823,8 @@ extern "C" {
 
 const char* mgx_last_error(void) { return g_err.c_str(); }
 
+int mgx_abi_version(void) { return MGX_ABI_VERSION; }
+
 int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_model** out) {
   if (!d || !out) return fail(MGX_E_ARG, "null argument");
   if (precision != MGX_F32 && precision != MGX_F64) return fail(MGX_E_ARG, "precision must be MGX_F32 or MGX_F64");
@@ -823,19 +841,28 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
     condim13 = condim13 && (c == 1 || c == 3);
   }
   mgx_model* m = new mgx_model();
+  m->hooks = read_hooks();
   m->precision = precision;
   m->device = device;
   m->npair = d->npair;
   m->wide = d->nv > MGX_MAX_NV;
-  const char* env_nefc = getenv("MGX_MAX_NEFC");
-  const char* env_ncon = getenv("MGX_MAX_NCON");
-  // capacities: the model's request (efc_capacity / con_capacity), else 192 rows / 64 contacts
-  int max_nefc = env_nefc ? atoi(env_nefc) : (d->efc_capacity > 0 ? d->efc_capacity : 192);
-  int max_ncon = env_ncon ? atoi(env_ncon) : (d->con_capacity > 0 ? d->con_capacity : 64);
-  if (max_nefc > 1024) max_nefc = 1024;
-  if (max_ncon > 512) max_ncon = 512;
+  // capacities: the model's request (efc_capacity / con_capacity), else 192 rows / 64 contacts.
+  // MGX_MAX_NEFC / MGX_MAX_NCON may raise them (read here, once); a value below the model's is
+  // refused: it would drop rows MuJoCo keeps. A smaller capacity is a property of the model itself
+  // (mgx_model_desc.efc_capacity / con_capacity), never of the environment.
+  int max_nefc = d->efc_capacity > 0 ? d->efc_capacity : 192;
+  int max_ncon = d->con_capacity > 0 ? d->con_capacity : 64;
+  if (const char* v = getenv("MGX_MAX_NEFC")) {
+    if (atoi(v) < max_nefc) { delete m; return fail(MGX_E_ARG, "MGX_MAX_NEFC below the model's row capacity"); }
+    max_nefc = atoi(v);
+  }
+  if (const char* v = getenv("MGX_MAX_NCON")) {
+    if (atoi(v) < max_ncon) { delete m; return fail(MGX_E_ARG, "MGX_MAX_NCON below the model's contact capacity"); }
+    max_ncon = atoi(v);
+  }
+  if (max_nefc > 1024 || max_ncon > 512) { delete m; return fail(MGX_E_CAPACITY, "capacity above 1024 rows / 512 contacts"); }
   max_nefc = (max_nefc + 3) & ~3;  // the staged solver sweeps rows in blocks of 4
-  if (max_nefc < 4 || max_ncon < 1) { delete m; return fail(MGX_E_ARG, "MGX_MAX_NEFC / MGX_MAX_NCON too small"); }
+  if (max_nefc < 4 || max_ncon < 1) { delete m; return fail(MGX_E_ARG, "row / contact capacity too small"); }
   int rb = precision == MGX_F32 ? 4 : 8;
   // broadphase survivor list: 128 for the small candidate sets (soccer 251, parkour 48 pairs),
   // up to 768 for large ones (bipedal 3185 pairs)
@@ -852,14 +879,19 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
                     max_nefc <= 1024 && max_ncon <= 192;  // three contact-metadata lane sets (RK_NCS)
   // ... and of a staged RK4 model (its checkAcc template, --mono) at most 512 rows, whose per-row
   // LDS arrays fit next to its working set with the rows in global scratch
-  const int mono_nefc = m->staged_ok && max_nefc > 192 ? 192 : (m->staged_rk_ok && max_nefc > 512 ? 512 : max_nefc);
-  const int mono_ncon = m->staged_ok && max_ncon > 64 ? 64 : max_ncon;
+  // A staged Euler model whose monolithic layout keeps its rows in global scratch (parkour) carries
+  // the full capacity there too: only its per-row scalars are in LDS.
+  const bool mono_lds_rows = !(d->layout_flags & MGX_ROWS_IN_SCRATCH);
+  const int mono_nefc = m->staged_ok && mono_lds_rows && max_nefc > 192 ? 192
+                        : (m->staged_rk_ok && max_nefc > 512 ? 512 : max_nefc);
+  const int mono_ncon = m->staged_ok && mono_lds_rows && max_ncon > 64 ? 64 : max_ncon;
   m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active);
   // rows that do not fit next to the rest of the per-env LDS working set go to global scratch
   if (m->L.bytes > 160 * 1024 || (d->layout_flags & MGX_ROWS_IN_SCRATCH))
     m->L = make_layout(d, rb, mono_ncon, mono_nefc, max_active, true);
   const bool any_staged = m->staged_ok || m->staged_rk_ok;
-  m->Ls = make_staged_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active);
+  m->Ls = make_staged_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active,
+                             m->hooks.gcon);
   m->Lf = finisher_layout(m->Ls, rb);
   int rc;
   if (precision == MGX_F32) {
@@ -955,6 +987,7 @@ int mgx_soccer_step(const mgx_model* m, const mgx_state* s, const mgx_soccer_env
                     double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
                     uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   if (!m->soccer_ok) return fail(MGX_E_ARG, "mgx_soccer_configure not called");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");
   int rc = check_state(s);

@@ -22,20 +22,32 @@ enum { AI_STEP = 0, AI_HELD = 1, AI_PHASE = 2, AI_PROG = 3, AI_STATUS = 4, AI_N 
 enum { AS_IN_BIN = 0, AS_HELD = 1, AS_ASSEMBLED = 2, AS_DROPPED = 3, AS_DAMAGED = 4 };
 enum { AP_IDLE = 0, AP_PICKUP = 1, AP_TRANSPORT = 2, AP_ALIGN = 3, AP_INSERT = 4 };
 
-// np.clip(action, low, high) in float32; ctrl[0:7] = a[0:7]; ctrl[7] = ctrl[8] = a[7] / 1000.0
-// (float32 / Python float stays float32 under NEP 50)
+// np.clip(action, low, high) in the action's dtype; ctrl[0:7] = a[0:7]; ctrl[7] = ctrl[8] = a[7] /
+// 1000.0 (float32 / Python float stays float32 under NEP 50; a float64 action divides in float64).
+// The reward does not read the action (:331-385).
 template <typename T>
-__device__ __forceinline__ void assembly_pre(const DevModel<T>& m, Env<T>& e, const mgx_assembly_ids& ids,
-                                             const float* action) {
+__device__ __forceinline__ void assembly_pre(const DevModel<T>& m, Env<T>& e, const mgx_assembly_ids& ids, ActRow act) {
   const int l = lane_id();
   if (l < 9) {
-    float a = action[l];
-    a = a < ids.action_low[l] ? ids.action_low[l] : (a > ids.action_high[l] ? ids.action_high[l] : a);
-    if (l < 7) e.ctrl[l] = (T)a;
-    if (l == 7) {
-      const float g = a / 1000.0f;
-      e.ctrl[7] = (T)g;
-      e.ctrl[8] = (T)g;
+    if (act.f64) {
+      double a = act.d()[l];
+      const double lo = (double)ids.action_low[l], hi = (double)ids.action_high[l];
+      a = a < lo ? lo : (a > hi ? hi : a);
+      if (l < 7) e.ctrl[l] = (T)a;
+      if (l == 7) {
+        const double g = a / 1000.0;
+        e.ctrl[7] = (T)g;
+        e.ctrl[8] = (T)g;
+      }
+    } else {
+      float a = act.f()[l];
+      a = a < ids.action_low[l] ? ids.action_low[l] : (a > ids.action_high[l] ? ids.action_high[l] : a);
+      if (l < 7) e.ctrl[l] = (T)a;
+      if (l == 7) {
+        const float g = a / 1000.0f;
+        e.ctrl[7] = (T)g;
+        e.ctrl[8] = (T)g;
+      }
     }
   }
   wsync();

@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(kTeamThreads) k_assembly(DevModel<T> m, mgx_as
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
   bool resetting = MODE == 1;
   if (MODE == 1) assembly_reset_prologue(m, e, ae, env);
-  else assembly_pre(m, e, ids, action + (size_t)env * 9);
+  else assembly_pre(m, e, ids, ActRow(action, ae.action_f64, env, 9));
   int warn = 0;
   for (;;) {
     const int nsteps = resetting ? ids.settle_steps : ids.substeps;  // assembly_env.py:186 / :228-229
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(64) k_assembly_logic(DevModel<T> m, mgx_assemb
     e.con_geom[2 * c + 1] = io.con_geom[((size_t)env * io.max_contacts + c) * 2 + 1];
   }
   wsync();
-  assembly_pre(m, e, ids, io.action + (size_t)env * 9);
+  assembly_pre(m, e, ids, ActRow(io.action, ae.action_f64, env, 9));
   assembly_post(m, e, ids, ae, env, io.obs, io.reward, io.terminated, io.truncated);
   for (int k = l; k < m.nu; k += 64) ((T*)io.ctrl)[(size_t)env * m.nu + k] = e.ctrl[k];
 }
@@ -182,6 +182,7 @@ int mgx_assembly_step(const mgx_model* m, const mgx_state* s, const mgx_assembly
                       double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
                       int n_env, const uint8_t* mask, void* stream) {
   if (!m || !s || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   const int rc = check_common(m, s, e);
   if (rc) return rc;
   if (n_env <= 0) return MGX_OK;

@@ -31,38 +31,62 @@ struct BipedalIds {
 
 __device__ __forceinline__ double norm2_np(double x, double y) { return sqrt(fma(y, y, x * x)); }
 
-// numpy float32 add.reduce over 26 contiguous values (pairwise: 8 accumulators, tree, tail)
-__device__ __forceinline__ float np_sum26_abs_clip(const float* a) {
+// numpy add.reduce over 26 contiguous values in the action's dtype (float32 or float64; pairwise:
+// 8 accumulators, tree, tail)
+template <typename A>
+__device__ __forceinline__ A np_sum26_abs_clip(const A* a) {
 #pragma clang fp contract(off)
-  float v[26];
+  A v[26];
   for (int j = 0; j < 26; j++) {
-    float x = a[j];
-    x = x < -100.0f ? -100.0f : (x > 100.0f ? 100.0f : x);
-    v[j] = fabsf(x);
+    A x = a[j];
+    x = x < (A)-100 ? (A)-100 : (x > (A)100 ? (A)100 : x);
+    v[j] = x < (A)0 ? -x : x;
   }
-  float r[8];
+  A r[8];
   for (int j = 0; j < 8; j++) r[j] = (v[j] + v[j + 8]) + v[j + 16];
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  A res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
   res += v[24];
   res += v[25];
   return res;
 }
 
-// action clip (float32) -> ctrl[:26], energy bookkeeping (rescue_env.py:419-429)
+// numpy type of current_energy / energy_used (mgx_bipedal_env.energy_kind)
+enum { EK_PY = 0, EK_F64 = 1, EK_F32 = 2 };
+
+// action clip -> ctrl[:26], energy bookkeeping (rescue_env.py:419-429) in numpy's arithmetic: the
+// cost np.sum(np.abs(a)) * 0.001 has the action's dtype; current_energy -= cost (and energy_used +=
+// cost) stays float32 while both are float32 (a Python float, after reset, becomes float32) and is
+// float64 from the first float64 operand on
 template <typename T>
-__device__ __forceinline__ void bipedal_pre(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, const float* action,
+__device__ __forceinline__ void bipedal_pre(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, ActRow act,
                                             mgx_bipedal_env be, int env) {
 #pragma clang fp contract(off)
   int l = lane_id();
   if (l < ids.n_act) {
-    float a = action[l];
-    a = a < -100.0f ? -100.0f : (a > 100.0f ? 100.0f : a);
-    e.ctrl[l] = (T)a;
+    if (act.f64) {
+      double a = act.d()[l];
+      a = a < -100.0 ? -100.0 : (a > 100.0 ? 100.0 : a);
+      e.ctrl[l] = (T)a;
+    } else {
+      float a = act.f()[l];
+      a = a < -100.0f ? -100.0f : (a > 100.0f ? 100.0f : a);
+      e.ctrl[l] = (T)a;
+    }
   }
   if (l == 0) {
-    float cost = np_sum26_abs_clip(action) * 0.001f;
-    be.energy[env] = be.energy[env] - cost;
-    be.energy_used[env] = be.energy_used[env] + cost;
+    int kind = be.energy_kind ? be.energy_kind[env] : EK_F32;
+    if (act.f64 || kind == EK_F64) {
+      const double cost = act.f64 ? np_sum26_abs_clip(act.d()) * 0.001 : (double)(np_sum26_abs_clip(act.f()) * 0.001f);
+      be.energy[env] = be.energy[env] - cost;
+      be.energy_used[env] = be.energy_used[env] + cost;
+      kind = EK_F64;
+    } else {
+      const float cost = np_sum26_abs_clip(act.f()) * 0.001f;
+      be.energy[env] = (double)((float)be.energy[env] - cost);
+      be.energy_used[env] = (double)((float)be.energy_used[env] + cost);
+      kind = EK_F32;
+    }
+    if (be.energy_kind) be.energy_kind[env] = (uint8_t)kind;
   }
   wsync();
 }
@@ -102,7 +126,7 @@ __device__ __forceinline__ void bipedal_interactions(const Env<T>& e, const Bipe
 // Observation: 102 float32 (rescue_env.py:545-600)
 template <typename T>
 __device__ __forceinline__ void bipedal_obs(const DevModel<T>& m, const Env<T>& e, const BipedalIds& ids, int step, int resc,
-                                            int car, float energy, float* obs) {
+                                            int car, double energy, bool energy64, float* obs) {
   int l = lane_id();
   const T* r = e.xpos + 3 * ids.torso;
   // slot 65: sum over the first min(ncon, 10) contacts of |dist|, sequential float64
@@ -124,8 +148,8 @@ __device__ __forceinline__ void bipedal_obs(const DevModel<T>& m, const Env<T>& 
     } else if (i < 92) {
       const double sz[3] = {20.0, 0.0, 0.0};
       v = sz[i - 89] - (double)r[i - 89];
-    } else if (i == 92) {
-      obs[i] = energy / 1000.0f;
+    } else if (i == 92) {  // current_energy / energy_limit in current_energy's numpy type
+      obs[i] = energy64 ? (float)(energy / 1000.0) : (float)energy / 1000.0f;
       continue;
     } else if (i == 93) v = 1.0 - ((double)step / (double)ids.max_episode_steps);
     else if (i == 94) v = (double)__popc(car);
@@ -150,7 +174,7 @@ __device__ __forceinline__ bool bipedal_upright(const Env<T>& e, const BipedalId
 // counter, interactions, obs, reward, termination, stats, prev position (rescue_env.py:435-467);
 // returns done
 template <typename T>
-__device__ __forceinline__ bool bipedal_post(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, const float* action,
+__device__ __forceinline__ bool bipedal_post(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, ActRow act,
                                              mgx_bipedal_env be, int env, float* obs, double* reward, uint8_t* terminated,
                                              uint8_t* truncated, uint8_t* upright_out = nullptr) {
 #pragma clang fp contract(off)
@@ -163,7 +187,8 @@ __device__ __forceinline__ bool bipedal_post(const DevModel<T>& m, Env<T>& e, co
   wsync();
   int resc = be.rescued[env], car = be.carried[env];
   bool upright = bipedal_upright(e, ids);
-  bipedal_obs(m, e, ids, st, resc, car, be.energy[env], obs + (size_t)env * 102);
+  const bool e64 = be.energy_kind && be.energy_kind[env] == EK_F64;
+  bipedal_obs(m, e, ids, st, resc, car, be.energy[env], e64, obs + (size_t)env * 102);
   int done = 0;
   if (l == 0) {
     const T* rp = e.xpos + 3 * ids.torso;
@@ -193,8 +218,8 @@ __device__ __forceinline__ bool bipedal_post(const DevModel<T>& m, Env<T>& e, co
     }
     if (upright) r += 50.0;
     else { r += -500.0; be.falls[env] += 1; }
-    float usage = np_sum26_abs_clip(action + (size_t)env * ids.n_act) * 0.001f;
-    if (usage < 0.5f) r += 10.0;
+    // energy_usage = np.sum(np.abs(action)) * 0.001 in the action's dtype (:650-652)
+    if (act.f64 ? np_sum26_abs_clip(act.d()) * 0.001 < 0.5 : np_sum26_abs_clip(act.f()) * 0.001f < 0.5f) r += 10.0;
     if (norm2_np(rx - -5.0, ry - -3.0) < 1.5) r += -200.0;
     if (norm2_np(rx - 8.0, ry - 6.0) < 1.2) r += -200.0;
     int nc = e.ncon < 20 ? e.ncon : 20;
@@ -214,7 +239,7 @@ __device__ __forceinline__ bool bipedal_post(const DevModel<T>& m, Env<T>& e, co
       } else {
         be.fall_timer[env] = 0;
       }
-      if (!term) term = be.energy[env] <= 0.0f || fabs(rx) > 25.0 || fabs(ry) > 25.0;
+      if (!term) term = be.energy[env] <= 0.0 || fabs(rx) > 25.0 || fabs(ry) > 25.0;
     }
     bool trunc = st >= ids.max_episode_steps;
     double* pp = be.prev_robot_pos + 3 * (size_t)env;
@@ -265,8 +290,9 @@ __device__ __forceinline__ void bipedal_reset_prologue(const DevModel<T>& m, Env
       e.qpos[ids.victim_y[i]] = e.qpos[ids.victim_y[i]] + d[3 + 2 * i];
     }
     be.step[env] = 0;
-    be.energy[env] = 1000.0f;
-    be.energy_used[env] = 0.0f;
+    be.energy[env] = 1000.0;  // Python floats again (energy_limit, 0.0)
+    be.energy_used[env] = 0.0;
+    if (be.energy_kind) be.energy_kind[env] = EK_PY;
     be.rescued[env] = 0;
     be.carried[env] = 0;
     be.carrying[env] = 0;
@@ -284,7 +310,7 @@ template <typename T>
 __device__ __forceinline__ void bipedal_reset_epilogue(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids,
                                                        mgx_bipedal_env be, int env, float* obs) {
   int l = lane_id();
-  bipedal_obs(m, e, ids, 0, 0, 0, 1000.0f, obs + (size_t)env * 102);
+  bipedal_obs(m, e, ids, 0, 0, 0, 1000.0, false, obs + (size_t)env * 102);
   if (l < 3) be.prev_robot_pos[3 * (size_t)env + l] = (double)e.xpos[3 * ids.torso + l];
   wsync();
 }

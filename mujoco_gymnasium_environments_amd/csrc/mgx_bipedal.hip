@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(64) k_bipedal(DevModel<T> m, BipedalIds ids, m
     }
     bipedal_reset_prologue(m, e, ids, dr, be, env);
   } else {
-    bipedal_pre(m, e, ids, action + (size_t)env * ids.n_act, be, env);
+    bipedal_pre(m, e, ids, ActRow(action, be.action_f64, env, ids.n_act), be, env);
   }
   int warn = 0;
   for (;;) {
@@ -61,7 +61,8 @@ __global__ void __launch_bounds__(64) k_bipedal(DevModel<T> m, BipedalIds ids, m
       if (l == 0 && be.episode) be.episode[env] += 1;
       break;
     }
-    const bool done = bipedal_post(m, e, ids, action, be, env, obs, reward, terminated, truncated);
+    const bool done =
+        bipedal_post(m, e, ids, ActRow(action, be.action_f64, env, ids.n_act), be, env, obs, reward, terminated, truncated);
     if (be.rollout && l == 0) {
       T* ro = (T*)be.rollout + 4 * (size_t)env;
       ro[0] += (T)reward[env];
@@ -105,8 +106,9 @@ __global__ void __launch_bounds__(64) k_bipedal_logic(DevModel<T> m, BipedalIds 
   e.ncon = nc;
   for (int c = l; c < nc; c += 64) e.con_dist[c] = ((const T*)io.con_dist)[(size_t)env * io.max_contacts + c];
   wsync();
-  bipedal_pre(m, e, ids, io.action + (size_t)env * ids.n_act, be, env);
-  bipedal_post(m, e, ids, io.action, be, env, io.obs, io.reward, io.terminated, io.truncated, io.upright);
+  const ActRow a(io.action, be.action_f64, env, ids.n_act);
+  bipedal_pre(m, e, ids, a, be, env);
+  bipedal_post(m, e, ids, a, be, env, io.obs, io.reward, io.terminated, io.truncated, io.upright);
   wsync();
   for (int k = l; k < m.nu; k += 64) ((T*)io.ctrl)[(size_t)env * m.nu + k] = e.ctrl[k];
 }
@@ -187,6 +189,7 @@ int mgx_bipedal_step(const mgx_model* m, const mgx_state* s, const mgx_bipedal_e
                      double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
                      uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   if (!m->bipedal_ok) return fail(MGX_E_ARG, "mgx_bipedal_configure not called");
   if (!bipedal_env_ok(e)) return fail(MGX_E_ARG, "null bipedal env buffer");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");

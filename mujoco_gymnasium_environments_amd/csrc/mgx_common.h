@@ -281,6 +281,22 @@ __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
   return x - v;
 }
 
+// ------------------------------------------------------------------ policy actions
+// One env's action row: float32, or float64 when the env struct's action_f64 is set. The
+// reference's np.clip(action, low, high) keeps a float64 policy's dtype (the bounds are float32
+// arrays or Python floats), so ctrl and every action term of the reward follow in float64; a
+// float32 action keeps numpy's float32 arithmetic.
+struct ActRow {
+  const void* p;
+  int f64;
+  __device__ ActRow(const void* base, int f64_, size_t row, int n)
+      : p(f64_ ? (const void*)((const double*)base + row * n) : (const void*)((const float*)base + row * n)),
+        f64(f64_) {}
+  __device__ const float* f() const { return static_cast<const float*>(p); }
+  __device__ const double* d() const { return static_cast<const double*>(p); }
+  __device__ double at(int i) const { return f64 ? d()[i] : (double)f()[i]; }
+};
+
 // ------------------------------------------------------------------ small math (MuJoCo forms)
 template <typename T> __device__ __forceinline__ T clampv(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
 template <typename T> __device__ __forceinline__ T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }

@@ -26,37 +26,48 @@ struct ConstructionIds {
   float action_limit;
 };
 
-// numpy float32 add.reduce of |a| over n contiguous values (pairwise: 8 accumulators over the
-// first 8*floor(n/8), tree (01)(23) / (45)(67), then the tail)
-__device__ __forceinline__ float np_sum_abs(const float* a, int n) {
+// numpy add.reduce of |clip(a, -lim, lim)| over n contiguous values in the action's dtype (float32
+// or float64; pairwise: 8 accumulators over the first 8*floor(n/8), tree (01)(23) / (45)(67), then
+// the tail)
+template <typename A>
+__device__ __forceinline__ A np_sum_abs(const A* a, int n, A lim) {
 #pragma clang fp contract(off)
+  auto v = [&](int u) {
+    A x = a[u];
+    x = x < -lim ? -lim : (x > lim ? lim : x);
+    return x < (A)0 ? -x : x;
+  };
   if (n < 8) {
-    float res = 0.0f;
-    for (int u = 0; u < n; u++) res += fabsf(a[u]);
+    A res = 0;
+    for (int u = 0; u < n; u++) res += v(u);
     return res;
   }
-  float r[8];
-  for (int k = 0; k < 8; k++) r[k] = fabsf(a[k]);
+  A r[8];
+  for (int k = 0; k < 8; k++) r[k] = v(k);
   int i = 8;
   for (; i + 8 <= n; i += 8)
-    for (int k = 0; k < 8; k++) r[k] += fabsf(a[i + k]);
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; i++) res += fabsf(a[i]);
+    for (int k = 0; k < 8; k++) r[k] += v(i + k);
+  A res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += v(i);
   return res;
 }
 
-// clip (float32, against the float32 action_space bounds) -> ctrl (:589-592); the clipped action
-// is kept in LDS (vec3 as floats) for the energy term
+// clip (against the float32 action_space bounds, in the action's dtype) -> ctrl (:589-592)
 template <typename T>
-__device__ __forceinline__ void construction_pre(const DevModel<T>& m, Env<T>& e, const ConstructionIds& ids,
-                                                 const float* action, float* clipped) {
+__device__ __forceinline__ void construction_pre(const DevModel<T>& m, Env<T>& e, const ConstructionIds& ids, ActRow act) {
   const int l = lane_id();
   if (l < ids.n_act) {
-    float a = action[l];
-    const float lim = ids.action_limit;
-    a = a < -lim ? -lim : (a > lim ? lim : a);
-    clipped[l] = a;
-    e.ctrl[l] = (T)a;
+    if (act.f64) {
+      double a = act.d()[l];
+      const double lim = (double)ids.action_limit;
+      a = a < -lim ? -lim : (a > lim ? lim : a);
+      e.ctrl[l] = (T)a;
+    } else {
+      float a = act.f()[l];
+      const float lim = ids.action_limit;
+      a = a < -lim ? -lim : (a > lim ? lim : a);
+      e.ctrl[l] = (T)a;
+    }
   }
   wsync();
 }
@@ -86,7 +97,7 @@ __device__ __forceinline__ void construction_obs(const DevModel<T>& m, const Env
 // terminated || truncated (uniform).
 template <typename T>
 __device__ __forceinline__ bool construction_post(const DevModel<T>& m, const Env<T>& e, const ConstructionIds& ids,
-                                                  const float* clipped, mgx_construction_env ce, int env, float* obs,
+                                                  ActRow act, mgx_construction_env ce, int env, float* obs,
                                                   double* reward, uint8_t* terminated, uint8_t* truncated) {
   const int l = lane_id();
   double* S = ce.scal + (size_t)env * CS_N;
@@ -112,12 +123,21 @@ __device__ __forceinline__ bool construction_post(const DevModel<T>& m, const En
     else r += prog * 100.0;
     r += 100.0 * 0.01;                       // hard_hat_on
     r -= (double)(I[CI_VIOL] * 100);
-    const float energy = -0.2f * np_sum_abs(clipped, ids.n_act);
-    float r32 = (float)r + energy;
     const double hz = (double)e.xpos[3 * ids.humanoid + 2];
-    if (hz > 1.0) r32 += 5.0f;               // stability_reward * 0.1
-    else r32 += -2000.0f;                    // fall_penalty
-    reward[env] = (double)r32;
+    double rv;
+    if (act.f64) {  // a float64 action: np.float64 energy term, the reward float64 from there on
+      r += -0.2 * np_sum_abs(act.d(), ids.n_act, (double)ids.action_limit);
+      if (hz > 1.0) r += 5.0;
+      else r += -2000.0;
+      rv = r;
+    } else {
+      const float energy = -0.2f * np_sum_abs(act.f(), ids.n_act, ids.action_limit);
+      float r32 = (float)r + energy;
+      if (hz > 1.0) r32 += 5.0f;               // stability_reward * 0.1
+      else r32 += -2000.0f;                    // fall_penalty
+      rv = (double)r32;
+    }
+    reward[env] = rv;
     // _check_terminated (:721-737)
     if (hz < 0.5) term = true;
     else if (prog >= 1.0) { I[CI_DONE] += 1; term = true; }
@@ -125,7 +145,17 @@ __device__ __forceinline__ bool construction_post(const DevModel<T>& m, const En
     trunc = step >= ids.max_episode_steps;
     terminated[env] = term;
     truncated[env] = trunc;
-    ce.total_reward[env] = ce.total_reward[env] + r32;
+    // episode_stats['total_reward'] += reward: float32 while both are float32 (0.0 after reset is a
+    // Python float), float64 from the first float64 reward on (total_kind, as bipedal's energy)
+    int kind = ce.total_kind ? ce.total_kind[env] : 2;
+    if (act.f64 || kind == 1) {
+      ce.total_reward[env] = ce.total_reward[env] + rv;
+      kind = 1;
+    } else {
+      ce.total_reward[env] = (double)((float)ce.total_reward[env] + (float)rv);
+      kind = 2;
+    }
+    if (ce.total_kind) ce.total_kind[env] = (uint8_t)kind;
   }
   wsync();
   construction_obs(m, e, S, I, obs + (size_t)env * MGX_CONSTRUCTION_OBS);
@@ -166,7 +196,8 @@ __device__ __forceinline__ void construction_reset_body(const DevModel<T>& m, WE
     I[CI_STEP] = 0; I[CI_BLOCKS] = 0; I[CI_VIOL] = 0; I[CI_DONE] = 0;
     S[CS_PROGRESS] = 0.0;
     S[CS_WIND] = (double)draws[1]; S[CS_RAIN] = (double)draws[2]; S[CS_TEMP] = (double)draws[3];
-    ce.total_reward[env] = 0.0f;
+    ce.total_reward[env] = 0.0;
+    if (ce.total_kind) ce.total_kind[env] = 0;
   }
   wsync();
   construction_obs(m, w.e, S, I, obs + (size_t)env * MGX_CONSTRUCTION_OBS);

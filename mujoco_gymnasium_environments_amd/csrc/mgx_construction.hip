@@ -49,7 +49,6 @@ __global__ void __launch_bounds__(MODE == 0 ? kTeamThreads : 64) k_construction(
   const int l = lane_id();
   T* qpos = (T*)s.qpos; T* qvel = (T*)s.qvel; T* qacc = (T*)s.qacc_warmstart; T* ctrl = (T*)s.ctrl;
   T* qfrc = (T*)s.qfrc_applied; T* xfrc = (T*)s.xfrc_applied; T* tm = (T*)s.time;
-  float* clipped = reinterpret_cast<float*>(e.vec3);
   if (MODE == 1) {
     const T* dr = draws ? draws + 4 * (size_t)env : nullptr;
     if (!draws) {
@@ -63,9 +62,10 @@ __global__ void __launch_bounds__(MODE == 0 ? kTeamThreads : 64) k_construction(
     return;
   }
   wload_state(m, w, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  construction_pre(m, e, ids, action + (size_t)env * ids.n_act, clipped);
+  const ActRow act(action, ce.action_f64, env, ids.n_act);
+  construction_pre(m, e, ids, act);
   const int warn = wmj_step(m, w);
-  const bool done = construction_post(m, e, ids, clipped, ce, env, obs, reward, terminated, truncated);
+  const bool done = construction_post(m, e, ids, act, ce, env, obs, reward, terminated, truncated);
   if (ce.rollout && l == 0) {
     double* ro = ce.rollout + 4 * (size_t)env;
     ro[0] += reward[env];
@@ -107,9 +107,9 @@ __global__ void __launch_bounds__(64) k_construction_logic(DevModel<T> m, Constr
   for (int k = l; k < m.nv; k += 64) e.qvel[k] = ((const T*)io.qvel)[(size_t)env * m.nv + k];
   for (int k = l; k < 3 * m.nbody; k += 64) e.xpos[k] = ((const T*)io.xpos)[(size_t)env * 3 * m.nbody + k];
   wsync();
-  float* clipped = reinterpret_cast<float*>(e.vec3);
-  construction_pre(m, e, ids, io.action + (size_t)env * ids.n_act, clipped);
-  construction_post(m, e, ids, clipped, ce, env, io.obs, io.reward, io.terminated, io.truncated);
+  const ActRow act(io.action, ce.action_f64, env, ids.n_act);
+  construction_pre(m, e, ids, act);
+  construction_post(m, e, ids, act, ce, env, io.obs, io.reward, io.terminated, io.truncated);
   for (int k = l; k < m.nu; k += 64) ((T*)io.ctrl)[(size_t)env * m.nu + k] = e.ctrl[k];
 }
 
@@ -313,6 +313,7 @@ int mgx_construction_step(const mgx_model* m, const mgx_state* s, const mgx_cons
                           float* obs, double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs,
                           int autoreset, uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   if (!m->construction_ok) return fail(MGX_E_ARG, "mgx_construction_configure not called");
   if (!construction_env_ok(e)) return fail(MGX_E_ARG, "null construction env buffer");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");

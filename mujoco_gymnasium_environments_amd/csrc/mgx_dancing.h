@@ -54,16 +54,22 @@ __device__ __forceinline__ R np_sum29(const R* v) {
   return res;
 }
 
-// action clip (float32) -> ctrl, rhythm, disco ball, spotlight (dancing_env.py:835-846)
+// action clip (in the action's dtype) -> ctrl, rhythm, disco ball, spotlight (dancing_env.py:835-846)
 template <typename T>
-__device__ __forceinline__ void dancing_pre(const DevModel<T>& m, Env<T>& e, const DancingIds& ids, const float* action,
+__device__ __forceinline__ void dancing_pre(const DevModel<T>& m, Env<T>& e, const DancingIds& ids, ActRow act,
                                             mgx_dancing_env de, int env) {
 #pragma clang fp contract(off)
   int l = lane_id();
   if (l < ids.n_act) {
-    float a = action[l];
-    a = a < -200.0f ? -200.0f : (a > 200.0f ? 200.0f : a);
-    e.ctrl[l] = (T)a;
+    if (act.f64) {
+      double a = act.d()[l];
+      a = a < -200.0 ? -200.0 : (a > 200.0 ? 200.0 : a);
+      e.ctrl[l] = (T)a;
+    } else {
+      float a = act.f()[l];
+      a = a < -200.0f ? -200.0f : (a > 200.0f ? 200.0f : a);
+      e.ctrl[l] = (T)a;
+    }
   }
   if (l == 0) {
     double* S = de.scal + (size_t)env * DS_N;
@@ -151,7 +157,7 @@ __device__ __forceinline__ bool dancing_upright(const Env<T>& e, const DancingId
 // counter, obs, reward, termination, stats, crowd, move transition, prev snapshots
 // (dancing_env.py:849-892); returns done
 template <typename T>
-__device__ __forceinline__ bool dancing_post(const DevModel<T>& m, Env<T>& e, const DancingIds& ids, const float* action,
+__device__ __forceinline__ bool dancing_post(const DevModel<T>& m, Env<T>& e, const DancingIds& ids, ActRow act,
                                              mgx_dancing_env de, int env, float* obs, double* reward, uint8_t* terminated,
                                              uint8_t* truncated) {
 #pragma clang fp contract(off)
@@ -202,14 +208,24 @@ __device__ __forceinline__ bool dancing_post(const DevModel<T>& m, Env<T>& e, co
       if (lo < hi) used += fabs((double)e.qpos[7 + i] - (lo + hi) / 2) / (hi - lo);
     }
     if (used > 5.0) r += 100.0 * 0.1;
-    float sq[29];
-    const float* a = action + (size_t)env * ids.n_act;
-    for (int j = 0; j < 29; j++) {
-      float x = a[j];
-      x = x < -200.0f ? -200.0f : (x > 200.0f ? 200.0f : x);
-      sq[j] = x * x;
+    // energy_penalty * np.sum(np.square(action)) in the action's dtype (:1186-1187)
+    if (act.f64) {
+      double sq[29];
+      for (int j = 0; j < 29; j++) {
+        double x = act.d()[j];
+        x = x < -200.0 ? -200.0 : (x > 200.0 ? 200.0 : x);
+        sq[j] = x * x;
+      }
+      r += -0.05 * np_sum29(sq);
+    } else {
+      float sq[29];
+      for (int j = 0; j < 29; j++) {
+        float x = act.f()[j];
+        x = x < -200.0f ? -200.0f : (x > 200.0f ? 200.0f : x);
+        sq[j] = x * x;
+      }
+      r += (double)(-0.05f * np_sum29(sq));
     }
-    r += (double)(-0.05f * np_sum29(sq));
     if (!up) { r += -500.0; combo = 1.0; }
     if (bp > 0.2 && bp < 0.8 && mm > 3.0) r += -50.0 * 0.1;
     if (r > 0) r *= combo;

@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, m
     }
     dancing_reset_prologue(m, e, dr, de, env);
   } else {
-    dancing_pre(m, e, ids, action + (size_t)env * ids.n_act, de, env);
+    dancing_pre(m, e, ids, ActRow(action, de.action_f64, env, ids.n_act), de, env);
   }
   int warn = 0;
   for (;;) {
@@ -61,7 +61,8 @@ __global__ void __launch_bounds__(64) k_dancing(DevModel<T> m, DancingIds ids, m
       if (l == 0 && de.episode) de.episode[env] += 1;
       break;
     }
-    const bool done = dancing_post(m, e, ids, action, de, env, obs, reward, terminated, truncated);
+    const bool done =
+        dancing_post(m, e, ids, ActRow(action, de.action_f64, env, ids.n_act), de, env, obs, reward, terminated, truncated);
     if (de.rollout && l == 0) {
       T* ro = (T*)de.rollout + 4 * (size_t)env;
       ro[0] += (T)reward[env];
@@ -111,8 +112,9 @@ __global__ void __launch_bounds__(64) k_dancing_logic(DevModel<T> m, DancingIds 
     e.con_geom[2 * c + 1] = io.con_geom[((size_t)env * io.max_contacts + c) * 2 + 1];
   }
   wsync();
-  dancing_pre(m, e, ids, io.action + (size_t)env * ids.n_act, de, env);
-  dancing_post(m, e, ids, io.action, de, env, io.obs, io.reward, io.terminated, io.truncated);
+  const ActRow a(io.action, de.action_f64, env, ids.n_act);
+  dancing_pre(m, e, ids, a, de, env);
+  dancing_post(m, e, ids, a, de, env, io.obs, io.reward, io.terminated, io.truncated);
   wsync();
   for (int k = l; k < m.nu; k += 64) ((T*)io.ctrl)[(size_t)env * m.nu + k] = e.ctrl[k];
 }
@@ -177,6 +179,7 @@ int mgx_dancing_step(const mgx_model* m, const mgx_state* s, const mgx_dancing_e
                      double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
                      uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   if (!m->dancing_ok) return fail(MGX_E_ARG, "mgx_dancing_configure not called");
   if (!dancing_env_ok(e)) return fail(MGX_E_ARG, "null dancing env buffer");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");

@@ -14,7 +14,30 @@
 #include "mgx_parkour.h"
 #include "mgx_staged.h"
 
+namespace mgx {
+// A/B and test hooks (MGX_* environment variables). Read once per model, in mgx_model_create, and
+// kept with the model, so a launch never depends on the environment at call time. None of them
+// changes a result: each selects another schedule of the same arithmetic (tests/test_gpu_capacity.py
+// checks the ones that move slots between launches bit for bit). MGX_PGS_LPS (solver lanes per
+// slot) is read once per process (pgs_lanes): the solver kernels' LDS limits are set from it.
+struct Hooks {
+  int pgs_lds_rows = 0;  // MGX_PGS_LDS_ROWS: the soccer main solver launch's LDS rows (0: model default)
+  int rk_lds_rows = 0;   // MGX_RK_LDS_ROWS: the RK4 main solver launch's LDS rows (0: 256)
+  int pgs_single = 0;    // MGX_PGS_SINGLE: one main launch over every slot, scalars from the pipe
+  int pgs_lds_b = 0;     // MGX_PGS_LDS_B: the main launch copies B into an LDS arena
+  int pgs_arena = 0;     // MGX_PGS_ARENA: that arena's bytes (0: MGX_PGS_ARENA_F32 / _F64)
+  int pgs_lds_pad = 0;   // MGX_PGS_LDS_PAD: pad the main solver launch's LDS (occupancy probe)
+  int pgs_wide_lds = 1;  // MGX_PGS_WIDE_LDS: the wide launch copies its slot's B into LDS
+  int pgs_spw = 0;       // MGX_PGS_SPW: slots per solver wave (debug)
+  int side_stream = 1;   // MGX_SIDE_STREAM: the wide solver launch on a side stream
+  int gcon = 1;          // MGX_GCON: the row builder's contact points in the pipe (0: in LDS)
+  int rows_lds = 0;      // MGX_ROWS_LDS: pad the row builder's LDS (occupancy probe)
+};
+Hooks read_hooks();
+}  // namespace mgx
+
 struct mgx_model {
+  mgx::Hooks hooks;
   int precision;
   int device;
   void* dbuf = nullptr;
@@ -78,7 +101,7 @@ int host_check_state(const mgx_state* s);
 int step_kernels_configure(const mgx_model* m);
 // the staged solver S2 (mgx_pgs.hip)
 template <typename T>
-void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big);
+void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big, const Hooks& h);
 // bytes: the solver kernels' dynamic-LDS limit; wide: the LDS-B instantiations' (the wide launch)
 int pgs_configure_lds(int precision, int bytes, int wide);
 // S1 / S3 and the one-wave settle (mgx_pgs.hip, the staged TU)
@@ -103,8 +126,6 @@ size_t make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks, Pipe
 // sqg: row scalars in the pipe, only the forces in LDS (the RK4 pipeline; soccer at full capacity)
 // twl: block-table words per block in LDS (mgx_twl: 8 for the 8-dof group layout, 4 dof-granular)
 int staged_pgs_lds_bytes(const mgx_model* m, int rows, int lps, int sqg, int twl);
-// the wide solver launch beside the main one on a side stream (MGX_SIDE_STREAM, default 1)
-int side_streams();
 // the staged RK4 bipedal step (mgx_rk_staged.hip)
 int bipedal_staged_configure(const mgx_model* m);
 int bipedal_step_staged(const mgx_model* m, const mgx_state* s, const mgx_bipedal_env* e, const float* action, float* obs,
@@ -125,7 +146,6 @@ int parkour_reset_staged(const mgx_model* m, const mgx_state* s, const mgx_parko
 int64_t parkour_workspace_bytes(const mgx_model* m, int n_env, int banks);
 int parkour_workspace_init(const mgx_model* m, void* workspace, uint64_t bytes, int n_env, int banks, hipStream_t st);
 int pgs_lanes();
-int pgs_lds_b();
 }  // namespace mgx
 
 #define MGX_WIDE_MSG "nv > 64: this model runs on the wide (two dofs per lane) kernels only"

@@ -30,39 +30,47 @@ struct MartialIds {
 // np.linalg.norm of a float64 2-vector: sqrt of the BLAS dot (one FMA)
 __device__ __forceinline__ double martial_norm2(double x, double y) { return sqrt(fma(y, y, x * x)); }
 
-// numpy float32 add.reduce of |clip(a, -1, 1)| over n contiguous values (pairwise: 8
-// accumulators over the first 8*floor(n/8), tree (01)(23) / (45)(67), then the tail)
-__device__ __forceinline__ float np_sum_abs_clip1(const float* action, int n) {
+// numpy add.reduce of |clip(a, -1, 1)| over n contiguous values in the action's dtype (float32
+// or float64; pairwise: 8 accumulators over the first 8*floor(n/8), tree (01)(23) / (45)(67), then
+// the tail)
+template <typename A>
+__device__ __forceinline__ A np_sum_abs_clip1(const A* action, int n) {
 #pragma clang fp contract(off)
   auto v = [&](int u) {
-    float a = action[u];
-    a = a < -1.0f ? -1.0f : (a > 1.0f ? 1.0f : a);
-    return fabsf(a);
+    A a = action[u];
+    a = a < (A)-1 ? (A)-1 : (a > (A)1 ? (A)1 : a);
+    return a < (A)0 ? -a : a;
   };
   if (n < 8) {
-    float res = 0.0f;
+    A res = 0;
     for (int u = 0; u < n; u++) res += v(u);
     return res;
   }
-  float r[8];
+  A r[8];
   for (int k = 0; k < 8; k++) r[k] = v(k);
   int i = 8;
   for (; i + 8 <= n; i += 8)
     for (int k = 0; k < 8; k++) r[k] += v(i + k);
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  A res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
   for (; i < n; i++) res += v(i);
   return res;
 }
 
-// clip -> ctrl (martial_arts_env.py:492-495): float32 action times the float64 ctrlrange bound
+// clip -> ctrl (martial_arts_env.py:492-495): the clipped action (float32, or float64 for a float64
+// policy) times the float64 ctrlrange bound
 template <typename T>
-__device__ __forceinline__ void martial_pre(const DevModel<T>& m, Env<T>& e, const MartialIds& ids,
-                                            const float* action) {
+__device__ __forceinline__ void martial_pre(const DevModel<T>& m, Env<T>& e, const MartialIds& ids, ActRow act) {
   const int l = lane_id();
   if (l < ids.n_act) {
-    float a = action[l];
-    a = a < -1.0f ? -1.0f : (a > 1.0f ? 1.0f : a);
-    e.ctrl[l] = (T)((double)a * ids.ctrl_scale[l]);
+    double a;
+    if (act.f64) {
+      a = act.d()[l];
+      a = a < -1.0 ? -1.0 : (a > 1.0 ? 1.0 : a);
+    } else {
+      float af = act.f()[l];
+      a = (double)(af < -1.0f ? -1.0f : (af > 1.0f ? 1.0f : af));
+    }
+    e.ctrl[l] = (T)(a * ids.ctrl_scale[l]);
   }
   wsync();
 }
@@ -93,10 +101,12 @@ __device__ __forceinline__ void martial_obs(const DevModel<T>& m, const Env<T>& 
 // _calculate_reward (:562-606) with the reference's numpy types: the reward is a Python float
 // until an np.float64 enters (min(1.0, h / 1.75) returns the np.float64 only when it is < 1;
 // the approach term); the energy term np.sum(np.abs(action)) * 0.01 is np.float32, so a
-// still-Python-float reward becomes float32 there and the approach term promotes it back.
+// still-Python-float reward becomes float32 there and the approach term promotes it back. A
+// float64 action (e64) makes the energy term np.float64, and the reward float64 from there on.
 // Advances the stance timer and techniques_performed as the reference does.
 __device__ __forceinline__ double martial_reward_np(double h, double rh, double lh, double rf, double lf, double ang,
-                                                    double dist, float energy, double* stance, int* tech) {
+                                                    double dist, float energy, double* stance, int* tech,
+                                                    bool e64 = false, double energy64 = 0.0) {
 #pragma clang fp contract(off)
   double r = 0.0;
   bool is64 = false;
@@ -110,7 +120,8 @@ __device__ __forceinline__ double martial_reward_np(double h, double rh, double 
     r += 200.0 * 0.01667;
   }
   const float ecost = energy * 0.01f;
-  if (is64) r -= (double)ecost;
+  if (e64) r -= energy64 * 0.01;
+  else if (is64) r -= (double)ecost;
   else r = (double)((float)r - ecost);
   if (dist < 2.0) r += 50.0 * (2.0 - dist);
   return r;
@@ -118,7 +129,7 @@ __device__ __forceinline__ double martial_reward_np(double h, double rh, double 
 
 // Post-physics: counter, obs, reward, termination, truncation, statistics. Returns done.
 template <typename T>
-__device__ __forceinline__ bool martial_post(const DevModel<T>& m, Env<T>& e, const MartialIds& ids, const float* action,
+__device__ __forceinline__ bool martial_post(const DevModel<T>& m, Env<T>& e, const MartialIds& ids, ActRow act,
                                              mgx_martial_env me, int env, float* obs, double* reward,
                                              uint8_t* terminated, uint8_t* truncated) {
 #pragma clang fp contract(off)
@@ -142,7 +153,8 @@ __device__ __forceinline__ bool martial_post(const DevModel<T>& m, Env<T>& e, co
     const double r = martial_reward_np(tz, nrm3(ids.right_hand, 0), nrm3(ids.left_hand, 0), nrm3(ids.right_foot, 0),
                                        nrm3(ids.left_foot, 0), nrm3(ids.torso, 3),
                                        martial_norm2((double)d1[0] - tx, (double)d1[1] - ty),
-                                       np_sum_abs_clip1(action + (size_t)env * ids.n_act, ids.n_act), &stance, &tech);
+                                       act.f64 ? 0.0f : np_sum_abs_clip1(act.f(), ids.n_act), &stance, &tech, act.f64 != 0,
+                                       act.f64 ? np_sum_abs_clip1(act.d(), ids.n_act) : 0.0);
     if (tz < 0.5) { falls += 1; term = true; }
     else term = fabs(tx) > 5.5 || fabs(ty) > 5.5;
     trunc = st >= ids.max_episode_steps;

@@ -64,9 +64,10 @@ __global__ void __launch_bounds__(64) k_martial(DevModel<T> m, MartialIds ids, m
     return;
   }
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  martial_pre(m, e, ids, action + (size_t)env * ids.n_act);
+  const ActRow act(action, me.action_f64, env, ids.n_act);
+  martial_pre(m, e, ids, act);
   const int warn = mj_step_env<T, false, true>(m, e);
-  const bool done = martial_post(m, e, ids, action, me, env, obs, reward, terminated, truncated);
+  const bool done = martial_post(m, e, ids, act, me, env, obs, reward, terminated, truncated);
   if (me.rollout && l == 0) {
     double* ro = me.rollout + 4 * (size_t)env;
     ro[0] += reward[env];
@@ -103,8 +104,9 @@ __global__ void __launch_bounds__(64) k_martial_logic(DevModel<T> m, MartialIds 
   for (int k = l; k < 4 * m.nbody; k += 64) e.xquat[k] = ((const T*)io.xquat)[(size_t)env * 4 * m.nbody + k];
   for (int k = l; k < 6 * m.nbody; k += 64) e.cvel[k] = ((const T*)io.cvel)[(size_t)env * 6 * m.nbody + k];
   wsync();
-  martial_pre(m, e, ids, io.action + (size_t)env * ids.n_act);
-  martial_post(m, e, ids, io.action, me, env, io.obs, io.reward, io.terminated, io.truncated);
+  const ActRow act(io.action, me.action_f64, env, ids.n_act);
+  martial_pre(m, e, ids, act);
+  martial_post(m, e, ids, act, me, env, io.obs, io.reward, io.terminated, io.truncated);
   for (int k = l; k < m.nu; k += 64) ((T*)io.ctrl)[(size_t)env * m.nu + k] = e.ctrl[k];
 }
 
@@ -164,6 +166,7 @@ int mgx_martial_step(const mgx_model* m, const mgx_state* s, const mgx_martial_e
                      double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
                      uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   if (!m->martial_ok) return fail(MGX_E_ARG, "mgx_martial_configure not called");
   if (!martial_env_ok(e)) return fail(MGX_E_ARG, "null martial-arts env buffer");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");

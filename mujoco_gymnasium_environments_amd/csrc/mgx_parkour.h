@@ -45,14 +45,21 @@ __device__ __forceinline__ double parkour_obs_d(int k, int f) {
   return t[k][f];
 }
 
-// action clip (float32) -> ctrl[:n_leg] (parkour_env.py:359-364)
+// action clip against the float32 bounds -> ctrl[:n_leg] (parkour_env.py:359-364), in the action's
+// dtype (a float64 action stays float64)
 template <typename T>
-__device__ __forceinline__ void parkour_pre(const DevModel<T>& m, Env<T>& e, const ParkourIds<T>& ids, const float* action) {
+__device__ __forceinline__ void parkour_pre(const DevModel<T>& m, Env<T>& e, const ParkourIds<T>& ids, ActRow act) {
   int l = lane_id();
   if (l < ids.n_leg) {
-    float a = action[l], lim = ids.act_lim[l];
-    a = a < -lim ? -lim : (a > lim ? lim : a);
-    e.ctrl[l] = (T)a;
+    if (act.f64) {
+      double a = act.d()[l], lim = (double)ids.act_lim[l];
+      a = a < -lim ? -lim : (a > lim ? lim : a);
+      e.ctrl[l] = (T)a;
+    } else {
+      float a = act.f()[l], lim = ids.act_lim[l];
+      a = a < -lim ? -lim : (a > lim ? lim : a);
+      e.ctrl[l] = (T)a;
+    }
   }
   wsync();
 }
@@ -73,17 +80,19 @@ __device__ __forceinline__ int parkour_foot_mask(const Env<T>& e, const ParkourI
   return mask;
 }
 
-// the reference's np.sum(np.abs(clip(a))) over 16 float32 values: numpy's pairwise sum
-// (eight partial sums r[j] = a[j] + a[j+8], then ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)))
-__device__ __forceinline__ float np_sum16_abs_clip(const float* a, const float* lim) {
+// the reference's np.sum(np.abs(clip(a))) over 16 values in the action's dtype (float32 or
+// float64): numpy's pairwise sum (eight partial sums r[j] = a[j] + a[j+8], then
+// ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)))
+template <typename A>
+__device__ __forceinline__ A np_sum16_abs_clip(const A* a, const float* lim) {
 #pragma clang fp contract(off)
-  float v[16];
+  A v[16];
   for (int j = 0; j < 16; j++) {
-    float x = a[j];
-    x = x < -lim[j] ? -lim[j] : (x > lim[j] ? lim[j] : x);
-    v[j] = fabsf(x);
+    A x = a[j], lo = (A)-lim[j], hi = (A)lim[j];
+    x = x < lo ? lo : (x > hi ? hi : x);
+    v[j] = x < (A)0 ? -x : x;
   }
-  float r[8];
+  A r[8];
   for (int j = 0; j < 8; j++) r[j] = v[j] + v[j + 8];
   return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 }
@@ -127,7 +136,7 @@ __device__ __forceinline__ void parkour_obs(const DevModel<T>& m, const Env<T>& 
 
 // reward + termination + counters (parkour_env.py:646-755, :381-385); returns done
 template <typename T>
-__device__ __forceinline__ bool parkour_post(const DevModel<T>& m, Env<T>& e, const ParkourIds<T>& ids, const float* action,
+__device__ __forceinline__ bool parkour_post(const DevModel<T>& m, Env<T>& e, const ParkourIds<T>& ids, ActRow act,
                                              ParkourState ps, int env, float* obs, double* reward, uint8_t* terminated,
                                              uint8_t* truncated) {
 #pragma clang fp contract(off)
@@ -170,11 +179,17 @@ __device__ __forceinline__ bool parkour_post(const DevModel<T>& m, Env<T>& e, co
     if (fabs((double)e.qpos[3]) > 0.7) r += 100.0;
     int nfeet = __popc(fm);
     if (nfeet >= 1 && nfeet <= 3) r += 200.0;
-    float effort = np_sum16_abs_clip(action + (size_t)env * ids.n_leg, ids.act_lim) * 0.1f;
     bool f32 = !(progress > 0);
     float rf = 0.0f;
-    if (f32) rf = (float)r - effort;
-    else r = r - (double)effort;
+    if (act.f64) {
+      // float64 action: np.float64 effort, so the reward is np.float64 from here on
+      r = r - np_sum16_abs_clip(act.d(), ids.act_lim) * 0.1;
+      f32 = false;
+    } else {
+      const float effort = np_sum16_abs_clip(act.f(), ids.act_lim) * 0.1f;
+      if (f32) rf = (float)r - effort;
+      else r = r - (double)effort;
+    }
     bool low = z < 0.2, many = e.ncon > 8;
     if (low) falls += 1;
     bool still = fabs(progress) < 0.01;

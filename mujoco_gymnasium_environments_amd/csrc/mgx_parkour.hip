@@ -67,11 +67,11 @@ __global__ void __launch_bounds__(64) k_parkour(DevModel<T> m, ParkourIds<T> ids
     return;
   }
   load_state(m, e, qpos, qvel, qacc, ctrl, qfrc, xfrc, tm, env);
-  const float* a = action + (size_t)env * ids.n_leg;
+  const ActRow a(action, ev.action_f64, env, ids.n_leg);
   parkour_pre(m, e, ids, a);
   int warn = 0;
   for (int k = 0; k < 10; k++) warn += mj_step_env(m, e);  // frame_skip (parkour_env.py:367-368)
-  bool done = parkour_post(m, e, ids, action, ev, env, obs, reward, terminated, truncated);
+  bool done = parkour_post(m, e, ids, a, ev, env, obs, reward, terminated, truncated);
   if (ev.rollout && l == 0) {
     T* ro = (T*)ev.rollout + 4 * (size_t)env;
     ro[0] += (T)reward[env];
@@ -112,8 +112,9 @@ __global__ void __launch_bounds__(64) k_parkour_logic(DevModel<T> m, ParkourIds<
     e.con_geom[2 * c + 1] = io.con_geom[((size_t)env * io.max_contacts + c) * 2 + 1];
   }
   wsync();
-  parkour_pre(m, e, ids, io.action + (size_t)env * ids.n_leg);
-  parkour_post(m, e, ids, io.action, ev, env, io.obs, io.reward, io.terminated, io.truncated);
+  const ActRow a(io.action, ev.action_f64, env, ids.n_leg);
+  parkour_pre(m, e, ids, a);
+  parkour_post(m, e, ids, a, ev, env, io.obs, io.reward, io.terminated, io.truncated);
   wsync();
   for (int k = l; k < m.nu; k += 64) ((T*)io.ctrl)[(size_t)env * m.nu + k] = e.ctrl[k];
 }
@@ -185,6 +186,7 @@ int mgx_parkour_step(const mgx_model* m, const mgx_state* s, const mgx_parkour_e
                      double* reward, uint8_t* terminated, uint8_t* truncated, float* final_obs, int autoreset,
                      uint64_t seed, int env_offset, int n_env, const uint8_t* mask, void* stream) {
   if (!m || !e || !action || !obs || !reward || !terminated || !truncated) return fail(MGX_E_ARG, "null argument");
+  if (e->action_f64 != 0 && e->action_f64 != 1) return fail(MGX_E_ARG, "action_f64 must be 0 (float32) or 1 (float64)");
   if (!m->parkour_ok) return fail(MGX_E_ARG, "mgx_parkour_configure not called");
   if (!parkour_env_ok(e)) return fail(MGX_E_ARG, "null parkour env buffer");
   if (autoreset && !e->episode) return fail(MGX_E_ARG, "autoreset needs the episode counter buffer");

@@ -23,18 +23,10 @@ int pgs_lanes() {
   }();
   return lanes;
 }
-// main launch with B in an LDS arena (1) or read from global memory (0): MGX_PGS_LDS_B
-// (compile-time default) or the environment variable of that name, read per call
-int pgs_lds_b() {
-  const char* e = getenv("MGX_PGS_LDS_B");
-  return e ? (atoi(e) != 0) : MGX_PGS_LDS_B;
-}
-
 template <typename T, int LPS, bool BLDS, bool SQG = false>
 static void launch_lps(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big,
-                       int spw_force = 0) {
-  static const int spw_env = getenv("MGX_PGS_SPW") ? atoi(getenv("MGX_PGS_SPW")) : 0;  // debug: slots per wave
-  const int spw = spw_force ? spw_force : spw_env ? spw_env : 64 / LPS;
+                       int spw_hook, int spw_force = 0) {
+  const int spw = spw_force ? spw_force : spw_hook ? spw_hook : 64 / LPS;  // spw_hook: MGX_PGS_SPW (debug)
   int grid = (slots + (spw < 0 ? -spw : spw) - 1) / (spw < 0 ? -spw : spw);
   switch ((P.dpl + LPS / 8 - 1) / (LPS / 8)) {  // register entries per lane
 #define MGX_PGS_CASE(E)                                                                                          \
@@ -53,25 +45,26 @@ static void launch_lps(const Pipe& P, int slots, int lds, hipStream_t st, int ma
 }
 
 template <typename T>
-void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big) {
+void launch_pgs(const Pipe& P, int slots, int lds, hipStream_t st, int maxit, T tol, T scale, int big, const Hooks& h) {
   if (big && P.warena > 0 && pgs_lanes() == 16) {
     // the wide launch with LDS-resident B: one slot per wave (all four lane groups on it), a
     // small grid striding over the few slots past the main launch's rows
-    launch_lps<T, 16, true>(P, MGX_PGS_WIDE_LDS_GRID, P.warena + 64, st, maxit, tol, scale, big, 1);
+    launch_lps<T, 16, true>(P, MGX_PGS_WIDE_LDS_GRID, P.warena + 64, st, maxit, tol, scale, big, h.pgs_spw, 1);
     return;
   }
-  const bool blds = !big && pgs_lds_b();
+  const bool blds = !big && h.pgs_lds_b;  // the main launch with B in an LDS arena (MGX_PGS_LDS_B)
+  const int sp = h.pgs_spw;
   if (pgs_lanes() == 64) {
-    if (blds) launch_lps<T, 64, true>(P, slots, lds, st, maxit, tol, scale, big);
-    else launch_lps<T, 64, false>(P, slots, lds, st, maxit, tol, scale, big);
+    if (blds) launch_lps<T, 64, true>(P, slots, lds, st, maxit, tol, scale, big, sp);
+    else launch_lps<T, 64, false>(P, slots, lds, st, maxit, tol, scale, big, sp);
   } else {
-    if (blds) launch_lps<T, 16, true>(P, slots, lds, st, maxit, tol, scale, big);
-    else if (P.sqg && !big) launch_lps<T, 16, false, true>(P, slots, lds, st, maxit, tol, scale, big);
-    else launch_lps<T, 16, false>(P, slots, lds, st, maxit, tol, scale, big);
+    if (blds) launch_lps<T, 16, true>(P, slots, lds, st, maxit, tol, scale, big, sp);
+    else if (P.sqg && !big) launch_lps<T, 16, false, true>(P, slots, lds, st, maxit, tol, scale, big, sp);
+    else launch_lps<T, 16, false>(P, slots, lds, st, maxit, tol, scale, big, sp);
   }
 }
-template void launch_pgs<float>(const Pipe&, int, int, hipStream_t, int, float, float, int);
-template void launch_pgs<double>(const Pipe&, int, int, hipStream_t, int, double, double, int);
+template void launch_pgs<float>(const Pipe&, int, int, hipStream_t, int, float, float, int, const Hooks&);
+template void launch_pgs<double>(const Pipe&, int, int, hipStream_t, int, double, double, int, const Hooks&);
 
 // ---- S1 / S3 (the row builder and the finisher)
 template <typename T>
@@ -196,9 +189,6 @@ template <typename T>
 void launch_soccer_rows(const DevModel<T>& Ms, const SoccerIds<T>& ids, const mgx_state& s, const mgx_soccer_env& ev,
                         const float* action, int n_env, const uint8_t* mask, const Pipe& P, int banks, int slots, int lds,
                         hipStream_t st) {
-  // occupancy probe: MGX_ROWS_LDS pads the row builder's LDS (fewer waves per CU; up to 64 KiB)
-  static const int pad = getenv("MGX_ROWS_LDS") ? atoi(getenv("MGX_ROWS_LDS")) : 0;
-  if (pad > lds && pad <= 64 * 1024) lds = pad;
   hipLaunchKernelGGL(k_soccer_rows<T>, dim3(slots), dim3(64), lds, st, Ms, ids, s, ev, action, n_env, mask, P, banks);
 }
 template <typename T>

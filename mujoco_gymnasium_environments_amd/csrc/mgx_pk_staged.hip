@@ -111,7 +111,8 @@ __device__ __forceinline__ void pk_bank_copy_live(const DevModel<T>& m, const Pi
 // (its settle step bk, while 0 <= bk < 10)
 template <typename T>
 __global__ void __launch_bounds__(64) k_pk_rows(DevModel<T> m, ParkourIds<T> ids, mgx_state s, const float* action,
-                                                int n_env, const uint8_t* mask, Pipe P, int banks, int sub) {
+                                                int action_f64, int n_env, const uint8_t* mask, Pipe P, int banks,
+                                                int sub) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   Env<T> e;
@@ -121,7 +122,7 @@ __global__ void __launch_bounds__(64) k_pk_rows(DevModel<T> m, ParkourIds<T> ids
     bind_carry_tail(m, e, P, b);
     load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied, (T*)s.xfrc_applied,
                (T*)s.time, b);
-    if (sub == 0) parkour_pre(m, e, ids, action + (size_t)b * ids.n_leg);
+    if (sub == 0) parkour_pre(m, e, ids, ActRow(action, action_f64, b, ids.n_leg));
   } else {
     const int bi = b - n_env;
     if (!banks || bi >= n_env * P.R) return;
@@ -199,7 +200,8 @@ __global__ void __launch_bounds__(64) k_pk_finish(DevModel<T> m, ParkourIds<T> i
     return;
   }
   if (l == 0 && s.overflow && over) s.overflow[env] += 1;
-  const bool done = parkour_post(m, e, ids, action, ev, env, obs, reward, terminated, truncated);
+  const bool done =
+      parkour_post(m, e, ids, ActRow(action, ev.action_f64, env, ids.n_leg), ev, env, obs, reward, terminated, truncated);
   if (ev.rollout && l == 0) {
     T* ro = (T*)ev.rollout + 4 * (size_t)env;
     ro[0] += (T)reward[env];
@@ -387,14 +389,16 @@ int step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms,
   const int banks = autoreset ? e->banks : 0;
   const size_t need = make_staged_pipe(m, e->workspace, n_env, e->banks, &P, false, PK_OBS);
   if (e->workspace_bytes < need) return fail(MGX_E_ARG, "workspace smaller than mgx_parkour_workspace_bytes");
-  if (P.maxE > P.capE || P.sqg) return fail(MGX_E_UNSUPPORTED, "staged parkour step: rows beyond the main solver launch");
+  // parkour_staged_ok: every slot is solved by the main launch (a slot over capE rows, e.g. the
+  // qpos0 pile-up after a bad-state reset, in its heaviest-first list with its scalars read from
+  // the pipe: Pipe.hmain)
   const int slots = n_env * (1 + banks);
   const T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
   const int mlds = staged_pgs_lds_bytes(m, P.capE, PK_LPS, 0, 8);
   const int spw = 64 / PK_LPS, grid = (slots + spw - 1) / spw;
   for (int k = 0; k < PK_SUBSTEPS; k++) {
-    hipLaunchKernelGGL(k_pk_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, action, n_env, mask, P, banks,
-                       k);
+    hipLaunchKernelGGL(k_pk_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, action, e->action_f64, n_env,
+                       mask, P, banks, k);
     MGX_PK_EPL(pk_epl(M), hipLaunchKernelGGL((k_pgs_groups<T, E, PK_LPS, false>), dim3(grid), dim3(64), mlds, st, P,
                                              M.iterations, M.tolerance, scale, spw, 0));
     if (banks && P.R > 0)
@@ -445,9 +449,15 @@ int configure_t(const mgx_model* m) {
 }  // namespace
 
 namespace mgx {
+// The staged parkour step runs the main solver launch only (no wide launch beside it): a model
+// (with its hooks) whose pipe would need one is refused here, and the env falls back to the
+// monolithic step (envs/parkour.py), which holds the same capacity.
 bool parkour_staged_ok(const mgx_model* m) {
   const int nv = m->precision == MGX_F32 ? m->mf.nv : m->md.nv;
-  return m->staged_ok && nv <= 64;
+  if (!m->staged_ok || nv > 64 || pgs_lanes() != PK_LPS || m->hooks.pgs_lds_b) return false;
+  Pipe P;
+  make_staged_pipe(m, nullptr, 1, 1, &P, false, PK_OBS);
+  return !P.sqg && (P.maxE <= P.capE || P.hmain);
 }
 
 int parkour_staged_configure(const mgx_model* m) {

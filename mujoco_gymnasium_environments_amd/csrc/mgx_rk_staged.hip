@@ -104,7 +104,7 @@ __device__ __forceinline__ void rk_bank_init(const DevModel<T>& m, Env<T>& e, co
 template <typename T>
 __device__ __forceinline__ void rk_bank_finalize(const DevModel<T>& m, Env<T>& e, const BipedalIds& ids, const Pipe& P,
                                                  int bi) {
-  bipedal_obs(m, e, ids, 0, 0, 0, 1000.0f, P.at<float>(P.o_bobs) + (size_t)bi * RK_OBS);
+  bipedal_obs(m, e, ids, 0, 0, 0, 1000.0, false, P.at<float>(P.o_bobs) + (size_t)bi * RK_OBS);
   int l = lane_id();
   if (l < 3) P.at<T>(P.o_bprev)[(size_t)bi * 6 + l] = e.xpos[3 * ids.torso + l];
   wsync();
@@ -129,8 +129,9 @@ __device__ __forceinline__ void rk_bank_copy_live(const DevModel<T>& m, const Pi
     ((T*)s.time)[env] = P.at<T>(P.o_btime)[bi];
     if (s.warning) s.warning[env] += P.at<int>(P.o_bwarn)[bi];
     be.step[env] = 0;
-    be.energy[env] = 1000.0f;
-    be.energy_used[env] = 0.0f;
+    be.energy[env] = 1000.0;
+    be.energy_used[env] = 0.0;
+    if (be.energy_kind) be.energy_kind[env] = EK_PY;
     be.rescued[env] = 0;
     be.carried[env] = 0;
     be.carrying[env] = 0;
@@ -161,7 +162,7 @@ __device__ __forceinline__ void rk_rows_slot(const DevModel<T>& m, Env<T>& e, co
     if (bi < 0) {
       load_state(m, e, (T*)s.qpos, (T*)s.qvel, (T*)s.qacc_warmstart, (T*)s.ctrl, (T*)s.qfrc_applied,
                  (T*)s.xfrc_applied, (T*)s.time, env);
-      bipedal_pre(m, e, ids, action + (size_t)env * ids.n_act, be, env);
+      bipedal_pre(m, e, ids, ActRow(action, be.action_f64, env, ids.n_act), be, env);
     } else {
       bank_load_state(m, e, P, bi);
     }
@@ -236,7 +237,8 @@ __device__ __forceinline__ void rk_step_end(const DevModel<T>& m, Env<T>& f, con
               (T*)s.time, env);
   if (l == 0 && s.warning) s.warning[env] += warn;
   if (l == 0 && s.overflow && overflow) s.overflow[env] += 1;
-  const bool done = bipedal_post(m, f, ids, action, be, env, obs, reward, terminated, truncated);
+  const bool done =
+      bipedal_post(m, f, ids, ActRow(action, be.action_f64, env, ids.n_act), be, env, obs, reward, terminated, truncated);
   if (be.rollout && l == 0) {
     T* ro = (T*)be.rollout + 4 * (size_t)env;
     ro[0] += (T)reward[env];
@@ -600,7 +602,7 @@ int step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms,
   const T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
   const int mlds = staged_pgs_lds_bytes(m, P.capE, RK_LPS, 1, 4), wlds = staged_pgs_lds_bytes(m, P.maxE, RK_LPS, 1, 4);
   const int wgrid = 64 / RK_LPS * MGX_PGS_WIDE_GRID;
-  RkSide* side = side_streams() ? rk_side(st) : nullptr;
+  RkSide* side = m->hooks.side_stream ? rk_side(st) : nullptr;
   for (int k = 0; k < 4; k++) {
     hipLaunchKernelGGL(k_rk_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, m->bp, *s, *e, action, n_env, mask, P,
                        banks, k);

@@ -31,13 +31,7 @@ struct SoccerIds {
 // One env's action row: float32, or float64 (mgx_soccer_env.action_f64) — the reference's np.clip
 // against the float32 action_space bounds keeps a float64 policy's action float64, so ctrl and
 // the energy term then follow in float64 (soccer_env.py:401-405, :674).
-struct SoccerAct {
-  const void* p;
-  int f64;
-  __device__ SoccerAct(const void* base, int f64_, size_t row, int nu)
-      : p(f64_ ? (const void*)((const double*)base + row * nu) : (const void*)((const float*)base + row * nu)),
-        f64(f64_) {}
-};
+using SoccerAct = ActRow;
 
 // Pre-physics env logic: action clip -> ctrl, goalkeeper, wind (soccer_env.py:401-411)
 template <typename T>

@@ -34,7 +34,7 @@ import torch
 from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import check, lib
-from ..spaces import Box, EnvBase
+from ..spaces import Box, EnvBase, policy_action
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets",
                      "robotic_arm_assembly.xml")
@@ -190,8 +190,12 @@ class AssemblyVectorEnv:
     def step(self, actions: torch.Tensor, stream=None):
         """One env step (10 mj_steps) for every env. ``actions`` float32 [N, 9]: 7 joint
         commands, gripper opening (mm), grip force (unused by the reference, :252-265)."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        # float32, or float64: the reference's np.clip keeps a float64 policy's dtype, so ctrl and the
+        # action terms of the reward follow in float64 (include/mgx.h action_f64)
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
+        self._env.action_f64 = 1 if dt == torch.float64 else 0
         assert actions.shape == (self.num_envs, N_ACT), actions.shape
         check(lib().mgx_assembly_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
                                       _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
@@ -256,7 +260,7 @@ class RoboticArmAssemblyEnv(EnvBase):
         return obs[0].cpu().numpy().copy(), self._get_info()
 
     def step(self, action: np.ndarray):
-        a = torch.from_numpy(np.asarray(action, dtype=np.float32).reshape(1, -1)).to(self._vec.device)
+        a = torch.from_numpy(policy_action(action).reshape(1, -1)).to(self._vec.device)
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         return obs[0].cpu().numpy().copy(), float(rew[0]), bool(term[0]), bool(trunc[0]), self._get_info()

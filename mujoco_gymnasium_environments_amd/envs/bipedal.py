@@ -31,7 +31,7 @@ from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import NativeError, check, lib
 from ..seeding import np_random
-from ..spaces import Box, EnvBase
+from ..spaces import Box, EnvBase, policy_action
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "bipedal_rescue.xml")
 # MuJoCo keeps every contact (no arena limit at these sizes). Measured at bench conditions (U(-100,
@@ -133,8 +133,11 @@ class BipedalVectorEnv:
         i32 = dict(dtype=torch.int32, device=dev)
         f64 = dict(dtype=torch.float64, device=dev)
         self.step_count = torch.zeros(N, **i32)
-        self.energy = torch.full((N,), ENERGY_LIMIT, dtype=torch.float32, device=dev)
-        self.energy_used = torch.zeros(N, dtype=torch.float32, device=dev)
+        # current_energy / energy_used hold float32 values (numpy's float32 arithmetic for float32
+        # actions) or float64 ones after a float64 action; energy_kind records which (include/mgx.h)
+        self.energy = torch.full((N,), ENERGY_LIMIT, **f64)
+        self.energy_used = torch.zeros(N, **f64)
+        self.energy_kind = torch.zeros(N, dtype=torch.uint8, device=dev)
         self.rescued = torch.zeros(N, **i32)
         self.carried = torch.zeros(N, **i32)
         self.carrying = torch.zeros(N, dtype=torch.uint8, device=dev)
@@ -161,6 +164,7 @@ class BipedalVectorEnv:
             self.step_count, self.energy, self.energy_used, self.rescued, self.carried, self.carrying, self.closest,
             self.prev_rescued, self.prev_carried, self.prev_sz, self.fall_timer, self.victims_rescued, self.distance,
             self.ttfr, self.falls, self.collisions, self.prev_robot_pos, self.episode, self.rollout)])
+        self._env.energy_kind = self.energy_kind.data_ptr()
         ids = self.tables.ids_struct()
         check(lib().mgx_bipedal_configure(self.native.handle, C.byref(ids)), "mgx_bipedal_configure")
         self.staged = staged
@@ -193,10 +197,14 @@ class BipedalVectorEnv:
         return self.obs, self.info()
 
     def step(self, actions: torch.Tensor, stream=None):
-        """One env step (one RK4 mj_step) for every env. ``actions`` float32 [N, 26]."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        """One env step (one RK4 mj_step) for every env. ``actions`` [N, 26] float32, or float64: a
+        float64 action is clipped and applied in float64 and its energy terms follow in float64, as
+        the reference's np.clip keeps a float64 policy's dtype (rescue_env.py:420-429, :650)."""
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
         assert actions.shape == (self.num_envs, N_ACT), actions.shape
+        self._env.action_f64 = 1 if dt == torch.float64 else 0
         check(lib().mgx_bipedal_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
                                      _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
                                      _ptr(self.truncated), _ptr(self.final_obs) if self.autoreset else None,
@@ -255,9 +263,10 @@ class BipedalRescueEnv(EnvBase):
         self.victim_priorities = [0.8, 1.0, 0.7, 0.9, 1.0]
         self.fire_zones = [{'pos': np.array([-5.0, -3.0, 0.0]), 'radius': 1.5},
                            {'pos': np.array([8.0, 6.0, 0.0]), 'radius': 1.2}]
-        # one env: the single-launch monolithic kernel has the lowest step latency
+        # one env on the staged RK4 pipeline at the model's full capacity (192 contacts / 768 rows; the
+        # monolithic kernel holds 512 rows), reset() settled by the same stages, no reset banks
         self._vec = BipedalVectorEnv(1, device=device, precision=precision, autoreset=False,
-                                     max_episode_steps=self.max_episode_steps, staged=False)
+                                     max_episode_steps=self.max_episode_steps, staged=True, banks=0)
         self.model = self._vec.model
         self.num_actuators = N_ACT
         self.action_space = Box(low=-ACTION_LIMIT, high=ACTION_LIMIT, shape=(N_ACT,), dtype=np.float32)
@@ -284,7 +293,7 @@ class BipedalRescueEnv(EnvBase):
                                                'energy_remaining')}
 
     def step(self, action: np.ndarray):
-        a = torch.from_numpy(np.asarray(action, dtype=np.float32).reshape(1, -1)).to(self._vec.device)
+        a = torch.from_numpy(policy_action(action).reshape(1, -1)).to(self._vec.device)
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = int(self._vec.step_count[0])
@@ -295,7 +304,7 @@ class BipedalRescueEnv(EnvBase):
         v = self._vec
         ttfr = float(v.ttfr[0])
         stats = {'victims_rescued': int(v.victims_rescued[0]), 'distance_traveled': float(v.distance[0]),
-                 'energy_used': np.float32(v.energy_used[0].item()),
+                 'energy_used': self._energy_type()(v.energy_used[0].item()),
                  'time_to_first_rescue': None if np.isnan(ttfr) else ttfr,
                  'falls': int(v.falls[0]), 'collisions': int(v.collisions[0])}
         up = v.obs[0, 55:59].double().cpu().numpy()
@@ -303,8 +312,13 @@ class BipedalRescueEnv(EnvBase):
         return {'episode_stats': stats, 'robot_position': v.prev_robot_pos[0].cpu().numpy().copy(),
                 'victims_remaining': 5 - bin(int(v.rescued[0])).count("1"),
                 'victims_carried': bin(int(v.carried[0])).count("1"),
-                'energy_remaining': np.float32(v.energy[0].item()),
+                'energy_remaining': self._energy_type()(v.energy[0].item()),
                 'robot_upright': bool(w * w - x * x - y * y + z * z > 0.7)}
+
+    def _energy_type(self):
+        """numpy type of current_energy / energy_used: a Python float after reset, np.float32 after
+        float32 actions, np.float64 once a float64 action's cost was subtracted"""
+        return {0: float, 1: np.float64, 2: np.float32}[int(self._vec.energy_kind[0])]
 
     def render(self):
         return None  # rescue_env.py:779-783 (viewer sync only)

@@ -30,7 +30,7 @@ from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import check, lib
 from ..seeding import np_random
-from ..spaces import Box, EnvBase
+from ..spaces import Box, EnvBase, policy_action
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets",
                      "humanoid_construction.xml")
@@ -101,7 +101,10 @@ class ConstructionVectorEnv:
         dev, N = self.device, num_envs
         self.scal = torch.zeros(N, 4, dtype=torch.float64, device=dev)   # progress, wind, rain, temperature
         self.ints = torch.zeros(N, 5, dtype=torch.int32, device=dev)     # task, step, blocks, violations, completed
-        self.total_reward = torch.zeros(N, dtype=torch.float32, device=dev)
+        # episode_stats['total_reward']: a float32 value (NEP 50 keeps it np.float32 for float32 actions)
+        # or float64 once a float64 action's reward was added; total_kind records which (include/mgx.h)
+        self.total_reward = torch.zeros(N, dtype=torch.float64, device=dev)
+        self.total_kind = torch.zeros(N, dtype=torch.uint8, device=dev)
         self.episode = torch.zeros(N, dtype=torch.int32, device=dev)
         self.rollout = torch.zeros(N, 4, dtype=torch.float64, device=dev)
         self.obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
@@ -111,6 +114,7 @@ class ConstructionVectorEnv:
         self.truncated = torch.zeros(N, dtype=torch.uint8, device=dev)
         self._env = cabi.MgxConstructionEnv(*[t.data_ptr() for t in (self.scal, self.ints, self.total_reward,
                                                                       self.episode, self.rollout)])
+        self._env.total_kind = self.total_kind.data_ptr()
         ids = self.tables.ids_struct()
         check(lib().mgx_construction_configure(self.native.handle, C.byref(ids)), "mgx_construction_configure")
         self.action_space = Box(low=-ACTION_LIMIT, high=ACTION_LIMIT, shape=(self.model.nu,), dtype=np.float32)
@@ -131,9 +135,13 @@ class ConstructionVectorEnv:
         return self.obs, self.info()
 
     def step(self, actions: torch.Tensor, stream=None):
-        """One env step for every env. ``actions`` float32 [N, nu] (clipped to +-200)."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        """One env step for every env. ``actions`` [N, nu] float32 or float64 (clipped to +-200)."""
+        # float32, or float64: the reference's np.clip keeps a float64 policy's dtype, so ctrl and the
+        # action terms of the reward follow in float64 (include/mgx.h action_f64)
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
+        self._env.action_f64 = 1 if dt == torch.float64 else 0
         assert actions.shape == (self.num_envs, self.model.nu), actions.shape
         check(lib().mgx_construction_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
                                           _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
@@ -164,10 +172,10 @@ class ConstructionVectorEnv:
 
 class HumanoidConstructionEnv(EnvBase):
     """Drop-in for humanoid_construction_env.construction_env.HumanoidConstructionEnv on libmgx.
-    Actions are taken as float32. For float32 input (``action_space.sample()``, float32 policies)
-    this is exactly the reference, which clips against its float32 action_space bounds. A float64
-    action stays float64 in the reference's clip, so its ``ctrl`` and energy term then differ from
-    this env's at the rounding of the float32 cast (documented quirk).
+    A float32 action (``action_space.sample()``, float32 policies) is clipped against the float32
+    bounds in float32, and the reward is np.float32; a float64 action (or a list of floats) stays
+    float64 through the clip, ``ctrl`` and the energy term, and the reward is np.float64, as in the
+    reference (construction_env.py:589-592, :691).
 
     ``info['episode_stats']['total_reward']`` is the running total *before* this step's reward:
     the reference copies ``episode_stats`` into ``info`` (construction_env.py:613-614, :746) and
@@ -210,13 +218,16 @@ class HumanoidConstructionEnv(EnvBase):
         return obs[0].cpu().numpy().copy(), self._info()
 
     def step(self, action: np.ndarray):
-        a = torch.from_numpy(np.asarray(action, dtype=np.float32).reshape(1, -1)).to(self._vec.device)
+        act = policy_action(action)
+        a = torch.from_numpy(act.reshape(1, -1)).to(self._vec.device)
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = int(self._vec.ints[0, 1])
         info = self._info()  # the total as it was before this step's reward (construction_env.py:614-617)
-        self._total_before = np.float32(self._vec.total_reward[0].item())
-        return obs[0].cpu().numpy().copy(), np.float32(rew[0].item()), bool(term[0]), bool(trunc[0]), info
+        kind = int(self._vec.total_kind[0])
+        self._total_before = (np.float64 if kind == 1 else np.float32)(self._vec.total_reward[0].item())
+        rtype = np.float64 if act.dtype == np.float64 else np.float32
+        return obs[0].cpu().numpy().copy(), rtype(rew[0].item()), bool(term[0]), bool(trunc[0]), info
 
     def _info(self) -> Dict[str, Any]:
         v = self._vec

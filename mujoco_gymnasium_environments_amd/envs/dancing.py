@@ -31,7 +31,7 @@ from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import check, lib
 from ..seeding import np_random
-from ..spaces import Box, EnvBase
+from ..spaces import Box, EnvBase, policy_action
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "humanoid_dancing.xml")
 MOVES = ['basic_step', 'spin', 'jump', 'moonwalk', 'robot_wave', 'freeze', 'hip_hop_bounce', 'breakdance_toprock',
@@ -70,6 +70,10 @@ def _dancing_model(rows_in_scratch: bool) -> mjcf.Model:
     # instead of three. MGX_DANCING_ROWS_LDS=1 keeps them in LDS.
     if rows_in_scratch:
         m.layout_flags = cabi.MGX_ROWS_IN_SCRATCH
+    # contact / row capacity: the library default, 64 contacts / 192 rows. The oracle census at the
+    # bench's U(-200, 200) actions (tools/capacity_census.py --task dancing: 32 envs x 500 env steps,
+    # autoreset) peaks at 29 contacts / 121 rows, so MuJoCo's arena never holds more than this does
+    # (Capacity); the bench line counts any overflowing step.
     return m
 
 
@@ -169,8 +173,12 @@ class DancingVectorEnv:
 
     def step(self, actions: torch.Tensor, stream=None):
         """One env step (one RK4 mj_step) for every env. ``actions`` float32 [N, 29]."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        # float32, or float64: the reference's np.clip keeps a float64 policy's dtype, so ctrl and the
+        # action terms of the reward follow in float64 (include/mgx.h action_f64)
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
+        self._env.action_f64 = 1 if dt == torch.float64 else 0
         assert actions.shape == (self.num_envs, N_ACT), actions.shape
         check(lib().mgx_dancing_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
                                      _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
@@ -243,7 +251,7 @@ class HumanoidDancingEnv(EnvBase):
                                              'combo_multiplier': info['combo_multiplier']}
 
     def step(self, action: np.ndarray):
-        a = torch.from_numpy(np.asarray(action, dtype=np.float32).reshape(1, -1)).to(self._vec.device)
+        a = torch.from_numpy(policy_action(action).reshape(1, -1)).to(self._vec.device)
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = int(self._vec.ints[0, 0])

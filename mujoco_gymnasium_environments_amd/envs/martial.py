@@ -24,7 +24,7 @@ from .. import cabi, mjcf
 from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import check, lib
 from ..seeding import np_random
-from ..spaces import Box, EnvBase
+from ..spaces import Box, EnvBase, policy_action
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets",
                      "humanoid_martial_arts.xml")
@@ -43,12 +43,22 @@ def martial_model(rows_in_scratch: Optional[bool] = None) -> mjcf.Model:
     return _martial_model(bool(rows_in_scratch))
 
 
+CON_CAPACITY = 96
+EFC_CAPACITY = 384
+
+
 @functools.lru_cache(maxsize=None)
 def _martial_model(rows_in_scratch: bool) -> mjcf.Model:
     """The scene the reference's _generate_xml_files writes (martial_arts_env.py:150-381)."""
     with open(ASSET) as f:
         m = mjcf.compile_xml(f.read())
     m.layout_flags = cabi.MGX_KEEP_CVEL  # the observation and reward read cvel (:536-589)
+    # contact / row capacity: the oracle census at the bench's U(-1, 1) actions
+    # (tools/capacity_census.py --task martial: 128 envs x 1000 env steps, autoreset) peaks at 75
+    # contacts / 320 rows, p99 208 rows — above the 64 / 192 default on ~1.5% of steps. MuJoCo keeps
+    # them all; 96 / 384 holds the census maximum (DESIGN.md §3, Capacity).
+    m.con_capacity = CON_CAPACITY
+    m.efc_capacity = EFC_CAPACITY
     # constraint rows in per-env global scratch: the env's LDS drops from 65 to 30 KiB (fp32),
     # five envs per CU instead of two (DESIGN.md §4); MGX_MARTIAL_ROWS_LDS=1 keeps them in LDS
     if rows_in_scratch:
@@ -138,8 +148,12 @@ class MartialArtsVectorEnv:
 
     def step(self, actions: torch.Tensor, stream=None):
         """One env step for every env. ``actions`` float32 [N, nu] in [-1, 1] (clipped)."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        # float32, or float64: the reference's np.clip keeps a float64 policy's dtype, so ctrl and the
+        # action terms of the reward follow in float64 (include/mgx.h action_f64)
+        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
+        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
+            actions = actions.to(device=self.device, dtype=dt).contiguous()
+        self._env.action_f64 = 1 if dt == torch.float64 else 0
         assert actions.shape == (self.num_envs, self.model.nu), actions.shape
         check(lib().mgx_martial_step(self.native.handle, C.byref(self.batch.state), C.byref(self._env),
                                      _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
@@ -203,7 +217,7 @@ class HumanoidMartialArtsEnv(EnvBase):
         return obs[0].cpu().numpy().copy(), self._info()
 
     def step(self, action: np.ndarray):
-        a = torch.from_numpy(np.asarray(action, dtype=np.float32).reshape(1, -1)).to(self._vec.device)
+        a = torch.from_numpy(policy_action(action).reshape(1, -1)).to(self._vec.device)
         obs, rew, term, trunc, _ = self._vec.step(a)
         torch.cuda.synchronize(self._vec.device)
         self.current_step = int(self._vec.ints[0, 0])

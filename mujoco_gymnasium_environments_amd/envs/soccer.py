@@ -48,7 +48,7 @@ REGISTERED_MAX_EPISODE_STEPS = 2500  # humanoid_soccer_env/__init__.py:21 (TimeL
 # env step. full_capacity=False keeps the round-1 capacity of 64 contacts / 192 rows and counts
 # the rare env step beyond it (mgx_state.overflow, MuJoCo's mjWARN_CONTACTFULL / CNSTRFULL
 # semantics: drop in row order); the monolithic kernel (staged=False) always holds 64 / 192
-# (Capacity).
+# (Capacity). The drop-in HumanoidSoccerEnv runs the staged step at full capacity.
 CON_CAPACITY = 96
 EFC_CAPACITY = 384
 
@@ -371,9 +371,13 @@ class HumanoidSoccerEnv(EnvBase):
         self.dt = 0.02
         self.max_episode_steps = MAX_EPISODE_STEPS
         self.render_mode = render_mode
-        # one env: the single-launch monolithic kernel has the lowest step latency
+        # one env on the staged pipeline at MuJoCo's full arena (96 contacts / 384 rows: no row is
+        # ever dropped at bench conditions, DESIGN.md §3 Capacity), reset() settled by the same
+        # stages (k_soccer_settle) from the gymnasium-seeded host draws; no reset banks (the
+        # caller resets). The monolithic kernel holds 64 / 192 and is not used here.
         self._vec = SoccerVectorEnv(1, device=device, precision=precision, autoreset=False,
-                                    max_episode_steps=self.max_episode_steps, staged=False)
+                                    max_episode_steps=self.max_episode_steps, staged=True, banks=0,
+                                    full_capacity=True)
         self.model = self._vec.model
         self.num_joints = self.model.nu
         self.action_space = Box(low=-150.0, high=150.0, shape=(self.num_joints,), dtype=np.float32)

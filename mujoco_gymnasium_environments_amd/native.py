@@ -97,6 +97,7 @@ _SIGS = {
     "mgx_model_destroy": ([_VP], C.c_int),
     "mgx_model_get_info": ([_VP, C.POINTER(cabi.MgxModelInfo)], C.c_int),
     "mgx_last_error": ([], C.c_char_p),
+    "mgx_abi_version": ([], C.c_int),
     "mgx_step": ([_VP, C.POINTER(cabi.MgxState), C.POINTER(cabi.MgxFrames), C.c_int, C.c_int, _VP, _VP], C.c_int),
     "mgx_reset_data": ([_VP, C.POINTER(cabi.MgxState), C.c_int, _VP, _VP], C.c_int),
     "mgx_debug_forward": ([_VP, C.POINTER(cabi.MgxState), C.c_int, _VP, _VP], C.c_int),
@@ -173,6 +174,9 @@ def lib() -> C.CDLL:
             f = getattr(L, name)
             f.argtypes = argt
             f.restype = rest
+        if L.mgx_abi_version() != cabi.MGX_ABI_VERSION:
+            raise NativeError(f"{LIB_PATH}: ABI version {L.mgx_abi_version()}, the bindings expect "
+                              f"{cabi.MGX_ABI_VERSION} (include/mgx.h): rebuild")
         _lib = L
     return _lib
 

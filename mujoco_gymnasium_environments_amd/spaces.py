@@ -52,3 +52,13 @@ except Exception:  # noqa: BLE001
         @property
         def unwrapped(self):
             return self
+
+
+def policy_action(action) -> np.ndarray:
+    """A policy's action as the reference's np.clip against float32 bounds would type it: float32
+    when numpy promotes the action with float32 to float32 (float32 / float16 arrays), float64
+    otherwise (float64 arrays, Python lists of floats, integer arrays). Contiguous, unclipped: the
+    device kernels clip in that dtype."""
+    a = np.asarray(action)
+    dt = np.float64 if np.result_type(a.dtype, np.float32) == np.float64 else np.float32
+    return np.ascontiguousarray(a, dtype=dt)

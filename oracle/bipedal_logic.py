@@ -57,6 +57,13 @@ class BipedalTables:
         return np.array(d)
 
 
+def _policy(action):
+    """The action as the reference's np.clip against float32 bounds types it: float32 stays float32,
+    float64 (and anything numpy promotes with float32 to float64) stays float64."""
+    a = np.asarray(action)
+    return a.astype(np.result_type(a.dtype, np.float32), copy=False)
+
+
 def quat2mat(q):
     w, x, y, z = np.asarray(q, dtype=np.float64)
     return np.array([[w*w + x*x - y*y - z*z, 2*(x*y - w*z), 2*(x*z + w*y)],
@@ -94,11 +101,14 @@ class BipedalLogic:
         s["prev_robot_pos"] = s["xpos"][self.t.torso].copy()
 
     def pre(self, s, action):
-        a = np.clip(np.asarray(action, np.float32), np.float32(-100.0), np.float32(100.0))
+        # the float32 action_space bounds keep the action's dtype (rescue_env.py:420); the cost, and
+        # current_energy / energy_used with it, follow numpy's promotion: a Python float (after reset)
+        # or np.float32 minus a float32 cost is float32, anything with a float64 operand float64
+        a = np.clip(_policy(action), np.float32(-100.0), np.float32(100.0))
         s["ctrl"][:len(a)] = a
-        cost = np.sum(np.abs(a)) * np.float32(0.001)
-        s["energy"] = np.float32(s["energy"]) - cost
-        s["stats"]["energy_used"] = np.float32(s["stats"]["energy_used"]) + cost
+        cost = np.sum(np.abs(a)) * 0.001
+        s["energy"] = s["energy"] - cost
+        s["stats"]["energy_used"] = s["stats"]["energy_used"] + cost
         return a
 
     def _robot(self, s):
@@ -145,7 +155,7 @@ class BipedalLogic:
             v = self._victim(s, i)
             o += [v[0], v[1], 1.0 if i in s["rescued"] else 0.0, 1.0 if i in s["carried"] else 0.0]
         o += list(SAFE_ZONE - robot)
-        o.append(np.float32(s["energy"]) / np.float32(ENERGY_LIMIT))
+        o.append(s["energy"] / ENERGY_LIMIT)  # in current_energy's numpy type (:586)
         o.append(1.0 - (s["step"] / self.max_episode_steps))
         o += [len(s["carried"]), len(s["rescued"])]
         for fp, _ in FIRES:
@@ -183,7 +193,7 @@ class BipedalLogic:
         else:
             r += -500.0
             s["stats"]["falls"] += 1
-        usage = np.sum(np.abs(np.asarray(action, np.float32))) * np.float32(0.001)
+        usage = np.sum(np.abs(action)) * 0.001  # the clipped action's dtype (:650)
         if usage < 0.5:
             r += 10.0
         for fp, rad in FIRES:

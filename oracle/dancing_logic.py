@@ -28,6 +28,13 @@ OBS_DIM = 94
 SEQ_LEN = 20
 
 
+def _policy(action):
+    """The action as the reference's np.clip against float32 bounds types it: float32 stays float32,
+    float64 (and anything numpy promotes with float32 to float64) stays float64."""
+    a = np.asarray(action)
+    return a.astype(np.result_type(a.dtype, np.float32), copy=False)
+
+
 class DancingTables:
     def __init__(self, m):
         self.model = m
@@ -78,7 +85,7 @@ class DancingLogic:
 
     # ---------------------------------------------------------------- pre-physics
     def pre(self, s, action):
-        a = np.clip(np.asarray(action, np.float32), np.float32(-200.0), np.float32(200.0))
+        a = np.clip(_policy(action), np.float32(-200.0), np.float32(200.0))  # float32 bounds: dtype kept
         s["ctrl"][:] = a
         s["t_beat"] += DT
         if s["t_beat"] >= BEAT:
@@ -174,7 +181,7 @@ class DancingLogic:
                     used += abs(s["qpos"][7 + i] - (lo + hi) / 2) / (hi - lo)
         if used > 5.0:
             r += 100.0 * 0.1
-        r += -0.05 * np.sum(np.square(np.asarray(action, np.float32)))
+        r += -0.05 * np.sum(np.square(action))  # the clipped action's dtype (:1186-1187)
         if not up:
             r += -500.0
             s["combo"] = 1.0

@@ -31,6 +31,13 @@ ACTION_LIMITS = np.array([80.0, 80.0, 60.0, 40.0] * 4, dtype=np.float32)  # park
 OBS_DIM = 95
 
 
+def _policy(action):
+    """The action as the reference's np.clip against float32 bounds types it: float32 stays float32,
+    float64 (and anything numpy promotes with float32 to float64) stays float64."""
+    a = np.asarray(action)
+    return a.astype(np.result_type(a.dtype, np.float32), copy=False)
+
+
 class ParkourTables:
     """Index tables looked up exactly as parkour_env.py:180-222 / :757-795 do."""
 
@@ -68,7 +75,7 @@ class ParkourLogic:
 
     # ----- pre-physics (parkour_env.py:359-364)
     def pre(self, s, action):
-        action = np.clip(np.asarray(action, np.float32), -ACTION_LIMITS, ACTION_LIMITS)
+        action = np.clip(_policy(action), -ACTION_LIMITS, ACTION_LIMITS)  # float32 bounds: dtype kept
         s["ctrl"][:self.t.n_leg] = action
         return action
 
@@ -144,9 +151,13 @@ class ParkourLogic:
         n = np.sum(self.foot_contacts(s))
         if 1 <= n <= 3:
             r += 200.0
-        effort = np.sum(np.abs(np.asarray(action, np.float32)))
-        f32 = not progress > 0
-        r = np.float32(r) - effort * np.float32(0.1) if f32 else r - float(effort * np.float32(0.1))
+        effort = np.sum(np.abs(action))  # the clipped action's dtype (parkour_env.py:702-703)
+        if effort.dtype == np.float64:  # a float64 action: the reward is np.float64 from here on
+            f32 = False
+            r = r - effort * 0.1
+        else:
+            f32 = not progress > 0
+            r = np.float32(r) - effort * np.float32(0.1) if f32 else r - float(effort * np.float32(0.1))
         c = np.float32 if f32 else float
         if pos[2] < 0.2:
             r -= c(2000.0)

@@ -50,6 +50,9 @@ class _Box:
         self.dtype = dtype
 
 
+# dtype of the synthetic policy actions fed to the reference step() (main_f64: float64)
+ACTION_DTYPE = np.float32
+
 def _np_random(seed=None):
     ss = np.random.SeedSequence(seed)
     return np.random.Generator(np.random.PCG64(ss)), ss.entropy
@@ -321,7 +324,7 @@ def soccer_envlogic_vectors(env, n, seed=1234, max_contacts=12):
         d.xfrc_applied[ball, :2] = rng.normal(size=2)
         qfrc_in = d.qfrc_applied[0]
         xfrc_in = d.xfrc_applied[ball, :2].copy()
-        action = rng.uniform(-200, 200, c.nu).astype(np.float32)
+        action = rng.uniform(-200, 200, c.nu).astype(ACTION_DTYPE)
         action = np.clip(action, env.action_space.low, env.action_space.high)
         # the episode stats entering this step; _calculate_reward advances goals / contacts /
         # time_upright on them (soccer_env.py:640-662)
@@ -458,7 +461,7 @@ def parkour_envlogic_vectors(env, n, seed=4321, max_contacts=14):
                    reached_in=mask, fall_count_in=env.fall_count, stuck_in=env.stuck_counter,
                    step_count_in=env.step_count, episode_reward_in=env.episode_reward)
         lim = env.action_space.high
-        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim).astype(np.float32)
+        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim).astype(ACTION_DTYPE)
         obs, reward, term, trunc, info = env.step(action)
         reached = sum(1 << b for b, k in enumerate(keys) if k in env.checkpoints_reached)
         out = dict(action=action, obs=obs, reward=float(reward), terminated=bool(term), truncated=bool(trunc),
@@ -578,7 +581,7 @@ def bipedal_envlogic_vectors(env, n, seed=777, max_contacts=24):
                                       es["falls"], es["collisions"]], dtype=np.float64),
                    prev_robot_pos_in=env.prev_robot_pos.copy())
         lim = env.action_space.high
-        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim * rng.choice([1.0, 0.01])).astype(np.float32)
+        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim * rng.choice([1.0, 0.01])).astype(ACTION_DTYPE)
         with contextlib.redirect_stdout(io.StringIO()):
             obs, reward, term, trunc, info = env.step(action)
         es = env.episode_stats
@@ -714,7 +717,7 @@ def dancing_envlogic_vectors(env, n, seed=999, max_contacts=16):
                    moves=np.array([MOVES.index(x['move']) for x in env.dance_sequence], dtype=np.int64),
                    durations=np.array([x['duration'] for x in env.dance_sequence]))
         lim = env.action_space.high
-        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim * rng.choice([1.0, 0.01, 0.1])).astype(np.float32)
+        action = (rng.uniform(-1.3, 1.3, len(lim)) * lim * rng.choice([1.0, 0.01, 0.1])).astype(ACTION_DTYPE)
         obs, reward, term, trunc, info = env.step(action)
         out = {k + "_out": v for k, v in _dance_state(env).items()}
         out.update(action=action, obs=obs, reward=float(reward), reward_is_f64=isinstance(reward, np.float64),
@@ -807,7 +810,7 @@ def martial_envlogic_vectors(env, n, seed=2468):
             env.prev_torso_pos = prev.copy()
         elif hasattr(env, "prev_torso_pos"):
             del env.prev_torso_pos
-        action = rng.uniform(-1.5, 1.5, nu).astype(np.float32)
+        action = rng.uniform(-1.5, 1.5, nu).astype(ACTION_DTYPE)
         stance_in, stats_in, step_in = env.stance_stability_time, [env.episode_stats[k] for k in keys], env.current_step
         obs, reward, term, trunc, info = env.step(action)
         vals = dict(qpos=d.qpos.copy(), qvel=d.qvel.copy(), xpos=xpos, xquat=d.xquat.copy(), cvel=d.cvel.copy(),
@@ -1024,7 +1027,7 @@ def assembly_envlogic_vectors(env, n, seed=8642, max_contacts=12):
             st[seq.index(held_in)] = 'held'
         env.component_status = dict(zip(seq, st))
         env.cumulative_reward = float(rng.choice([0.0, rng.normal(scale=1e4)]))
-        action = (rng.uniform(-3, 3, 9) * np.array([1] * 7 + [50, 30])).astype(np.float32)
+        action = (rng.uniform(-3, 3, 9) * np.array([1] * 7 + [50, 30])).astype(ACTION_DTYPE)
         snap = dict(qpos=d.qpos.copy(), qvel=d.qvel.copy(), xpos=d.xpos.copy(), xquat=d.xquat.copy(),
                     site_xpos=d.site_xpos.copy(), ncon=len(cons),
                     con_geom=_pad(np.array([[cn.geom1, cn.geom2] for cn in cons], np.int64).reshape(-1, 2),
@@ -1130,7 +1133,7 @@ def construction_envlogic_vectors(env, n, seed=1357):
         st['total_reward'] = float(rng.choice([0.0, rng.normal(scale=1e4)]))
         env.episode_stats = st
         scale = rng.choice([1.0, 150.0, 400.0])
-        action = rng.uniform(-scale, scale, c.nu).astype(np.float32)
+        action = rng.uniform(-scale, scale, c.nu).astype(ACTION_DTYPE)
         snap = dict(qpos=d.qpos.copy(), qvel=d.qvel.copy(), torso_z=z, task=task, blocks=env.blocks_placed,
                     violations=env.safety_violations,
                     weather=[env.wind_strength, env.rain_intensity, env.temperature], step_in=env.current_step,
@@ -1159,6 +1162,25 @@ def main_dancing():
     denv = dancing_env()
     np.savez_compressed(f"{HERE}/dancing_reset.npz", **dancing_reset_vectors(denv, list(range(0, 40)) + [777]))
     np.savez_compressed(f"{HERE}/dancing_envlogic.npz", **dancing_envlogic_vectors(denv, 600))
+
+
+def main_f64(n=200):
+    """The env-logic vectors with float64 actions (the same synthetic states, actions not rounded to
+    float32): the reference's np.clip keeps a float64 policy's dtype, so ctrl, the action terms of
+    the reward and the numpy types downstream follow in float64 (<task>_envlogic_f64.npz)."""
+    global ACTION_DTYPE
+    install_stubs()
+    ACTION_DTYPE = np.float64
+    np.savez_compressed(f"{HERE}/soccer_envlogic_f64.npz", **soccer_envlogic_vectors(soccer_env(), n))
+    np.savez_compressed(f"{HERE}/parkour_envlogic_f64.npz", **parkour_envlogic_vectors(parkour_env(), n))
+    np.savez_compressed(f"{HERE}/bipedal_envlogic_f64.npz", **bipedal_envlogic_vectors(bipedal_env(), n))
+    np.savez_compressed(f"{HERE}/dancing_envlogic_f64.npz", **dancing_envlogic_vectors(dancing_env(), n))
+    np.savez_compressed(f"{HERE}/martial_envlogic_f64.npz", **martial_envlogic_vectors(martial_env()[0], n))
+    np.savez_compressed(f"{HERE}/assembly_envlogic_f64.npz", **assembly_envlogic_vectors(assembly_env(), n))
+    np.savez_compressed(f"{HERE}/construction_envlogic_f64.npz",
+                        **construction_envlogic_vectors(construction_env(), n))
+    ACTION_DTYPE = np.float32
+    print("float64-action fixtures written to", HERE)
 
 
 def main():
@@ -1191,6 +1213,8 @@ if __name__ == "__main__":
         main_assembly()
     elif len(sys.argv) > 1 and sys.argv[1] == "construction":
         main_construction()
+    elif len(sys.argv) > 1 and sys.argv[1] == "f64":
+        main_f64()
     elif len(sys.argv) > 1 and sys.argv[1] == "soccer":
         install_stubs()
         np.savez_compressed(f"{HERE}/soccer_envlogic.npz", **soccer_envlogic_vectors(soccer_env(), 400))

@@ -30,12 +30,14 @@ def _venv(n, precision="f64", autoreset=False):
     return AssemblyVectorEnv(n, precision=precision, autoreset=autoreset)
 
 
-def test_logic_matches_reference_vectors(golden):
+@pytest.mark.parametrize("act64", [False, True], ids=["float32_actions", "float64_actions"])
+def test_logic_matches_reference_vectors(golden, act64):
+    """act64: the float64-action vectors (make_fixtures.py main_f64) with mgx_assembly_env.action_f64 = 1."""
     import torch
     from mujoco_gymnasium_environments_amd import cabi
     from mujoco_gymnasium_environments_amd.batch import _ptr
     from mujoco_gymnasium_environments_amd.native import check, lib
-    g = golden
+    g = golden if not act64 else dict(np.load("tests/golden/assembly_envlogic_f64.npz"))
     N = len(g["reward"])
     v = _venv(N)
     dev = v.device
@@ -51,7 +53,8 @@ def test_logic_matches_reference_vectors(golden):
     ncon = t(g["ncon"], torch.int32)
     cgeom = t(g["con_geom"], torch.int32)
     cdist = t(g["con_dist"])
-    action = t(g["action"], torch.float32)
+    action = t(g["action"], torch.float64 if act64 else torch.float32)
+    v._env.action_f64 = 1 if act64 else 0
     ctrl = torch.zeros(N, 9, dtype=torch.float64, device=dev)
     obs = torch.zeros(N, 110, dtype=torch.float32, device=dev)
     rew = torch.zeros(N, dtype=torch.float64, device=dev)

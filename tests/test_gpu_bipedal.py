@@ -26,12 +26,16 @@ def _mask(rows):
     return np.array([sum(1 << int(v) for v in r if v >= 0) for r in rows], dtype=np.int32)
 
 
-@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("prec", ["f64", "f32", "f64_actions"])
 def test_bipedal_logic_kernel_matches_reference(bipedal_model, prec):
     from mujoco_gymnasium_environments_amd import cabi
     from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
     from mujoco_gymnasium_environments_amd.native import check, lib
-    g = dict(np.load("tests/golden/bipedal_envlogic.npz"))
+    # f64_actions: the fp64 kernel on the float64-action vectors (make_fixtures.py main_f64),
+    # mgx_bipedal_env.action_f64 = 1 — the reference keeps a float64 action float64 through np.clip
+    act64 = prec == "f64_actions"
+    prec = "f64" if act64 else prec
+    g = dict(np.load("tests/golden/bipedal_envlogic" + ("_f64" if act64 else "") + ".npz"))
     n = g["obs"].shape[0]
     env = BipedalVectorEnv(n, precision=prec, autoreset=False)
     dt = env.batch.dtype
@@ -56,7 +60,7 @@ def test_bipedal_logic_kernel_matches_reference(bipedal_model, prec):
     mc = g["con_dist"].shape[1]
     T = dict(qpos=_t(g["qpos"], dt), qvel=_t(g["qvel"], dt), xpos=_t(g["xpos"], dt), xquat=_t(g["xquat"], dt),
              ncon=_t(g["ncon"], torch.int32), con_dist=_t(g["con_dist"], dt),
-             ctrl=torch.zeros(n, bipedal_model.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float32),
+             ctrl=torch.zeros(n, bipedal_model.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float64 if act64 else torch.float32),
              obs=torch.zeros(n, 102, dtype=torch.float32, device="cuda:0"),
              reward=torch.zeros(n, dtype=torch.float64, device="cuda:0"),
              term=torch.zeros(n, dtype=torch.uint8, device="cuda:0"),
@@ -66,6 +70,7 @@ def test_bipedal_logic_kernel_matches_reference(bipedal_model, prec):
                                 T["xquat"].data_ptr(), T["ncon"].data_ptr(), T["con_dist"].data_ptr(), mc, 0,
                                 T["ctrl"].data_ptr(), T["action"].data_ptr(), T["obs"].data_ptr(),
                                 T["reward"].data_ptr(), T["term"].data_ptr(), T["trunc"].data_ptr(), T["up"].data_ptr())
+    env._env.action_f64 = 1 if act64 else 0
     check(lib().mgx_bipedal_logic_test(env.native.handle, C.byref(io), C.byref(env._env), n, None), "logic_test")
     torch.cuda.synchronize()
     obs, rew = T["obs"].cpu().numpy(), T["reward"].cpu().numpy()

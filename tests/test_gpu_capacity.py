@@ -6,12 +6,14 @@ per env; full_capacity=False keeps 192 / 64 and counts the overflow (DESIGN.md Â
 solver launch solves every slot (row scalars read from the pipe, make_staged_pipe `sqg`); the
 test hook MGX_PGS_LDS_ROWS instead gives the main launch that many LDS-scalar rows per slot and
 lists a slot with more for the wide launch (B, scalars and table in LDS, one slot per wave)
-instead of truncating it. Read per step, a low value sends ordinary bench-condition states â€”
-40..120 rows â€” through the wide launch on every step:
+instead of truncating it. The hooks are read once, when the env's model is created (mgx_model_create,
+Hooks); a low value sends ordinary bench-condition states â€” 40..120 rows â€” through the wide launch
+on every step:
   * bit-identical to the default launch (which launch solves a slot changes nothing);
   * fp64 end to end against the oracle (no cap) with every slot over the lowered threshold;
-  * MGX_MAX_NEFC below a state's rows still truncates in MuJoCo's row order and counts the step
-    in mgx_state.overflow (the documented behaviour past the storage capacity).
+  * a model whose own row capacity is below a state's rows truncates in MuJoCo's row order and
+    counts the step in mgx_state.overflow (the documented behaviour past the storage capacity);
+    MGX_MAX_NEFC can raise a model's capacity, never lower it (refused).
 """
 import os
 
@@ -44,7 +46,8 @@ def test_wide_solver_launch_bit_identical(soccer_model, prec):
     from mujoco_gymnasium_environments_amd.envs.soccer import EFC_CAPACITY, SoccerVectorEnv
     n, steps = 64, 30
     a = SoccerVectorEnv(n, precision=prec, seed=21, full_capacity=True)
-    b = SoccerVectorEnv(n, precision=prec, seed=21, full_capacity=True)
+    with _LdsRows(16):  # read when b's model is created
+        b = SoccerVectorEnv(n, precision=prec, seed=21, full_capacity=True)
     assert a.native.info.max_nefc == 192  # the monolithic layout (reset settle, debug) keeps 192
     a.reset()
     b.reset()
@@ -54,8 +57,7 @@ def test_wide_solver_launch_bit_identical(soccer_model, prec):
     for t in range(steps):
         act = torch.rand(n, soccer_model.nu, device="cuda:0", generator=g) * 300 - 150
         ra = a.step(act)
-        with _LdsRows(16):
-            rb = b.step(act)
+        rb = b.step(act)
         torch.cuda.synchronize()
         for x, y, name in zip(ra[:4], rb[:4], ("obs", "reward", "terminated", "truncated")):
             assert torch.equal(x, y), (t, name)
@@ -90,7 +92,8 @@ def test_lds_arena_solver_bit_identical(soccer_model, prec):
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
     n, steps = 64, 25
     a = SoccerVectorEnv(n, precision=prec, seed=33)
-    b = SoccerVectorEnv(n, precision=prec, seed=33)
+    with _Env(MGX_PGS_LDS_B="1", MGX_PGS_ARENA="24576"):  # read when b's model is created
+        b = SoccerVectorEnv(n, precision=prec, seed=33)
     a.reset()
     b.reset()
     g = torch.Generator(device="cuda:0")
@@ -98,8 +101,7 @@ def test_lds_arena_solver_bit_identical(soccer_model, prec):
     for t in range(steps):
         act = torch.rand(n, soccer_model.nu, device="cuda:0", generator=g) * 300 - 150
         ra = a.step(act)
-        with _Env(MGX_PGS_LDS_B="1", MGX_PGS_ARENA="24576"):
-            rb = b.step(act)
+        rb = b.step(act)
         torch.cuda.synchronize()
         for x, y, name in zip(ra[:4], rb[:4], ("obs", "reward", "terminated", "truncated")):
             assert torch.equal(x, y), (t, name)
@@ -113,7 +115,8 @@ def test_rows_over_main_launch_match_oracle(soccer_model, soccer_packed):
     from mujoco_gymnasium_environments_amd.seeding import np_random
     m = soccer_model
     n = 4
-    env = SoccerVectorEnv(n, precision="f64", autoreset=False, full_capacity=True)
+    with _LdsRows(8):  # read when the env's model is created
+        env = SoccerVectorEnv(n, precision="f64", autoreset=False, full_capacity=True)
     draws = np.stack([env.tables.reset_draws(np_random(100 + i)[0]) for i in range(n)])
     env.reset(draws=draws)
     torch.cuda.synchronize()
@@ -126,8 +129,7 @@ def test_rows_over_main_launch_match_oracle(soccer_model, soccer_packed):
     over = 0
     for t in range(25):
         act = rng.uniform(-20, 20, (n, m.nu)).astype(np.float32)
-        with _LdsRows(8):
-            obs, rew, term, _, _ = env.step(torch.from_numpy(act).cuda())
+        obs, rew, term, _, _ = env.step(torch.from_numpy(act).cuda())
         torch.cuda.synchronize()
         og, rg, tg = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
         for i, (sim, L, s) in enumerate(oracles):
@@ -144,11 +146,22 @@ def test_rows_over_main_launch_match_oracle(soccer_model, soccer_packed):
 
 
 def test_storage_capacity_truncates_and_counts(soccer_model, monkeypatch):
-    """Past the storage capacity (here MGX_MAX_NEFC = 40) rows are dropped in MuJoCo's order
-    and the step is counted in mgx_state.overflow; below it nothing is counted."""
+    """Past the storage capacity (here a model whose own row capacity is 40) rows are dropped in
+    MuJoCo's order and the step is counted in mgx_state.overflow; below it nothing is counted.
+    MGX_MAX_NEFC below a model's capacity is refused at model creation."""
+    import copy
+
+    from mujoco_gymnasium_environments_amd.envs import soccer as soccer_mod
     from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    from mujoco_gymnasium_environments_amd.native import NativeError
+    m40 = copy.deepcopy(soccer_model)
+    m40.efc_capacity = 40
+    monkeypatch.setattr(soccer_mod, "soccer_model", lambda full_capacity=False: m40)
+    small = SoccerVectorEnv(32, precision="f64", seed=3, full_capacity=False)
+    monkeypatch.undo()
     monkeypatch.setenv("MGX_MAX_NEFC", "40")
-    small = SoccerVectorEnv(32, precision="f64", seed=3)
+    with pytest.raises(NativeError, match="MGX_MAX_NEFC below"):
+        SoccerVectorEnv(2, precision="f64", seed=3)
     monkeypatch.delenv("MGX_MAX_NEFC")
     full = SoccerVectorEnv(32, precision="f64", seed=3, full_capacity=True)
     small.reset()

@@ -41,12 +41,16 @@ def cpacked(cmodel):
     return cabi.pack_model(cmodel)
 
 
-@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("prec", ["f64", "f32", "f64_actions"])
 def test_construction_logic_kernel_matches_reference(cmodel, prec):
     from mujoco_gymnasium_environments_amd import cabi
     from mujoco_gymnasium_environments_amd.envs.construction import ConstructionVectorEnv
     from mujoco_gymnasium_environments_amd.native import check, lib
-    g = dict(np.load("tests/golden/construction_envlogic.npz"))
+    # f64_actions: the fp64 kernel on the float64-action vectors (make_fixtures.py main_f64),
+    # mgx_construction_env.action_f64 = 1 — the reference keeps a float64 action float64 through np.clip
+    act64 = prec == "f64_actions"
+    prec = "f64" if act64 else prec
+    g = dict(np.load("tests/golden/construction_envlogic" + ("_f64" if act64 else "") + ".npz"))
     n = g["obs"].shape[0]
     m = cmodel
     env = ConstructionVectorEnv(n, precision=prec, autoreset=False)
@@ -59,13 +63,14 @@ def test_construction_logic_kernel_matches_reference(cmodel, prec):
     xpos = np.zeros((n, m.nbody, 3))
     xpos[:, hid, 2] = g["torso_z"]
     T = dict(qpos=_t(g["qpos"], dt), qvel=_t(g["qvel"], dt), xpos=_t(xpos, dt),
-             ctrl=torch.zeros(n, m.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float32),
+             ctrl=torch.zeros(n, m.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float64 if act64 else torch.float32),
              obs=torch.zeros(n, 135, dtype=torch.float32, device="cuda:0"),
              reward=torch.zeros(n, dtype=torch.float64, device="cuda:0"),
              term=torch.zeros(n, dtype=torch.uint8, device="cuda:0"),
              trunc=torch.zeros(n, dtype=torch.uint8, device="cuda:0"))
     io = cabi.MgxConstructionLogicIO(*[T[k].data_ptr() for k in ("qpos", "qvel", "xpos", "ctrl", "action", "obs",
                                                                   "reward", "term", "trunc")])
+    env._env.action_f64 = 1 if act64 else 0
     check(lib().mgx_construction_logic_test(env.native.handle, C.byref(io), C.byref(env._env), n, None), "logic")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(T["term"].cpu().numpy().astype(bool), g["terminated"])

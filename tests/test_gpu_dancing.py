@@ -28,12 +28,16 @@ def _t(x, dtype, dev="cuda:0"):
     return torch.as_tensor(np.ascontiguousarray(x)).to(device=dev, dtype=dtype).contiguous()
 
 
-@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("prec", ["f64", "f32", "f64_actions"])
 def test_dancing_logic_kernel_matches_reference(dancing_model, prec):
     from mujoco_gymnasium_environments_amd import cabi
     from mujoco_gymnasium_environments_amd.envs.dancing import DancingVectorEnv
     from mujoco_gymnasium_environments_amd.native import check, lib
-    g = dict(np.load("tests/golden/dancing_envlogic.npz"))
+    # f64_actions: the fp64 kernel on the float64-action vectors (make_fixtures.py main_f64),
+    # mgx_dancing_env.action_f64 = 1 — the reference keeps a float64 action float64 through np.clip
+    act64 = prec == "f64_actions"
+    prec = "f64" if act64 else prec
+    g = dict(np.load("tests/golden/dancing_envlogic" + ("_f64" if act64 else "") + ".npz"))
     n = g["obs"].shape[0]
     env = DancingVectorEnv(n, precision=prec, autoreset=False)
     dt = env.batch.dtype
@@ -54,7 +58,7 @@ def test_dancing_logic_kernel_matches_reference(dancing_model, prec):
     T = dict(qpos=_t(g["qpos"], dt), qvel=_t(g["qvel"], dt), xpos=_t(g["xpos"], dt), xquat=_t(g["xquat"], dt),
              sc=_t(g["subtree_com"], dt), ncon=_t(g["ncon"], torch.int32),
              con_geom=_t(np.maximum(g["con_geom"], -1), torch.int32),
-             ctrl=torch.zeros(n, dancing_model.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float32),
+             ctrl=torch.zeros(n, dancing_model.nu, dtype=dt, device="cuda:0"), action=_t(g["action"], torch.float64 if act64 else torch.float32),
              obs=torch.zeros(n, 94, dtype=torch.float32, device="cuda:0"),
              reward=torch.zeros(n, dtype=torch.float64, device="cuda:0"),
              term=torch.zeros(n, dtype=torch.uint8, device="cuda:0"),
@@ -63,6 +67,7 @@ def test_dancing_logic_kernel_matches_reference(dancing_model, prec):
                                 T["xquat"].data_ptr(), T["sc"].data_ptr(), T["ncon"].data_ptr(),
                                 T["con_geom"].data_ptr(), mc, 0, T["ctrl"].data_ptr(), T["action"].data_ptr(),
                                 T["obs"].data_ptr(), T["reward"].data_ptr(), T["term"].data_ptr(), T["trunc"].data_ptr())
+    env._env.action_f64 = 1 if act64 else 0
     check(lib().mgx_dancing_logic_test(env.native.handle, C.byref(io), C.byref(env._env), n, None), "logic_test")
     torch.cuda.synchronize()
     obs, rew = T["obs"].cpu().numpy(), T["reward"].cpu().numpy()

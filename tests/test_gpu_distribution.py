@@ -1,0 +1,144 @@
+"""GPU: distribution parity with the CPU oracle at bench conditions (soccer, parkour, bipedal).
+
+At the bench's action ranges the unconverged 50-sweep PGS amplifies fp64 rounding, so the device
+and the oracle (like any two fp64 implementations of mj_step) follow the same trajectory for
+3..25 steps only (tests/test_gpu_*::*_bench_actions). Past that horizon the claim to
+check is statistical: the device's termination, truncation, episode and bad-state (MuJoCo's
+auto-reset, mj_checkPos / checkVel / checkAcc) rates and its mean reward are the oracle's.
+
+Setup per task: n envs, each with its own gymnasium-seeded reset stream (np_random(seed + e)) and
+its own action stream at the bench's distribution; the device VectorEnv (fp64, autoreset off) and
+the oracle (oracle/envs.py, in a process pool) step the same per-env streams, and each side resets
+an env with the next draws of that env's stream when its episode ends — so both start every env's
+k-th episode from the same draws, and an env pair differs only by where its trajectories separate.
+The test is paired over envs: for each rate, d_e = device_e - oracle_e per env, and
+|mean(d)| <= 4 std(d) / sqrt(n) + a small floor (a 4-sigma CLT bound over independent envs; bad
+states cluster inside an env, which the per-env pairing absorbs).
+"""
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+TASKS = {
+    # task: (envs, env steps per env); the oracle side runs in 8 processes (~10-20 s per task)
+    "soccer": (128, 200),
+    "parkour": (128, 200),
+    "bipedal": (64, 100),
+}
+
+
+def _acts(task, e, steps, nu):
+    rng = np.random.default_rng(50_000 + e)
+    if task == "soccer":
+        return rng.uniform(-150, 150, (steps, nu)).astype(np.float32)
+    if task == "parkour":
+        from mujoco_gymnasium_environments_amd.envs.parkour import action_limits
+        return (rng.uniform(-1, 1, (steps, 16)) * action_limits()).astype(np.float32)
+    return rng.uniform(-100, 100, (steps, 26)).astype(np.float32)
+
+
+def _setup(task):
+    from oracle.envs import task_setup
+    return task_setup(task)
+
+
+def _oracle_rollout(args):
+    """One env on the oracle: per-env counts over `steps` env steps with autoreset."""
+    task, e, steps, seed = args
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.envs import ORACLES
+    packed, tb, draws_fn, _ = _setup(task)
+    rng = np_random(seed + e)[0]
+    acts = _acts(task, e, steps, packed.model.nu)
+    env = ORACLES[task](packed, tb)
+    env.reset(draws_fn(rng))
+    st = dict(term=0, trunc=0, eps=0, bad=0, rsum=0.0, rn=0)
+    for k in range(steps):
+        _, r, te, tr = env.step(acts[k])
+        if np.isfinite(r):
+            st["rsum"] += r
+            st["rn"] += 1
+        if te or tr:
+            st["term"] += te
+            st["trunc"] += tr
+            st["eps"] += 1
+            env.reset(draws_fn(rng))
+    st["bad"] = env.bad_states
+    return st
+
+
+def _device_rollout(task, n, steps, seed):
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    packed, _, draws_fn, _ = _setup(task)
+    if task == "soccer":
+        from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv as V
+    elif task == "parkour":
+        from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv as V
+    else:
+        from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv as V
+    env = V(n, precision="f64", autoreset=False)
+    rngs = [np_random(seed + e)[0] for e in range(n)]
+    draws = np.stack([draws_fn(r) for r in rngs])
+    env.reset(draws=draws)
+    acts = np.stack([_acts(task, e, steps, packed.model.nu) for e in range(n)], axis=1)  # [steps, n, nu]
+    acts_d = torch.from_numpy(acts).cuda()
+    st = {k: np.zeros(n) for k in ("term", "trunc", "eps", "rsum", "rn")}
+    w0 = env.batch.warning.cpu().numpy().astype(np.int64)
+    for k in range(steps):
+        _, rew, term, trunc, _ = env.step(acts_d[k])
+        r, te, tr = rew.cpu().numpy(), term.cpu().numpy().astype(bool), trunc.cpu().numpy().astype(bool)
+        fin = np.isfinite(r)
+        st["rsum"] += np.where(fin, r, 0.0)
+        st["rn"] += fin
+        st["term"] += te
+        st["trunc"] += tr
+        done = te | tr
+        st["eps"] += done
+        if done.any():
+            nd = np.zeros_like(draws)
+            for e in np.nonzero(done)[0]:
+                nd[e] = draws_fn(rngs[e])
+            env.reset(env_mask=torch.from_numpy(done.astype(np.uint8)).cuda(), draws=nd)
+    torch.cuda.synchronize()
+    st["bad"] = env.batch.warning.cpu().numpy().astype(np.int64) - w0
+    assert int(env.batch.overflow.sum()) == 0, "rows beyond the capacity"
+    return st
+
+
+def _paired(name, dev, ora, n, floor):
+    d = dev - ora
+    mean, sd = float(d.mean()), float(d.std(ddof=1)) if n > 1 else 0.0
+    bound = 4 * sd / np.sqrt(n) + floor
+    return name, float(dev.mean()), float(ora.mean()), mean, bound, abs(mean) <= bound
+
+
+@pytest.mark.parametrize("task", list(TASKS))
+def test_distribution_matches_oracle_at_bench_conditions(task):
+    n, steps = TASKS[task]
+    seed = 7000
+    with mp.get_context("spawn").Pool(min(8, os.cpu_count() or 1)) as pool:
+        ores = pool.map_async(_oracle_rollout, [(task, e, steps, seed) for e in range(n)])
+        dev = _device_rollout(task, n, steps, seed)
+        ora = ores.get(timeout=110)
+    ora = {k: np.array([o[k] for o in ora], dtype=np.float64) for k in ora[0]}
+    rows = [
+        _paired("termination rate", dev["term"] / steps, ora["term"] / steps, n, 0.002),
+        _paired("truncation rate", dev["trunc"] / steps, ora["trunc"] / steps, n, 0.002),
+        _paired("episode rate (1 / mean length)", dev["eps"] / steps, ora["eps"] / steps, n, 0.002),
+        _paired("bad-state rate", dev["bad"] / steps, ora["bad"] / steps, n, 0.002),
+        _paired("mean reward", dev["rsum"] / np.maximum(dev["rn"], 1), ora["rsum"] / np.maximum(ora["rn"], 1), n,
+                1e-3),
+    ]
+    print(f"\n{task}: {n} envs x {steps} steps, device fp64 vs oracle (mean device, mean oracle, "
+          f"paired diff, 4-sigma bound)")
+    for name, a, b, d, bound, ok in rows:
+        print(f"  {name:32s} {a:12.5g} {b:12.5g} {d:+11.4g} {bound:10.4g} {'ok' if ok else 'FAIL'}")
+    bad = [r[0] for r in rows if not r[5]]
+    assert not bad, f"{task}: {bad} differ beyond the paired 4-sigma bound"

@@ -85,13 +85,15 @@ def test_mixed_streams_equal_sequential(layout, monkeypatch):
     """layout "bench": bench.py's default (4 grouped streams, construction's at high priority, no
     side streams); "stream_per_task": 7 streams, the staged tasks' side streams on."""
     import bench
-    # side streams on for the sequential run; bench.mixed_streams turns them off for the bench
-    # layout (monkeypatch restores the variable after the test)
+    # side streams on for the sequential run; bench.mixed_side_streams turns them off for the
+    # bench layout (monkeypatch restores the variable after the test)
     monkeypatch.setenv("MGX_SIDE_STREAM", "1")
     make, acts = _tasks()
     seq = _run(make(), acts)
+    nstreams = 4 if layout == "bench" else 7
+    bench.mixed_side_streams(7, nstreams)  # read when the models are created
     envs = make()
-    streams = bench.mixed_streams(list(envs), 4 if layout == "bench" else len(envs), 1, torch.device("cuda:0"))
+    streams = bench.mixed_streams(list(envs), nstreams, 1, torch.device("cuda:0"))
     con = _run(envs, acts, streams)
     for k in seq:
         for t in range(STEPS):

@@ -20,12 +20,16 @@ def _t(x, dtype, dev="cuda:0"):
     return torch.as_tensor(np.ascontiguousarray(x)).to(device=dev, dtype=dtype).contiguous()
 
 
-@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("prec", ["f64", "f32", "f64_actions"])
 def test_parkour_logic_kernel_matches_reference(parkour_model, prec):
     from mujoco_gymnasium_environments_amd import cabi
     from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv
     from mujoco_gymnasium_environments_amd.native import check, lib
-    g = dict(np.load("tests/golden/parkour_envlogic.npz"))
+    # f64_actions: the fp64 kernel on the float64-action vectors (make_fixtures.py main_f64),
+    # mgx_parkour_env.action_f64 = 1 — the reference keeps a float64 action float64 through np.clip
+    act64 = prec == "f64_actions"
+    prec = "f64" if act64 else prec
+    g = dict(np.load("tests/golden/parkour_envlogic" + ("_f64" if act64 else "") + ".npz"))
     n = g["obs"].shape[0]
     env = ParkourVectorEnv(n, precision=prec, autoreset=False)
     dt = env.batch.dtype
@@ -40,7 +44,7 @@ def test_parkour_logic_kernel_matches_reference(parkour_model, prec):
     env.step_count.copy_(_t(g["step_count_in"], torch.int32))
     T = dict(qpos=_t(g["qpos"], dt), qvel=_t(g["qvel"], dt), xpos=_t(g["xpos"], dt),
              ncon=_t(g["ncon"], torch.int32), con_geom=_t(np.maximum(g["con_geom"], -1), torch.int32),
-             ctrl=_t(g["ctrl_in"], dt), action=_t(g["action"], torch.float32),
+             ctrl=_t(g["ctrl_in"], dt), action=_t(g["action"], torch.float64 if act64 else torch.float32),
              obs=torch.zeros(n, 95, dtype=torch.float32, device="cuda:0"),
              reward=torch.zeros(n, dtype=torch.float64, device="cuda:0"),
              term=torch.zeros(n, dtype=torch.uint8, device="cuda:0"),
@@ -49,6 +53,7 @@ def test_parkour_logic_kernel_matches_reference(parkour_model, prec):
                                 T["ncon"].data_ptr(), T["con_geom"].data_ptr(), mc, 0, T["ctrl"].data_ptr(),
                                 T["action"].data_ptr(), T["obs"].data_ptr(), T["reward"].data_ptr(),
                                 T["term"].data_ptr(), T["trunc"].data_ptr())
+    env._env.action_f64 = 1 if act64 else 0
     check(lib().mgx_parkour_logic_test(env.native.handle, C.byref(io), C.byref(env._env), n, None), "logic_test")
     torch.cuda.synchronize()
     obs, rew = T["obs"].cpu().numpy(), T["reward"].cpu().numpy()

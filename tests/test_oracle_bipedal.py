@@ -24,6 +24,13 @@ def golden():
     return dict(np.load(G + "bipedal_envlogic.npz"))
 
 
+@pytest.fixture(scope="module", params=["", "_f64"], ids=["float32_actions", "float64_actions"])
+def golden_any(request):
+    """The env-logic vectors with float32 actions, and the same states with float64 actions
+    (make_fixtures.py main_f64: the reference keeps a float64 action float64 through np.clip)."""
+    return dict(np.load(G + "bipedal_envlogic" + request.param + ".npz"))
+
+
 def _ids(row):
     return [int(x) for x in row if x >= 0]
 
@@ -62,7 +69,9 @@ def test_golden_fixture_coverage(golden):
     assert (golden["fall_timer_in"] < 0).any() and (golden["prev_rescued_in"] < 0).any()
 
 
-def test_bipedal_logic_matches_reference(tables, golden, bipedal_model):
+def test_bipedal_logic_matches_reference(tables, golden_any, bipedal_model):
+    golden = golden_any
+    f64 = golden["action"].dtype == np.float64
     L = BipedalLogic(tables)
     nu = bipedal_model.nu
     n = golden["obs"].shape[0]
@@ -76,7 +85,9 @@ def test_bipedal_logic_matches_reference(tables, golden, bipedal_model):
         assert term == bool(golden["terminated"][i]) and trunc == bool(golden["truncated"][i]), i
         assert s["rescued"] == _ids(golden["rescued_out"][i]) and s["carried"] == _ids(golden["carried_out"][i]), i
         assert s["carrying"] == bool(golden["carrying_out"][i]) and s["step"] == golden["current_step_out"][i], i
-        assert isinstance(s["energy"], np.float32) and float(s["energy"]) == golden["energy_out"][i], i
+        # current_energy's numpy type: float32 with float32 actions, float64 once a float64 cost
+        assert isinstance(s["energy"], np.float64 if f64 else np.float32), (i, type(s["energy"]))
+        assert bool(golden["energy_is_f32"][i]) == (not f64) and float(s["energy"]) == golden["energy_out"][i], i
         assert s["closest"] == golden["closest_out"][i], i
         assert s["prev_rescued"] == golden["prev_rescued_out"][i] and s["prev_carried"] == golden["prev_carried_out"][i]
         np.testing.assert_array_equal(s["prev_sz"], golden["prev_sz_out"][i])

@@ -27,6 +27,13 @@ def golden():
     return dict(np.load(G + "dancing_envlogic.npz"))
 
 
+@pytest.fixture(scope="module", params=["", "_f64"], ids=["float32_actions", "float64_actions"])
+def golden_any(request):
+    """The env-logic vectors with float32 actions, and the same states with float64 actions
+    (make_fixtures.py main_f64: the reference keeps a float64 action float64 through np.clip)."""
+    return dict(np.load(G + "dancing_envlogic" + request.param + ".npz"))
+
+
 def state_from_golden(g, i, nu):
     s = {k: (g[k + "_in"][i].copy() if np.ndim(g[k + "_in"][i]) else g[k + "_in"][i].item()) for k in KEYS}
     s["hist"] = [int(x) for x in g["hist_in"][i] if x >= 0]
@@ -48,7 +55,8 @@ def test_golden_fixture_coverage(golden):
     assert (golden["obs"][:, 78:88].sum(1) == 0).any(), "move index past the sequence end"
 
 
-def test_dancing_logic_matches_reference(model, golden):
+def test_dancing_logic_matches_reference(model, golden_any):
+    golden = golden_any
     L = DancingLogic(DancingTables(model))
     n = golden["obs"].shape[0]
     for i in range(n):

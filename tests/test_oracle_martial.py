@@ -31,8 +31,10 @@ def test_martial_model_inventory(model):
     assert model.jnt_qposadr[model.name2id("joint", "dummy1_base")] == 0  # quirk M1 target
 
 
-def test_martial_logic_matches_reference(model):
-    g = dict(np.load(G + "martial_envlogic.npz"))
+@pytest.mark.parametrize("sfx", ["", "_f64"], ids=["float32_actions", "float64_actions"])
+def test_martial_logic_matches_reference(model, sfx):
+    """sfx _f64: the same states with float64 actions (make_fixtures.py main_f64)."""
+    g = dict(np.load(G + "martial_envlogic" + sfx + ".npz"))
     t = MartialTables(model)
     L = MartialLogic(t)
     for i in range(g["obs"].shape[0]):

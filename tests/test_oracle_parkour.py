@@ -25,6 +25,13 @@ def golden():
     return dict(np.load(G + "parkour_envlogic.npz"))
 
 
+@pytest.fixture(scope="module", params=["", "_f64"], ids=["float32_actions", "float64_actions"])
+def golden_any(request):
+    """The env-logic vectors with float32 actions, and the same states with float64 actions
+    (make_fixtures.py main_f64: the reference keeps a float64 action float64 through np.clip)."""
+    return dict(np.load(G + "parkour_envlogic" + request.param + ".npz"))
+
+
 def state_from_golden(g, i):
     n = int(g["ncon"][i])
     return dict(qpos=g["qpos"][i].copy(), qvel=g["qvel"][i].copy(), xpos=g["xpos"][i].copy(),
@@ -44,7 +51,8 @@ def test_golden_fixture_coverage(golden):
     assert (golden["fall_count_out"] > golden["fall_count_in"]).any()
 
 
-def test_parkour_logic_matches_reference(tables, golden):
+def test_parkour_logic_matches_reference(tables, golden_any):
+    golden = golden_any
     L = ParkourLogic(tables)
     n = golden["obs"].shape[0]
     for i in range(n):

@@ -49,9 +49,11 @@ def test_golden_fixture_shapes(golden):
     assert golden["ball_contact"].any() and golden["goal_scored_out"].any()
 
 
-def test_soccer_logic_matches_reference(soccer_model, tables, golden):
+@pytest.mark.parametrize("sfx", ["", "_f64"], ids=["float32_actions", "float64_actions"])
+def test_soccer_logic_matches_reference(soccer_model, tables, golden, sfx):
+    """sfx _f64: the same states with float64 actions (make_fixtures.py main_f64)."""
     L = SoccerLogic(tables)
-    g = golden
+    g = golden if not sfx else dict(np.load(G + "soccer_envlogic_f64.npz"))
     for i in range(g["obs"].shape[0]):
         s = state_from_golden(g, i, soccer_model.nbody, soccer_model.nv)
         a = g["action"][i]
