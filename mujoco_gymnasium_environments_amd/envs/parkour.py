@@ -25,6 +25,7 @@ from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import NativeError, check, lib
 from ..seeding import np_random
 from ..spaces import Box, EnvBase, policy_action
+from .sharded import StreamShardedEnv
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "quadruped_parkour.xml")
 
@@ -230,6 +231,27 @@ class ParkourVectorEnv:
 
     def close(self):
         pass
+
+
+class StreamShardedParkourEnv(StreamShardedEnv):
+    """``num_envs`` parkour envs as ``n_streams`` shards on their own HIP streams (envs/sharded.py):
+    one shard's row builder fills the CUs another shard's solver leaves idle while its few
+    heaviest slots (up to 338 rows at bench conditions) finish their Gauss–Seidel chains. Same
+    trajectories as one ParkourVectorEnv over all envs (tests/test_gpu_parkour.py)."""
+
+    def __init__(self, num_envs: int, n_streams: int = 2, device: str = "cuda:0", precision: str = "f64",
+                 seed: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True,
+                 env_offset: int = 0, staged: bool = True, banks: int = 1):
+        super().__init__(lambda n, off: ParkourVectorEnv(n, device=device, precision=precision, seed=seed,
+                                                         max_episode_steps=max_episode_steps, autoreset=autoreset,
+                                                         env_offset=env_offset + off, staged=staged, banks=banks),
+                         num_envs, n_streams, device)
+
+    def checkpoints_reached(self) -> torch.Tensor:
+        return torch.cat([s.checkpoints_reached() for s in self.shards])
+
+    def course_completion(self) -> torch.Tensor:
+        return torch.cat([s.course_completion() for s in self.shards])
 
 
 def _popcount(x: torch.Tensor) -> torch.Tensor:

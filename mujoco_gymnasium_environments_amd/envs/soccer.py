@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import ctypes as C
 import functools
-from collections.abc import Mapping
 import os
 from typing import Any, Dict, Optional, Tuple
 
@@ -25,6 +24,7 @@ from ..batch import PhysicsBatch, _ptr, stream_handle
 from ..native import NativeError, check, lib
 from ..seeding import np_random
 from ..spaces import Box, EnvBase
+from .sharded import StreamShardedEnv
 
 ASSET = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "humanoid_soccer.xml")
 
@@ -245,110 +245,21 @@ class SoccerVectorEnv:
         pass
 
 
-class _CatInfo(Mapping):
-    """info() of a stream-sharded batch: each field is the shards' device views concatenated on
-    first access (no kernels are launched for fields the caller never reads). A read-only
-    Mapping, so get / items / values / `in` all go through __getitem__ and agree with the
-    single-batch SoccerVectorEnv.info() dict."""
-
-    def __init__(self, shards):
-        self._shards = shards
-        self._keys = list(shards[0].info().keys())
-        self._cache: Dict[str, Any] = {}
-
-    def __getitem__(self, k):
-        if k not in self._cache:
-            if k not in self._keys:
-                raise KeyError(k)
-            self._cache[k] = torch.cat([s.info()[k] for s in self._shards])
-        return self._cache[k]
-
-    def __iter__(self):
-        return iter(self._keys)
-
-    def __len__(self):
-        return len(self._keys)
-
-
-class StreamShardedSoccerEnv:
+class StreamShardedSoccerEnv(StreamShardedEnv):
     """``num_envs`` soccer envs as ``n_streams`` contiguous shards, each its own staged pipeline
-    (SoccerVectorEnv, own workspace) on its own HIP stream. One step launches every shard's
-    rows -> PGS -> finish chain on its stream, so one shard's row builder (LDS-limited) overlaps
-    another's solver (under one wave per SIMD). Shard i owns global envs
-    [env_offset + start_i, ...): draws are keyed by the global env index, so trajectories are the
-    ones a single SoccerVectorEnv over all envs produces (tests/test_gpu_f32_staged.py). obs /
-    reward / flags / final_obs are one tensor each; the shards write into row slices of it."""
+    (SoccerVectorEnv, own workspace) on its own HIP stream (envs/sharded.py). One step launches
+    every shard's rows -> PGS -> finish chain on its stream, so one shard's row builder
+    (LDS-limited) overlaps another's solver (under one wave per SIMD) and the solver's heavy-slot
+    tail. Trajectories are the ones a single SoccerVectorEnv over all envs produces
+    (tests/test_gpu_staged.py)."""
 
     def __init__(self, num_envs: int, n_streams: int = 2, device: str = "cuda:0", precision: str = "f64",
                  seed: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, autoreset: bool = True,
                  env_offset: int = 0, staged: bool = True, banks: int = 3):
-        if n_streams < 1 or n_streams > num_envs:
-            raise ValueError("need 1 <= n_streams <= num_envs")
-        self.num_envs = num_envs
-        self.device = torch.device(device)
-        base, extra = divmod(num_envs, n_streams)
-        self.bounds = []
-        a = 0
-        for i in range(n_streams):
-            b = a + base + (1 if i < extra else 0)
-            self.bounds.append((a, b))
-            a = b
-        self.shards = [SoccerVectorEnv(b - a, device=device, precision=precision, seed=seed,
-                                       max_episode_steps=max_episode_steps, autoreset=autoreset,
-                                       env_offset=env_offset + a, staged=staged, banks=banks)
-                       for a, b in self.bounds]
-        s0 = self.shards[0]
-        self.model, self.tables, self.action_space = s0.model, s0.tables, s0.action_space
-        dev, N = self.device, num_envs
-        self.obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
-        self.final_obs = torch.zeros(N, OBS_DIM, dtype=torch.float32, device=dev)
-        self.reward = torch.zeros(N, dtype=torch.float64, device=dev)
-        self.terminated = torch.zeros(N, dtype=torch.uint8, device=dev)
-        self.truncated = torch.zeros(N, dtype=torch.uint8, device=dev)
-        for (a, b), s in zip(self.bounds, self.shards):  # shard outputs are row slices (contiguous)
-            s.obs, s.final_obs = self.obs[a:b], self.final_obs[a:b]
-            s.reward, s.terminated, s.truncated = self.reward[a:b], self.terminated[a:b], self.truncated[a:b]
-        self.streams = [torch.cuda.Stream(device=dev) for _ in self.shards]
-
-    def _fan_out(self, stream, fn):
-        cs = stream if stream is not None else torch.cuda.current_stream(self.device)
-        for st in self.streams:
-            st.wait_stream(cs)
-        for (a, b), s, st in zip(self.bounds, self.shards, self.streams):
-            fn(a, b, s, st)
-        for st in self.streams:
-            cs.wait_stream(st)
-
-    def reset(self, seed: Optional[int] = None, env_mask: Optional[torch.Tensor] = None,
-              draws: Optional[np.ndarray] = None, stream=None):
-        """SoccerVectorEnv.reset over every shard (mask / draws sliced per shard)."""
-        d = None if draws is None else np.asarray(draws).reshape(self.num_envs, -1)
-        self._fan_out(stream, lambda a, b, s, st: s.reset(seed=seed, env_mask=None if env_mask is None else env_mask[a:b],
-                                                           draws=None if d is None else d[a:b], stream=st))
-        return self.obs, self.info()
-
-    def step(self, actions: torch.Tensor, stream=None):
-        """One env step for every env; actions float32 or float64 [N, nu] on the device."""
-        dt = torch.float64 if actions.dtype == torch.float64 else torch.float32
-        if actions.dtype != dt or not actions.is_contiguous() or actions.device != self.device:
-            actions = actions.to(device=self.device, dtype=dt).contiguous()
-        assert actions.shape == (self.num_envs, self.model.nu), actions.shape
-        self._fan_out(stream, lambda a, b, s, st: s.step(actions[a:b], stream=st))
-        return self.obs, self.reward, self.terminated, self.truncated, self.info()
-
-    def info(self) -> Dict[str, Any]:
-        return _CatInfo(self.shards)
-
-    @property
-    def episode(self) -> torch.Tensor:
-        return torch.cat([s.episode for s in self.shards])
-
-    @property
-    def rollout(self) -> torch.Tensor:
-        return torch.cat([s.rollout for s in self.shards])
-
-    def close(self):
-        pass
+        super().__init__(lambda n, off: SoccerVectorEnv(n, device=device, precision=precision, seed=seed,
+                                                        max_episode_steps=max_episode_steps, autoreset=autoreset,
+                                                        env_offset=env_offset + off, staged=staged, banks=banks),
+                         num_envs, n_streams, device)
 
 
 def _obs_bounds(num_joints: int):

@@ -430,3 +430,29 @@ def test_bipedal_f32_distribution_matches_f64():
     assert abs(a["reward"] - b["reward"]) <= 0.03 * abs(a["reward"]) + 1.0
     p = min(max(a["term"], 0.01), 0.99)
     assert abs(a["term"] - b["term"]) <= 5 * np.sqrt(p * (1 - p) / n) + 0.02, (a["term"], b["term"])
+
+
+@pytest.mark.parametrize("serial", [False, True], ids=["streams", "sub_batches"])
+def test_bipedal_stream_shards_equal_single_batch(serial):
+    """The generic StreamShardedEnv (envs/sharded.py; bench.py --streams / --sub-batches) over
+    BipedalVectorEnv: 2 shards on 2 HIP streams, or 2 sub-batches one after another on one
+    stream, reproduce one batch bit for bit (fp64, U(+-100) actions)."""
+    from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+    from mujoco_gymnasium_environments_amd.envs.sharded import StreamShardedEnv
+    n = 101
+    one = BipedalVectorEnv(n, precision="f64", seed=4)
+    sh = StreamShardedEnv(lambda k, off: BipedalVectorEnv(k, precision="f64", seed=4, env_offset=off), n, 2,
+                          serial=serial)
+    one.reset()
+    sh.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(2)
+    for t in range(40):
+        a = ((torch.rand(n, 26, device="cuda:0", generator=g) * 2 - 1) * 100.0).contiguous()
+        s1 = one.step(a)
+        s2 = sh.step(a)
+        for x, y, name in zip(s1[:4], s2[:4], ("obs", "reward", "terminated", "truncated")):
+            assert torch.equal(x, y), (t, name)
+    torch.cuda.synchronize()
+    assert torch.equal(one.episode, sh.episode)
+    assert torch.equal(one.rollout, sh.rollout)

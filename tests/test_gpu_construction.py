@@ -58,7 +58,7 @@ def test_construction_logic_kernel_matches_reference(cmodel, prec):
     env.scal.copy_(_t(np.concatenate([g["progress_in"][:, None], g["weather"]], 1), torch.float64))
     env.ints.copy_(_t(np.stack([g["task"], g["step_in"], g["blocks"], g["violations"], g["completed_in"]], 1),
                       torch.int32))
-    env.total_reward.copy_(_t(g["total_in"].astype(np.float32), torch.float32))
+    env.total_reward.copy_(_t(g["total_in"], torch.float64))  # the device rounds it as numpy does per kind
     hid = env.tables.humanoid
     xpos = np.zeros((n, m.nbody, 3))
     xpos[:, hid, 2] = g["torso_z"]

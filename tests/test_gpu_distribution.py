@@ -30,7 +30,7 @@ TASKS = {
     # task: (envs, env steps per env); the oracle side runs in 8 processes (~10-20 s per task)
     "soccer": (128, 200),
     "parkour": (128, 200),
-    "bipedal": (64, 100),
+    "bipedal": (64, 250),
 }
 
 

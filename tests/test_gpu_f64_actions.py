@@ -92,7 +92,8 @@ def test_float64_actions_match_oracle(task):
             if not live[i]:
                 continue
             np.testing.assert_allclose(og[i], ob, rtol=1e-5, atol=1e-5, err_msg=f"{task} step {t} env {i}")
-            assert abs(rg[i] - r) <= 1e-6 * max(1.0, abs(r)), (task, t, i, rg[i], r)
+            # (bipedal's approach term is +inf on the first step after a reset, rescue_env.py:632-635)
+            assert rg[i] == r or abs(rg[i] - r) <= 1e-6 * max(1.0, abs(r)), (task, t, i, rg[i], r)
             assert bool(tg[i]) == te and bool(trg[i]) == tr, (task, t, i)
             if task == "bipedal":  # the action-only energy bookkeeping, float64 from the first step on
                 assert isinstance(o.s["energy"], np.float64)

@@ -271,3 +271,35 @@ def test_parkour_end_to_end_f64_bench_actions(parkour_model):
     print(f"\nparkour U(+-lim): steps compared per env {horizon.tolist()}; "
           f"worst device error {[f'{w:.1e}' for w in worst]}")
     assert horizon.min() >= 2 and horizon.sum() >= 50, horizon
+
+
+def test_parkour_stream_shards_equal_single_batch():
+    """StreamShardedParkourEnv (3 shards on 3 HIP streams, ragged sizes) reproduces one
+    ParkourVectorEnv over the same envs bit for bit at bench conditions (fp64, U(-lim, lim)
+    actions, the heavy exploding-state slots and their same-step resets): the shards only
+    partition the launches."""
+    from mujoco_gymnasium_environments_amd.envs.parkour import (ParkourVectorEnv, StreamShardedParkourEnv,
+                                                                action_limits)
+    n = 190
+    one = ParkourVectorEnv(n, precision="f64", seed=21)
+    sh = StreamShardedParkourEnv(n, 3, precision="f64", seed=21)
+    assert [b - a for a, b in sh.bounds] == [64, 63, 63]
+    o1, _ = one.reset()
+    o2, _ = sh.reset()
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    lim = torch.as_tensor(action_limits(), dtype=torch.float32, device="cuda:0")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(13)
+    for t in range(60):
+        a = ((torch.rand(n, 16, device="cuda:0", generator=g) * 2 - 1) * lim).contiguous()
+        s1 = one.step(a)
+        s2 = sh.step(a)
+        for x, y, name in zip(s1[:4], s2[:4], ("obs", "reward", "terminated", "truncated")):
+            assert torch.equal(x, y), (t, name)
+    torch.cuda.synchronize()
+    assert torch.equal(one.episode, sh.episode) and torch.equal(one.final_obs, sh.final_obs)
+    assert torch.equal(one.batch.qpos, torch.cat([s.batch.qpos for s in sh.shards]))
+    assert torch.equal(one.checkpoints_reached(), sh.checkpoints_reached())
+    assert torch.equal(one.info()["fall_count"], sh.info()["fall_count"])
+    assert int(one.batch.warning.sum()) == sum(int(s.batch.warning.sum()) for s in sh.shards)
