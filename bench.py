@@ -50,10 +50,10 @@ METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 M
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
 # latest tools/profile_round.sh summaries of the soccer step (HBM traffic per step), per precision
-PMC_PROFILE = {"f64": "r05_head_pmc.json", "f32": "r03_f32_pmc.json"}
+PMC_PROFILE = {"f64": "r06_head_pmc.json", "f32": "r03_f32_pmc.json"}
 PMC_PROFILE_BIPEDAL = "r05_bipedal_pmc.json"
 PMC_PROFILE_ASSEMBLY = "r05_assembly_pmc.json"
-PMC_PROFILE_PARKOUR = "r05_parkour_pmc.json"
+PMC_PROFILE_PARKOUR = "r06_parkour_pmc.json"
 PMC_PROFILE_CONSTRUCTION = "r05_construction_pmc.json"
 PMC_PROFILE_MIXED = "r05_mixed_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
@@ -296,8 +296,11 @@ def cpu_baseline_assembly(n_envs: int, n_steps: int, seed: int = 0) -> dict:
 # round 5 (assembly now the longest stream): soccer beside construction, dancing beside bipedal —
 # 125.8k / 126.0k / 126.5k against 125.0k / 124.5k / 124.6k env-steps/s for the round-4 grouping
 # (construction alone; bipedal + soccer; parkour + martial arts + dancing), alternating runs on one box
-MIXED_GROUPS = [["humanoid_construction", "humanoid_soccer"], ["robotic_arm_assembly"],
-                ["bipedal_rescue", "humanoid_dancing"], ["quadruped_parkour", "humanoid_martial_arts"]]
+# Round 6 (parkour at MuJoCo's full arena, 96 contacts / 384 rows): parkour's stream alone, martial
+# arts beside construction and soccer — 112.8k -> 128.8k env-steps/s against the round-5 grouping
+# (parkour with martial arts), one box, profiles/r06_mixed_groups_ab.json
+MIXED_GROUPS = [["humanoid_construction", "humanoid_soccer", "humanoid_martial_arts"], ["robotic_arm_assembly"],
+                ["bipedal_rescue", "humanoid_dancing"], ["quadruped_parkour"]]
 # MGX_MIX_GROUPS (A/B hook): another grouping, groups separated by ';', tasks by ',' (group 0 is
 # the high-priority one)
 if os.environ.get("MGX_MIX_GROUPS"):
@@ -326,8 +329,9 @@ def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
 
     HIP streams map onto GPU_MAX_HW_QUEUES hardware queues (4 on the box): with a stream per
     task (7, plus the staged tasks' side streams) unrelated tasks share queues and wait on each
-    other's kernels. Four streams instead: construction (with soccer) and assembly, the long Newton
-    steps, each on a stream of their own, the other PGS tasks in two pairs; no side streams
+    other's kernels. Four streams instead: construction (with soccer and martial arts) and assembly,
+    the long Newton steps, each on a stream of their own, bipedal with dancing, and parkour (its
+    heavy-slot solver chains) alone; no side streams
     (MGX_SIDE_STREAM=0, mixed_side_streams). Construction's stream runs at high priority
     (mix_priority 1, measured 73.2k -> 75.5k env-steps/s in round 4; in round 5 group 0 alone is
     still best: 122.7k against 119.4k with assembly's group, 118.9k with both). mix_streams 7: one
@@ -611,9 +615,10 @@ def main():
                     help="soccer: 96 contacts / 384 rows per env (the default since round 5; kept for old scripts)")
     ap.add_argument("--reduced-capacity", action="store_true",
                     help="soccer: the round-1 capacity, 64 contacts / 192 rows, rows beyond it dropped and counted")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=None,
                     help="soccer / parkour / bipedal: split the rank's envs into this many stream shards, each "
-                         "its own staged pipeline on its own HIP stream (envs/sharded.py)")
+                         "its own staged pipeline on its own HIP stream (envs/sharded.py); default 3 for "
+                         "parkour (145.9k -> 157.8k env-steps/s, profiles/r06_stream_shards_ab.json), else 1")
     ap.add_argument("--sub-batches", type=int, default=1,
                     help="parkour / bipedal: step the rank's envs as this many sub-batches one after another "
                          "on one stream (envs/sharded.py serial shards: one sub-batch's B live in the "
@@ -627,6 +632,8 @@ def main():
     ap.add_argument("--task", default="soccer", choices=["soccer", "parkour", "bipedal", "mixed", "assembly",
                                                           "construction"])
     args = ap.parse_args()
+    if args.streams is None:
+        args.streams = 3 if args.task == "parkour" and args.sub_batches <= 1 else 1
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # no outer launcher: one child process per GPU, started before any GPU call

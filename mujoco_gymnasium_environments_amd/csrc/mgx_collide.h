@@ -475,6 +475,10 @@ __device__ __forceinline__ int box_box(const T* pa, const T* Ra, const T* ha, co
     for (int c = 0; c < 3; c++) { out[0].n[c] = n[c]; out[0].pos[c] = (T)0.5 * (P[c] + Q[c]); }
     return 1;
   }
+  // a NaN pose fails every separation test and leaves no axis selected: no contact (indexing with
+  // face_axis = -1 read ha[-1] / hb[-1], one real before the model's geom_size slice, and A[-1];
+  // round-6 fault audit). Finite poses always select an axis: results unchanged.
+  if (face_axis < 0) return 0;
   bool refA = face_axis < 3;
   int ri = refA ? face_axis : face_axis - 3;
   const T* pr = refA ? pa : pb;

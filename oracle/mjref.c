@@ -979,6 +979,9 @@ static int box_box(const double *pa, const double *Ra, const double *ha, const d
     for (int c = 0; c < 3; c++) { out[0].n[c] = n[c]; out[0].pos[c] = 0.5 * (P[c] + Q[c]); }
     return 1;
   }
+  /* a NaN pose fails every separation test and leaves no axis selected: no contact (indexing
+     with face_axis = -1 would read before the size and axis arrays) */
+  if (face_axis < 0) return 0;
   /* face contact: reference box R, incident box I */
   int refA = face_axis < 3;
   int ri = refA ? face_axis : face_axis - 3;

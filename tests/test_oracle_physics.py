@@ -312,3 +312,21 @@ def test_position_servo_kp_and_forcerange():
         s.qpos[0] = 0.02
         s.forward()
         assert abs(s.actuator_force[0] - min(50.0, kp * (0.05 - 0.02))) < 1e-12
+
+
+def test_box_box_nan_pose_gives_no_contact():
+    """A NaN box orientation fails every separation test of box_box, so no face axis is selected;
+    the routine returns no contact instead of indexing the size and axis arrays with -1 (round-6
+    fault audit; the device's mgx_collide.h box_box has the same guard). Finite
+    poses are unaffected: the resting-box scene still gives its 4 face contacts."""
+    import ctypes as C
+    xml = (HDR + '<worldbody><geom type="box" size="2 2 0.1"/>'
+           '<body pos="0 0 0.29"><freejoint/><geom type="box" size="0.2 0.3 0.2" mass="4"/></body>'
+           '</worldbody></mujoco>')
+    m, pk, s = sim_of(xml)
+    s.forward()
+    lib = s.L
+    assert lib.ref_collide_pair(C.addressof(pk.desc), s.d, 0) == 4
+    xmat = s.geom_xmat
+    xmat[9:18] = np.nan
+    assert lib.ref_collide_pair(C.addressof(pk.desc), s.d, 0) == 0
