@@ -1449,10 +1449,13 @@ __device__ __forceinline__ T row_cost_change(T x, T dx, T D) {
 
 // newton()'s row passes over the batches b0, b0 + bs, ... of MGX_RB rows (bs = the wave count:
 // wave 0 takes the even batches, the helper wave the odd ones; one wave takes them all in order).
-// setup: aref, b, x at u = 0 and at the warmstart, D per row; the two costs' partial sums
+// setup: aref, b, x at u = 0 and at the warmstart, D per row; the two costs' partial sums, the
+// even batches' in c0 / cw and the odd batches' in c0o / cwo whatever the wave count, so one wave
+// and a wave pair add the same partial sums in the same order (c0 + c0o: ADVICE r05, the warmstart
+// choice cw < c0 may not depend on the workgroup size)
 template <typename T>
 __device__ __forceinline__ void nt_setup_rows(const Env<T>& e, int ne, int nv, T wv, T ws, T wd, int b0, int bs, T& c0,
-                                              T& cw) {
+                                              T& cw, T& c0o, T& cwo) {
   const int l = lane_id();
   const bool dl = l < nv;
   const int lc = dl ? l : 0;
@@ -1472,8 +1475,9 @@ __device__ __forceinline__ void nt_setup_rows(const Env<T>& e, int ne, int nv, T
         T* q = efc + 8 * r;
         const T aref = -q[6] * dv - q[5];
         const T b = ds - aref, D = (T)1 / q[2], xw = b + dw;
-        if (b < 0) c0 += (T)0.5 * D * b * b;
-        if (xw < 0) cw += (T)0.5 * D * xw * xw;
+        const bool odd = ((r0 / MGX_RB) & 1) != 0;
+        if (b < 0) (odd ? c0o : c0) += (T)0.5 * D * b * b;
+        if (xw < 0) (odd ? cwo : cw) += (T)0.5 * D * xw * xw;
         if (l == 0) { q[5] = aref; q[0] = b; q[1] = b; q[3] = xw; q[4] = D; }
       }
     }
@@ -1532,17 +1536,20 @@ __device__ __forceinline__ void newton(const DevModel<T>& m, Env<T>& e) {
   // Rows are read row-major (lane = dof, one coalesced load per row, wave reductions), which is
   // what keeps the global-scratch rows (Layout.gB) off the latency path; the row scalars are
   // uniform and lane 0 stores them.
-  T c0 = 0, cw = 0;
+  T c0 = 0, cw = 0, c0o = 0, cwo = 0;
   const int nw = e.nw;
   if (nw > 1) {  // the helper's inputs
     if (dl) { e.vec0[l] = wv; e.vec1[l] = ws; e.vec2[l] = wd; }
   }
   team_begin(e, TEAM_SETUP, ne);
-  nt_setup_rows(e, ne, nv, wv, ws, wd, 0, nw, c0, cw);
+  nt_setup_rows(e, ne, nv, wv, ws, wd, 0, nw, c0, cw, c0o, cwo);
   team_end(e);
   if (nw > 1) {  // the helper's partial costs (odd batches), in vec3[0..1]
     c0 += e.vec3[0];
     cw += e.vec3[1];
+  } else {
+    c0 += c0o;
+    cw += cwo;
   }
   const T uw = wd;
   cw += usum((T)0.5 * uw * uw);
@@ -1702,9 +1709,9 @@ __device__ __forceinline__ void team_helper_n(const DevModel<T>& m, Env<T>& e) {
     const int a = __builtin_amdgcn_readfirstlane(e.ctl[1]);
     if (cmd == TEAM_SETUP) {
       const T wv = dl ? e.vec0[l] : (T)0, ws = dl ? e.vec1[l] : (T)0, wd = dl ? e.vec2[l] : (T)0;
-      T c0 = 0, cw = 0;
-      nt_setup_rows(e, a, nv, wv, ws, wd, 1, 2, c0, cw);
-      if (l == 0) { e.vec3[0] = c0; e.vec3[1] = cw; }
+      T c0 = 0, cw = 0, c0o = 0, cwo = 0;  // odd batches only: c0o / cwo
+      nt_setup_rows(e, a, nv, wv, ws, wd, 1, 2, c0, cw, c0o, cwo);
+      if (l == 0) { e.vec3[0] = c0o; e.vec3[1] = cwo; }
     } else if (cmd == TEAM_HESS) {  // tile row 3 and the gradient (newton's hess_grad)
       e.vec1[l] = hessian_mfma<T, 3, 4, true>(e.Bm, e.Bs, e.efc, a, nv, e.hess);
     } else if (cmd == TEAM_TRAIL) {

@@ -1010,7 +1010,12 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
         nm = max(nm, __shfl_xor(nm, 16));
         nm = max(nm, __shfl_xor(nm, 32));
         if (__builtin_amdgcn_readfirstlane(nm) > P.capE) {
+          // the launch's longest chains (their slots' rows exceed the LDS rows): first pick of
+          // their SIMD's issue slots over co-resident waves (another stream's kernels, the next
+          // stage of a stream shard), as the wide launch does
+          __builtin_amdgcn_s_setprio(3);
           pgs_group<T, EPL, LPS, false, true, DOFB>(P, smem, slot, P.maxE, maxit, tol, scale, spw, -1);
+          __builtin_amdgcn_s_setprio(0);
           __syncthreads();
           continue;
         }

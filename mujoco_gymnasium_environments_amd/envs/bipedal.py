@@ -119,7 +119,13 @@ class BipedalVectorEnv:
         builder, the lane-group PGS and a stage finisher, with ``banks`` reset states settled ahead
         per env); ``staged=False`` runs one wave per env for the whole step. An episode lasts at
         least 101 steps unless truncated earlier (the fall timer, rescue_env.py:670-697), so one
-        bank, ready 10 steps after it restarts, covers every autoreset."""
+        bank, ready 10 steps after it restarts, covers every autoreset.
+
+        Capacity: the staged step holds the model's 192 contacts / 768 rows (the oracle census
+        peaks at 585 rows, so no row is dropped at bench actions); the monolithic step
+        (``staged=False``) keeps its rows in per-env scratch sized for 512 rows and drops rows past
+        that in MuJoCo's order, counted in ``batch.overflow`` — the two paths compute the same
+        physics on every env step under 512 rows (tests/test_gpu_bipedal.py)."""
         self.num_envs = num_envs
         self.device = torch.device(device)
         self.model = bipedal_model()

@@ -1,5 +1,5 @@
 """Stream shards: one batch of envs stepped as several contiguous shards, each its own staged
-pipeline (own VectorEnv, own workspace) on its own HIP stream.
+pipeline (own VectorEnv, own workspace) on its own HIP stream (shard 0 on the caller's).
 
 Why: a staged step is a chain of launches per substep (rows -> lane-group PGS -> finish). The
 solver launch ends with a tail in which a few waves run the heaviest slots' Gauss–Seidel chains
@@ -83,7 +83,10 @@ class StreamShardedEnv:
             for (a, b), s in zip(self.bounds, self.shards):  # row slices: contiguous
                 setattr(s, name, full[a:b])
         self.serial = serial
-        self.streams = [] if serial else [torch.cuda.Stream(device=self.device) for _ in self.shards]
+        # shard 0 runs on the caller's stream, shards 1.. on streams of their own: K shards take K
+        # HIP streams, so up to 4 fit the box's 4 hardware queues (GPU_MAX_HW_QUEUES) without a
+        # shard's kernels queueing behind the caller stream's wait for all of them
+        self.streams = [] if serial else [torch.cuda.Stream(device=self.device) for _ in self.shards[1:]]
 
     def _fan_out(self, stream, fn):
         cs = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -93,7 +96,7 @@ class StreamShardedEnv:
             return
         for st in self.streams:
             st.wait_stream(cs)
-        for (a, b), s, st in zip(self.bounds, self.shards, self.streams):
+        for (a, b), s, st in zip(self.bounds, self.shards, [cs] + self.streams):
             fn(a, b, s, st)
         for st in self.streams:
             cs.wait_stream(st)

@@ -160,3 +160,31 @@ def test_task_kernels_reject_newton_models(soccer_model):
         ids = SoccerTables(m).ids_struct()
         rc = lib().mgx_soccer_configure(b.native.handle, C.byref(ids))
         assert rc < 0 and b"PGS" in lib().mgx_last_error()
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_newton_qfrc_constraint_is_jt_f(newton_case, prec):
+    """the Newton solvers return qfrc_constraint as u - g (g = u + sum D x B from
+    the last Hessian / gradient pass) instead of summing J' f, which cancels when |u| >> |sum f B|.
+    Pinned on the contact-heavy states of newton_case (|qacc| up to 1e12): the device's
+    qfrc_constraint against J' f formed in fp64 on the host from the device's own efc_force and the
+    oracle's J at the same state (same rows, same order) — so the solver's iterate is factored out
+    and only the u - g arithmetic is measured. Bars relative to max(1, |J' f|): fp64 1e-8, fp32 5e-3."""
+    from mujoco_gymnasium_environments_amd.batch import PhysicsBatch
+    m, packed, states = newton_case
+    b = PhysicsBatch(m, N, precision=prec)
+    load_states(b, states)
+    dbg = b.debug_forward()
+    worst = 0.0
+    for i, st in enumerate(states):
+        o = oracle_at(packed, st)
+        o.forward()
+        ne = int(o.nefc[0])
+        if ne == 0:
+            continue
+        J = np.asarray(o.efc_J[:ne * m.nv], dtype=np.float64).reshape(ne, m.nv)
+        jtf = J.T @ np.asarray(dbg["efc_force"][i][:ne], dtype=np.float64)
+        err = _rel(np.asarray(dbg["qfrc_constraint"][i][:m.nv], dtype=np.float64), jtf)
+        worst = max(worst, err)
+    print(f"\nqfrc_constraint vs J'f ({prec}): max relative error {worst:.3g}")
+    assert worst < (1e-8 if prec == "f64" else 5e-3), worst
