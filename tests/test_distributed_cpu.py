@@ -145,3 +145,19 @@ def test_gloo_world2_bench_harness_env_shards():
             r, t1, t2 = e.step(acts[k])
             rew, term, trunc = rew + r, term + t1, trunc + t2
     assert abs(red0[2] - rew) <= 1e-9 * abs(rew) and (red0[3], red0[4]) == (term, trunc)
+
+
+def test_shard_bounds_partition():
+    """Stream shards / sub-batches (envs/sharded.py) and rank shards partition envs the same way:
+    contiguous, covering, the first num_envs % k shards one env larger, refusing k > num_envs."""
+    import pytest as _pytest
+
+    from mujoco_gymnasium_environments_amd.envs.sharded import shard_bounds
+    for n, k in ((4096, 3), (190, 3), (101, 2), (7, 7), (5, 1)):
+        b = shard_bounds(n, k)
+        assert b[0][0] == 0 and b[-1][1] == n and len(b) == k
+        assert all(b[i][1] == b[i + 1][0] for i in range(k - 1))
+        sizes = [y - x for x, y in b]
+        assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+    with _pytest.raises(ValueError):
+        shard_bounds(3, 4)
