@@ -51,11 +51,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
 # latest tools/profile_round.sh summaries of the soccer step (HBM traffic per step), per precision
 PMC_PROFILE = {"f64": "r06_head_pmc.json", "f32": "r03_f32_pmc.json"}
-PMC_PROFILE_BIPEDAL = "r05_bipedal_pmc.json"
+PMC_PROFILE_BIPEDAL = "r06_bipedal_pmc.json"
 PMC_PROFILE_ASSEMBLY = "r05_assembly_pmc.json"
 PMC_PROFILE_PARKOUR = "r06_parkour_pmc.json"
 PMC_PROFILE_CONSTRUCTION = "r05_construction_pmc.json"
-PMC_PROFILE_MIXED = "r05_mixed_pmc.json"
+PMC_PROFILE_MIXED = "r06_mixed_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
@@ -617,8 +617,8 @@ def main():
                     help="soccer: the round-1 capacity, 64 contacts / 192 rows, rows beyond it dropped and counted")
     ap.add_argument("--streams", type=int, default=None,
                     help="soccer / parkour / bipedal: split the rank's envs into this many stream shards, each "
-                         "its own staged pipeline on its own HIP stream (envs/sharded.py); default 3 for "
-                         "parkour (145.9k -> 157.8k env-steps/s, profiles/r06_stream_shards_ab.json), else 1")
+                         "its own staged pipeline on its own HIP stream (envs/sharded.py); default 4 for "
+                         "parkour (145.9k -> 159.6k env-steps/s, profiles/r06_stream_shards_ab.json), else 1")
     ap.add_argument("--sub-batches", type=int, default=1,
                     help="parkour / bipedal: step the rank's envs as this many sub-batches one after another "
                          "on one stream (envs/sharded.py serial shards: one sub-batch's B live in the "
@@ -633,7 +633,7 @@ def main():
                                                           "construction"])
     args = ap.parse_args()
     if args.streams is None:
-        args.streams = 3 if args.task == "parkour" and args.sub_batches <= 1 else 1
+        args.streams = 4 if args.task == "parkour" and args.sub_batches <= 1 else 1
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # no outer launcher: one child process per GPU, started before any GPU call
