@@ -593,8 +593,12 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
       p.capE = p.maxE;
       p.sqg = 1;
     } else {
-      int r = MGX_PGS_LDS_ROWS;
-      while (r + 8 <= p.maxE && staged_pgs_lds_bytes(m, r + 8, pgs_lanes(), 0, mgx_twl(false)) <= 160 * 1024 / 4) r += 8;
+      // MGX_PGS_WPC (A/B): size the LDS rows for more waves per CU than four; the slots beyond
+      // them run in the main launch with their scalars from the pipe (hmain), whose LDS then
+      // sets the wave's allocation when it is the larger
+      const int budget = 160 * 1024 / H.pgs_wpc;
+      int r = H.pgs_wpc == 4 ? MGX_PGS_LDS_ROWS : 8;
+      while (r + 8 <= p.maxE && staged_pgs_lds_bytes(m, r + 8, pgs_lanes(), 0, mgx_twl(false)) <= budget) r += 8;
       p.capE = r;
     }
   }
@@ -625,7 +629,8 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
   // maxE rows fits the LDS of a capE-row wave. The MGX_PGS_LDS_ROWS test hook keeps the wide launch.
   p.hmain = !rk && !cap_env && !p.sqg && !H.pgs_lds_b && p.capE < p.maxE &&
             staged_pgs_lds_bytes(m, p.maxE, pgs_lanes(), 1, mgx_twl(false)) <=
-                staged_pgs_lds_bytes(m, p.capE, pgs_lanes(), 0, mgx_twl(false));
+                (H.pgs_wpc == 4 ? staged_pgs_lds_bytes(m, p.capE, pgs_lanes(), 0, mgx_twl(false))
+                                : 160 * 1024 / H.pgs_wpc);
   if (p.hmain) p.warena = 0;
   p.nbk = (p.hmain ? p.maxE : p.capE) / 4 + 1;
   p.o_hist = take((size_t)(p.maxE / 4 + 1) * 4);
@@ -690,6 +695,8 @@ mgx::Hooks mgx::read_hooks() {
   h.pgs_lds_pad = get("MGX_PGS_LDS_PAD", 0);
   h.pgs_wide_lds = get("MGX_PGS_WIDE_LDS", 1);
   h.pgs_spw = get("MGX_PGS_SPW", 0);
+  h.pgs_wpc = get("MGX_PGS_WPC", 4);
+  if (h.pgs_wpc < 4 || h.pgs_wpc > 16) h.pgs_wpc = 4;
   // MGX_SIDE_STREAM=0 runs the wide solver launch after the main one on the caller's stream: with
   // more streams than hardware queues (several tasks on one GPU, each on its own stream) a side
   // stream can queue behind another task's long kernels
@@ -758,6 +765,7 @@ static int soccer_step_staged(const mgx_model* m, const DevModel<T>& M, const De
   // follows the main launch there.
   const int wgrid = 64 / pgs_lanes() * MGX_PGS_WIDE_GRID, wlds = pgs_lds_bytes(m, P.maxE);
   int mlds = H.pgs_lds_b ? P.arena : pgs_lds_bytes(m, P.capE, P.sqg);
+  if (P.hmain) mlds = std::max(mlds, pgs_lds_bytes(m, P.maxE, 1));  // the heavy slots' SQG layout
   // occupancy probe: MGX_PGS_LDS_PAD pads the main solver launch's LDS (fewer waves per CU)
   if (H.pgs_lds_pad > mlds && H.pgs_lds_pad <= 96 * 1024) mlds = H.pgs_lds_pad;
   if (!H.pgs_lds_b && (P.maxE <= P.capE || P.hmain)) {

@@ -394,7 +394,8 @@ int step_staged(const mgx_model* m, const DevModel<T>& M, const DevModel<T>& Ms,
   // the pipe: Pipe.hmain)
   const int slots = n_env * (1 + banks);
   const T scale = (T)1 / (M.meaninertia * (T)(M.nv > 1 ? M.nv : 1));
-  const int mlds = staged_pgs_lds_bytes(m, P.capE, PK_LPS, 0, 8);
+  const int mlds = std::max(staged_pgs_lds_bytes(m, P.capE, PK_LPS, 0, 8),
+                           P.hmain ? staged_pgs_lds_bytes(m, P.maxE, PK_LPS, 1, 8) : 0);
   const int spw = 64 / PK_LPS, grid = (slots + spw - 1) / spw;
   for (int k = 0; k < PK_SUBSTEPS; k++) {
     hipLaunchKernelGGL(k_pk_rows<T>, dim3(slots), dim3(64), m->Ls.bytes, st, Ms, ids, *s, action, e->action_f64, n_env,

@@ -175,3 +175,35 @@ def test_storage_capacity_truncates_and_counts(soccer_model, monkeypatch):
     torch.cuda.synchronize()
     assert int(small.batch.overflow.sum()) > 0
     assert int(full.batch.overflow.sum()) == 0
+
+
+@pytest.mark.parametrize("wpc", [6])
+def test_solver_occupancy_hook_bit_identical(soccer_model, wpc):
+    """MGX_PGS_WPC sizes the main solver launch's LDS rows for more waves per CU; slots beyond
+    them run in the same launch with their row scalars read from the pipe (Pipe.hmain) — the same
+    arithmetic, so the same states bit for bit at bench actions (fp64, full capacity), and the
+    staged parkour step likewise."""
+    from mujoco_gymnasium_environments_amd.envs.parkour import ParkourVectorEnv, action_limits
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    n, steps = 256, 30
+    a = SoccerVectorEnv(n, precision="f64", seed=41)
+    pa = ParkourVectorEnv(n, precision="f64", seed=41)
+    with _Env(MGX_PGS_WPC=str(wpc)):  # read when b's model is created
+        b = SoccerVectorEnv(n, precision="f64", seed=41)
+        pb = ParkourVectorEnv(n, precision="f64", seed=41)
+    assert pb.staged
+    for e in (a, b, pa, pb):
+        e.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(3)
+    lim = torch.as_tensor(action_limits(), dtype=torch.float32, device="cuda:0")
+    for t in range(steps):
+        act = torch.rand(n, soccer_model.nu, device="cuda:0", generator=g) * 300 - 150
+        pact = ((torch.rand(n, 16, device="cuda:0", generator=g) * 2 - 1) * lim).contiguous()
+        for (x, y), ac in (((a, b), act), ((pa, pb), pact)):
+            rx, ry = x.step(ac), y.step(ac)
+            for u, v, name in zip(rx[:4], ry[:4], ("obs", "reward", "terminated", "truncated")):
+                assert torch.equal(u, v), (type(x).__name__, t, name)
+    torch.cuda.synchronize()
+    assert torch.equal(a.batch.qpos, b.batch.qpos) and torch.equal(pa.batch.qpos, pb.batch.qpos)
+    assert int(a.batch.overflow.sum()) == 0 and int(pa.batch.overflow.sum()) == 0
