@@ -8,10 +8,11 @@ included. An out-of-bounds index in the algorithm shows here as an ASan report.
 
     python tools/asan_oracle.py [--envs 3] [--steps 300]
 
-builds oracle/mjref.c with -fsanitize=address,undefined into /tmp/mjref_asan/, then re-runs
-itself with that library (MJREF_LIB) and the sanitizer runtimes preloaded (this container has no
-LD_PRELOAD of its own), stepping every PGS task's oracle env (oracle/envs.py) at the bench's
-action distribution with autoreset. Exit status 0 and "clean" when no report was raised.
+builds the ASan + UBSan oracle (`make -C oracle asan`, the library tools/oracle_asan.sh runs the
+oracle unit tests against), then re-runs itself with that library (MJREF_LIB) and the sanitizer
+runtimes preloaded (this container has no LD_PRELOAD of its own), stepping every PGS task's oracle
+env (oracle/envs.py) at the bench's action distribution with autoreset — the states the unit
+tests do not reach. Exit status 0 and "clean" when no report was raised.
 """
 from __future__ import annotations
 
@@ -22,17 +23,11 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = "/tmp/mjref_asan"
 
 
 def build() -> str:
-    os.makedirs(OUT, exist_ok=True)
-    lib = os.path.join(OUT, "libmjref.so")
-    cmd = ["gcc", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=all", "-shared", "-fPIC", "-I", ROOT, os.path.join(ROOT, "oracle", "mjref.c"),
-           "-o", lib, "-lm"]
-    subprocess.run(cmd, check=True)
-    return lib
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], check=True)
+    return os.path.join(ROOT, "oracle", "_build", "libmjref_asan.so")
 
 
 def runtime(name: str) -> str:
