@@ -632,6 +632,7 @@ size_t mgx::make_staged_pipe(const mgx_model* m, void* ws, int n_env, int banks,
                 (H.pgs_wpc == 4 ? staged_pgs_lds_bytes(m, p.capE, pgs_lanes(), 0, mgx_twl(false))
                                 : 160 * 1024 / H.pgs_wpc);
   if (p.hmain) p.warena = 0;
+  p.prio_rows = H.pgs_prio_rows > 0 ? H.pgs_prio_rows : p.capE;
   p.nbk = (p.hmain ? p.maxE : p.capE) / 4 + 1;
   p.o_hist = take((size_t)(p.maxE / 4 + 1) * 4);
   p.o_blist = take((size_t)(p.maxE / 4 + 1) * S * 4);
@@ -695,6 +696,7 @@ mgx::Hooks mgx::read_hooks() {
   h.pgs_lds_pad = get("MGX_PGS_LDS_PAD", 0);
   h.pgs_wide_lds = get("MGX_PGS_WIDE_LDS", 1);
   h.pgs_spw = get("MGX_PGS_SPW", 0);
+  h.pgs_prio_rows = get("MGX_PGS_PRIO_ROWS", 0);
   h.pgs_wpc = get("MGX_PGS_WPC", 4);
   if (h.pgs_wpc < 4 || h.pgs_wpc > 16) h.pgs_wpc = 4;
   // MGX_SIDE_STREAM=0 runs the wide solver launch after the main one on the caller's stream: with

@@ -62,6 +62,9 @@ struct Pipe {
                        // to maxE) go to the second, wide-LDS launch (o_k2big)
   int arena;           // LDS bytes of one main-launch solver wave (scalars + block table + B of its slots)
   int sqg;             // soccer main launch: row scalars read from the pipe, forces only in LDS (capE > 192)
+  int prio_rows;       // main launch: a wave whose slots reach more rows than this raises its wave
+                       // priority (s_setprio 3): the launch's longest chains issue first on a
+                       // shared SIMD (default: capE, i.e. the hmain waves; MGX_PGS_PRIO_ROWS)
   int hmain;           // 1: slots over capE rows stay in the main launch's heaviest-first list; a wave
                        // holding one runs with its row scalars read from the pipe (SQG), whose LDS
                        // (forces + table for maxE rows) fits the wave's capE-row allocation
@@ -1003,22 +1006,28 @@ __global__ void __launch_bounds__(64) k_pgs_groups(Pipe P, int maxit, T tol, T s
     const int idx = dup ? base : (s < spn && base + s < cnt) ? base + s : -1;
     const int slot = big ? (idx >= 0 ? list[idx] : -1) : sorted_slot(P, idx, LPS);
     if constexpr (!BLDS && !SQG) {
-      // a wave holding a slot over the main launch's LDS-scalar rows (heaviest first: the first
-      // waves) reads its row scalars from the pipe instead; same arithmetic, so the same results
-      if (!big && P.hmain) {
+      if (!big) {
         int nm = slot >= 0 ? P.at<int>(P.o_ne)[slot] : 0;
         nm = max(nm, __shfl_xor(nm, 16));
         nm = max(nm, __shfl_xor(nm, 32));
-        if (__builtin_amdgcn_readfirstlane(nm) > P.capE) {
-          // the launch's longest chains (their slots' rows exceed the LDS rows): first pick of
-          // their SIMD's issue slots over co-resident waves (another stream's kernels, the next
-          // stage of a stream shard), as the wide launch does
-          __builtin_amdgcn_s_setprio(3);
+        nm = __builtin_amdgcn_readfirstlane(nm);
+        // the launch's longest chains (heaviest first: the first waves): first pick of their
+        // SIMD's issue slots over co-resident waves (another stream's kernels, the next stage of a
+        // stream shard), as the wide launch does; no effect on any result
+        const bool hi = nm > P.prio_rows;
+        if (hi) __builtin_amdgcn_s_setprio(3);
+        // a wave holding a slot over the main launch's LDS-scalar rows reads its row scalars from
+        // the pipe instead; same arithmetic, so the same results
+        if (P.hmain && nm > P.capE) {
           pgs_group<T, EPL, LPS, false, true, DOFB>(P, smem, slot, P.maxE, maxit, tol, scale, spw, -1);
-          __builtin_amdgcn_s_setprio(0);
+          if (hi) __builtin_amdgcn_s_setprio(0);
           __syncthreads();
           continue;
         }
+        pgs_group<T, EPL, LPS, false, false, DOFB>(P, smem, slot, P.capE, maxit, tol, scale, spw, -1);
+        if (hi) __builtin_amdgcn_s_setprio(0);
+        __syncthreads();
+        continue;
       }
     }
     pgs_group<T, EPL, LPS, BLDS && true, SQG, DOFB>(P, smem, slot, big ? P.maxE : P.capE, maxit, tol, scale, spw,
