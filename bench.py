@@ -763,7 +763,7 @@ def main():
         if not args.no_f64_line:
             other = "f32" if args.precision == "f64" else "f64"
             out[f"{other}_line"] = bipedal_other_line(args, dev, N, g, other)
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline_bipedal(max(1, args.cpu_envs // 8), args.cpu_steps // 10)
         print(json.dumps(out))
     elif rank == 0 and args.task == "assembly":
@@ -787,7 +787,7 @@ def main():
                          "kernel": "mgx_assembly_step = k_assembly<T,0,GB>", "alg_bytes_per_step": bytes_per_launch,
                          "launch_ms": round(launch_ms, 4)},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline_assembly(2, max(5, args.cpu_steps // 2))
         print(json.dumps(out))
     elif rank == 0 and args.task == "construction":
@@ -841,7 +841,7 @@ def main():
                          "alg_bytes_per_step": bytes_per_launch,
                          "launch_ms": round(launch_ms, 4)},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline_parkour(max(1, args.cpu_envs // 4), args.cpu_steps // 4)
         print(json.dumps(out))
     elif rank == 0:
@@ -886,7 +886,7 @@ def main():
         if not args.no_f64_line and world == 1 and not args.mono and args.streams == 1:
             other = "f32" if args.precision == "f64" else "f64"
             out[f"{other}_line"] = other_precision_line(args, dev, N, g, other)
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_steps)
         print(json.dumps(out))
     if dist:
