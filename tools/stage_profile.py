@@ -88,12 +88,18 @@ def main_task(task):
     for k in range(2):
         env.step(acts[k % 4])
     torch.cuda.synchronize()
-    buf = torch.zeros(n * 32, dtype=torch.int64, device="cuda:0")
+    # staged RK4 (bipedal_staged): the row builder's blocks are the slots (live + reset banks) and
+    # the solver's blocks its waves, so the stamp buffer holds a row per slot, 4 x the envs at most
+    staged = task == "bipedal_staged"
+    nslot = 4 * n if staged else n
+    buf = torch.zeros(nslot * 32, dtype=torch.int64, device="cuda:0")
     assert setter(C.c_void_p(buf.data_ptr())) == 0
     for k in range(steps):
         env.step(acts[k % 4])
     torch.cuda.synchronize()
-    raw = buf.view(n, 32).double().cpu().numpy()
+    raw = buf.view(nslot, 32).double().cpu().numpy()
+    if staged:
+        return report_rows(raw, n, steps, env, "staged RK4 row builder (per RK4 stage)")
     v = raw / steps
     tot = v[:, :len(STAGES)].sum(1).mean()
     calls = raw[:, 23].sum()
@@ -110,6 +116,31 @@ def main_task(task):
             print(f"    {st:22s} {v[:, 10 + i].mean():14.0f}")
     print(f"  lds bytes per env {env.native.info.lds_bytes_per_env}, scratch bytes per env "
           f"{env.native.info.scratch_bytes_per_env}")
+
+
+def report_rows(raw, n, steps, env, title):
+    """The staged row builders' stamps (stage_rows: one row per slot, live envs first, then the
+    reset banks) and the solver's sweep counters (slots 26..30 of its wave rows)."""
+    import numpy as np
+    calls = np.maximum(raw[:, 23], 1)
+    act = raw[:, 23] > 0
+    v = raw[act] / calls[act, None]
+    names = STAGES_ROWS
+    print(f"{title}: envs={n} steps={steps} slots with work {act.sum()} (live {act[:n].sum()}, bank "
+          f"{act[n:].sum()}); mean cycles per slot-stage (s_memtime units)")
+    tot = v[:, :len(names) - SUBSTAGES].sum(1).mean()
+    print(f"  total {tot:.0f}")
+    for i, s in enumerate(names):
+        print(f"  {s:40s} {v[:, i].mean():12.0f}  {100 * v[:, i].mean() / tot:5.1f}%   p99 {np.percentile(v[:, i], 99):.0f}")
+    k2 = raw[:, 28] > 0
+    if k2.any():
+        cyc, blks = raw[k2, 26].sum(), raw[k2, 27].sum()
+        rt = raw[k2, 29].sum()
+        print(f"  solver waves: {int(raw[k2, 28].sum())} wave-launches; sweep cycles per block "
+              f"{cyc / max(blks, 1):.0f}; blocks swept by the heaviest wave {raw[k2, 30].max():.0f} "
+              f"(mean {blks / raw[k2, 28].sum():.0f}); shader clock {cyc / max(rt, 1) * 0.1:.2f} GHz")
+    print(f"  per slot-stage: nefc mean {(raw[:, 20].sum() / max(raw[:, 23].sum(), 1)):.1f}  ncon mean "
+          f"{(raw[:, 22].sum() / max(raw[:, 23].sum(), 1)):.1f}")
 
 
 def main():
