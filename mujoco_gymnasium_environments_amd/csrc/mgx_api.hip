@@ -697,6 +697,7 @@ mgx::Hooks mgx::read_hooks() {
   h.pgs_wide_lds = get("MGX_PGS_WIDE_LDS", 1);
   h.pgs_spw = get("MGX_PGS_SPW", 0);
   h.pgs_prio_rows = get("MGX_PGS_PRIO_ROWS", 0);
+  h.tight_bp = get("MGX_TIGHT_BROADPHASE", -1);
   h.pgs_wpc = get("MGX_PGS_WPC", 4);
   if (h.pgs_wpc < 4 || h.pgs_wpc > 16) h.pgs_wpc = 4;
   // MGX_SIDE_STREAM=0 runs the wide solver launch after the main one on the caller's stream: with
@@ -903,6 +904,10 @@ int mgx_model_create(const mgx_model_desc* d, int precision, int device, mgx_mod
   m->Ls = make_staged_layout(d, rb, max_ncon, any_staged ? max_nefc : 4, m->staged_ok ? 128 : max_active,
                              m->hooks.gcon);
   m->Lf = finisher_layout(m->Ls, rb);
+  {
+    const int tight = m->hooks.tight_bp >= 0 ? (m->hooks.tight_bp != 0) : (d->npair > MGX_TIGHT_BROADPHASE_PAIRS);
+    m->L.tight_bp = m->Ls.tight_bp = m->Lf.tight_bp = tight;
+  }
   int rc;
   if (precision == MGX_F32) {
     rc = build_model<float>(d, device, m, m->mf);

@@ -419,6 +419,45 @@ __device__ __forceinline__ int clip_poly(T (*in)[2], int n, int axis, T lim, T s
   return m;
 }
 
+// Broadphase prefilters for scenes with many candidate pairs (collision(), DevModel.npair >
+// MGX_TIGHT_BROADPHASE_PAIRS). Both are conservative: a pair they reject has no contact within its
+// margin, so the narrowphase would return none and the contact list is unchanged; each test carries
+// a slack of `tol` (relative to the geoms' sizes) so rounding can only let more pairs through.
+// Two boxes separated along one of their six face axes by more than the margin: the face-axis
+// part of box_box's separating-axis test.
+template <typename T>
+__device__ __forceinline__ bool box_box_separated(const T* pa, const T* Ra, const T* ha, const T* pb, const T* Rb,
+                                                  const T* hb, T margin, T tol) {
+  const T d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+  for (int ax = 0; ax < 6; ax++) {
+    const T* R = ax < 3 ? Ra : Rb;
+    const int c = ax < 3 ? ax : ax - 3;
+    const T n[3] = {R[c], R[3 + c], R[6 + c]};  // the box's axis c (column c of its frame)
+    T ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) {
+      ra += ha[k] * fabs(Ra[k] * n[0] + Ra[3 + k] * n[1] + Ra[6 + k] * n[2]);
+      rb += hb[k] * fabs(Rb[k] * n[0] + Rb[3 + k] * n[1] + Rb[6 + k] * n[2]);
+    }
+    if (fabs(dot3(d, n)) - ra - rb > margin + tol * (ra + rb + (T)1)) return true;
+  }
+  return false;
+}
+// A geom within its bounding sphere (center c, radius r) against a box: the sphere is farther
+// from the box than the margin.
+template <typename T>
+__device__ __forceinline__ bool sphere_box_separated(const T* c, T r, const T* pb, const T* Rb, const T* hb, T margin,
+                                                     T tol) {
+  const T v[3] = {c[0] - pb[0], c[1] - pb[1], c[2] - pb[2]};
+  T d2 = 0;
+  for (int k = 0; k < 3; k++) {
+    const T q = Rb[k] * v[0] + Rb[3 + k] * v[1] + Rb[6 + k] * v[2];  // box frame
+    const T o = fabs(q) - hb[k];
+    if (o > 0) d2 += o * o;
+  }
+  const T lim = (r + margin) * ((T)1 + tol) + tol * (hb[0] + hb[1] + hb[2] + (T)1);
+  return d2 > lim * lim;
+}
+
 template <typename T>
 __device__ __forceinline__ int box_box(const T* pa, const T* Ra, const T* ha, const T* pb, const T* Rb, const T* hb, T margin,
                        Con<T>* out) {

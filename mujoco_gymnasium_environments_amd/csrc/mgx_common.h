@@ -15,6 +15,7 @@
 #define MGX_MAX_NBODY 64
 #define MGX_MAX_DEPTH 16      // longest dof chain (root..dof), soccer: 13
 #define MGX_MAX_CONPAIR 8     // contacts per geom pair (box-box)
+#define MGX_TIGHT_BROADPHASE_PAIRS 64  // more candidate pairs: box prefilters after the spheres (default)
 #define MGX_EFC_SLOTS 6       // staged soccer step: max_nefc <= 64 * MGX_EFC_SLOTS = 384
 
 namespace mgx {
@@ -60,6 +61,10 @@ struct Layout {
   // over the phase-A arrays dead by then; contacts keep their normal only (3 reals, stride
   // cfs = 3; the frame is rebuilt where it is read) instead of the 9-real frame
   int late_geom, cfs;
+  // collision(): the box prefilters after the bounding spheres (mgx_collide.h box_box_separated /
+  // sphere_box_separated; conservative, the contact list is unchanged). Set per model: on when it
+  // has more than MGX_TIGHT_BROADPHASE_PAIRS candidate pairs (MGX_TIGHT_BROADPHASE=0/1 overrides)
+  int tight_bp;
   // staged row builder: LDS copy of xfrc_applied for the velocity stage (its per-dof force sums
   // read it nbody times per lane), in the phase-A region
   int xfrc_lds;

@@ -31,6 +31,7 @@ struct Hooks {
   int pgs_spw = 0;       // MGX_PGS_SPW: slots per solver wave (debug)
   int pgs_wpc = 4;       // MGX_PGS_WPC: main solver launch's waves per CU its LDS rows are sized for
   int pgs_prio_rows = 0; // MGX_PGS_PRIO_ROWS: rows above which a main-launch solver wave raises its priority
+  int tight_bp = -1;     // MGX_TIGHT_BROADPHASE: box prefilters in the broadphase (-1: by the pair count)
   int side_stream = 1;   // MGX_SIDE_STREAM: the wide solver launch on a side stream
   int gcon = 1;          // MGX_GCON: the row builder's contact points in the pipe (0: in LDS)
   int rows_lds = 0;      // MGX_ROWS_LDS: pad the row builder's LDS (occupancy probe)

@@ -6,6 +6,7 @@ module raises. ``build()`` compiles it for gfx950 with hipcc (cross-compiles wit
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 import subprocess
 
@@ -50,16 +51,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
     def command(src, obj):
         return [hipcc, *flags, *SOURCE_FLAGS.get(src, []), "-c", "-o", obj, os.path.join(CSRC, src)]
 
+    def deps_hash(src):
+        h = hashlib.sha1()
+        for d in deps(src):
+            with open(d, "rb") as f:
+                h.update(f.read())
+        return h.hexdigest()
+
     def stamp_ok(src, obj):
-        # an object is reused only when it is newer than its source and headers AND was built by
-        # the same command (compiler, common and per-source flags), recorded next to it
+        # an object is reused only when it was built by the same command (compiler, common and
+        # per-source flags) from the same source and header contents, both recorded next to it
+        # (contents, not mtimes: a header edited while a build runs must not leave objects of the
+        # old and the new struct layouts side by side)
         try:
             with open(obj + ".cmd") as f:
-                if f.read() != " ".join(command(src, obj)):
+                if f.read() != " ".join(command(src, obj)) + "\n" + deps_hash(src):
                     return False
         except OSError:
             return False
-        return all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in deps(src))
+        return True
 
     objs = [os.path.join(build_dir, src.replace(".hip", ".o")) for src in SOURCES]
     if not force and os.path.exists(LIB_PATH):
@@ -73,13 +83,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if not force and os.path.exists(obj) and stamp_ok(src, obj):
             continue
         cmd = command(src, obj)
-        procs.append((src, obj, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
-    for src, obj, cmd, p in procs:
+        dh = deps_hash(src)  # the contents this compile starts from
+        procs.append((src, obj, cmd, dh, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                                          text=True)))
+    for src, obj, cmd, dh, p in procs:
         _, err = p.communicate()
         if p.returncode != 0:
             raise NativeError(f"hipcc {src} failed ({p.returncode}):\n{err[-4000:]}")
         with open(obj + ".cmd", "w") as f:
-            f.write(" ".join(cmd))
+            f.write(" ".join(cmd) + "\n" + dh)
     r = subprocess.run([hipcc, *flags, "-shared", "-o", LIB_PATH + ".tmp", *objs], capture_output=True, text=True)
     if r.returncode != 0:
         raise NativeError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-4000:]}")

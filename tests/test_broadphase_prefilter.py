@@ -1,0 +1,118 @@
+"""CPU: the device broadphase's box prefilters are conservative (mgx_collide.h box_box_separated /
+sphere_box_separated, applied in collision() when a model has more than 64 candidate pairs: every
+task but parkour).
+
+A pair the prefilters reject must have no contact: the test restates both filters in numpy (same
+formulas, same slack) and runs them on the oracle's own states at bench-condition actions —
+bipedal_rescue (3,185 candidate pairs), martial arts (294), soccer (251) and dancing (106) through
+oracle/envs.py with autoreset, robotic_arm_assembly (803) on its oracle physics with random
+actuator targets — and
+asserts that every pair in the oracle's contact list passes them. It also reports how many
+sphere-test survivors they remove (the point of the filters: fewer narrowphase rounds).
+"""
+import numpy as np
+import pytest
+
+GBOX, GPLANE = 6, 0
+TOL = 1e-9
+
+
+def box_box_separated(pa, Ra, ha, pb, Rb, hb, margin, tol=TOL):
+    d = pb - pa
+    for ax in range(6):
+        R, c = (Ra, ax) if ax < 3 else (Rb, ax - 3)
+        n = R[:, c]
+        ra = float(np.sum(ha * np.abs(Ra.T @ n)))
+        rb = float(np.sum(hb * np.abs(Rb.T @ n)))
+        if abs(float(d @ n)) - ra - rb > margin + tol * (ra + rb + 1.0):
+            return True
+    return False
+
+
+def sphere_box_separated(c, r, pb, Rb, hb, margin, tol=TOL):
+    q = Rb.T @ (c - pb)
+    o = np.maximum(np.abs(q) - hb, 0.0)
+    lim = (r + margin) * (1.0 + tol) + tol * (float(np.sum(hb)) + 1.0)
+    return float(o @ o) > lim * lim
+
+
+def survivors(m, xpos, xmat):
+    """pairs passing the bounding-sphere test, and which of them the box prefilters reject"""
+    gt = np.asarray(m.geom_type)
+    pg = np.asarray(m.pair_geom).reshape(-1, 2)
+    rb = np.asarray(m.geom_rbound)
+    mg = np.asarray(m.pair_margin)
+    size = np.asarray(m.geom_size).reshape(-1, 3)
+    passed, rejected = [], set()
+    for p, (g1, g2) in enumerate(pg):
+        if gt[g1] == GPLANE:
+            continue
+        if np.linalg.norm(xpos[g2] - xpos[g1]) > rb[g1] + rb[g2] + mg[p]:
+            continue
+        passed.append(p)
+        if gt[g1] == GBOX and gt[g2] == GBOX:
+            rej = box_box_separated(xpos[g1], xmat[g1], size[g1], xpos[g2], xmat[g2], size[g2], mg[p])
+        elif gt[g1] == GBOX or gt[g2] == GBOX:
+            gb, go = (g1, g2) if gt[g1] == GBOX else (g2, g1)
+            rej = sphere_box_separated(xpos[go], rb[go], xpos[gb], xmat[gb], size[gb], mg[p])
+        else:
+            rej = False
+        if rej:
+            rejected.add(p)
+    return passed, rejected
+
+
+def _check(m, sim, totals):
+    xpos = sim.geom_xpos.reshape(-1, 3).copy()
+    xmat = sim.geom_xmat.reshape(-1, 3, 3).copy()
+    passed, rejected = survivors(m, xpos, xmat)
+    in_contact = set(int(p) for p in sim.contacts()["pair"])
+    assert not (in_contact & rejected), sorted(in_contact & rejected)
+    totals[0] += len(passed)
+    totals[1] += len(rejected)
+    totals[2] += len(in_contact)
+
+
+@pytest.mark.parametrize("task,steps", [("bipedal", 25), ("martial", 60), ("soccer", 100), ("dancing", 100)])
+def test_prefilters_keep_every_contact_pair(task, steps):
+    from mujoco_gymnasium_environments_amd.seeding import np_random
+    from oracle.envs import ORACLES, task_setup
+    packed, tb, draws_fn, acts_fn = task_setup(task)
+    m = packed.model
+    acts = acts_fn(np.random.default_rng(5), steps)
+    totals = [0, 0, 0]
+    for e in range(2):
+        rng = np_random(40 + e)[0]
+        env = ORACLES[task](packed, tb)
+        env.reset(draws_fn(rng))
+        for t in range(steps):
+            _, _, te, tr = env.step(acts[t])
+            _check(m, env.sim, totals)
+            if te or tr:
+                env.reset(draws_fn(rng))
+    print(f"\n{task}: sphere-test survivors {totals[0]}, removed by the box prefilters {totals[1]}, "
+          f"pairs in contact {totals[2]}")
+    assert totals[2] > 0
+    if task == "bipedal":
+        assert totals[1] > 0.3 * totals[0]  # the filters do remove most box survivors
+
+
+def test_prefilters_keep_every_contact_pair_assembly():
+    from mujoco_gymnasium_environments_amd import cabi
+    from mujoco_gymnasium_environments_amd.envs.assembly import assembly_model
+    from oracle.mjref import RefSim
+    m = assembly_model()
+    pk = cabi.pack_model(m)
+    sim = RefSim(pk)
+    sim.reset()
+    rng = np.random.default_rng(2)
+    lo = np.array([-2.0] * 7 + [0, 0]) / np.array([1.0] * 7 + [1000.0, 1000.0])
+    hi = np.array([2.0] * 7 + [100, 50]) / np.array([1.0] * 7 + [1000.0, 1000.0])
+    totals = [0, 0, 0]
+    for t in range(60):
+        sim.ctrl[:] = rng.uniform(lo, hi)
+        sim.step()
+        _check(m, sim, totals)
+    print(f"\nassembly: sphere-test survivors {totals[0]}, removed by the box prefilters {totals[1]}, "
+          f"pairs in contact {totals[2]}")
+    assert totals[2] > 0

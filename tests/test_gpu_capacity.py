@@ -207,3 +207,31 @@ def test_solver_occupancy_hook_bit_identical(soccer_model, wpc):
     torch.cuda.synchronize()
     assert torch.equal(a.batch.qpos, b.batch.qpos) and torch.equal(pa.batch.qpos, pb.batch.qpos)
     assert int(a.batch.overflow.sum()) == 0 and int(pa.batch.overflow.sum()) == 0
+
+
+def test_broadphase_prefilters_bit_identical():
+    """The broadphase's box prefilters (Layout.tight_bp, on by default for models with more than 64
+    candidate pairs) only drop pairs the narrowphase would return no contact for: soccer (staged,
+    fp64) and bipedal (staged RK4, fp64) step bit-identically with them off (MGX_TIGHT_BROADPHASE=0)
+    at bench actions (tests/test_broadphase_prefilter.py checks the same on the oracle's states)."""
+    from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
+    from mujoco_gymnasium_environments_amd.envs.soccer import SoccerVectorEnv
+    n, steps = 128, 30
+    a = SoccerVectorEnv(n, precision="f64", seed=51)
+    pa = BipedalVectorEnv(n, precision="f64", seed=51)
+    with _Env(MGX_TIGHT_BROADPHASE="0"):  # read when b's model is created
+        b = SoccerVectorEnv(n, precision="f64", seed=51)
+        pb = BipedalVectorEnv(n, precision="f64", seed=51)
+    for e in (a, b, pa, pb):
+        e.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(8)
+    for t in range(steps):
+        act = torch.rand(n, a.model.nu, device="cuda:0", generator=g) * 300 - 150
+        bact = ((torch.rand(n, 26, device="cuda:0", generator=g) * 2 - 1) * 100).contiguous()
+        for (x, y), ac in (((a, b), act), ((pa, pb), bact)):
+            rx, ry = x.step(ac), y.step(ac)
+            for u, v, name in zip(rx[:4], ry[:4], ("obs", "reward", "terminated", "truncated")):
+                assert torch.equal(u, v), (type(x).__name__, t, name)
+    torch.cuda.synchronize()
+    assert torch.equal(a.batch.qpos, b.batch.qpos) and torch.equal(pa.batch.qpos, pb.batch.qpos)
