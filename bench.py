@@ -50,7 +50,7 @@ METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 M
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
 # latest tools/profile_round.sh summaries of the soccer step (HBM traffic per step), per precision
-PMC_PROFILE = {"f64": "r06_head_pmc.json", "f32": "r03_f32_pmc.json"}
+PMC_PROFILE = {"f64": "r06_final_head_pmc.json", "f32": "r03_f32_pmc.json"}
 PMC_PROFILE_BIPEDAL = "r06_bipedal_pmc.json"
 PMC_PROFILE_ASSEMBLY = "r05_assembly_pmc.json"
 PMC_PROFILE_PARKOUR = "r06_parkour_pmc.json"
