@@ -504,6 +504,26 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
   B.reals(d->geom_quat, 4 * ng, &M.geom_quat); B.reals(d->geom_rbound, ng, &M.geom_rbound);
   B.ints(d->pair_geom, 2 * np, &M.pair_geom); B.ints(d->pair_condim, np, &M.pair_condim);
   B.reals(d->pair_friction, 5 * np, &M.pair_friction); B.reals(d->pair_margin, np, &M.pair_margin);
+  {
+    std::vector<int> bpi(4 * (size_t)np, 0);
+    std::vector<double> bpr(4 * (size_t)np, 0.0);
+    for (int p = 0; p < np; p++) {
+      const int g1 = d->pair_geom[2 * p], g2 = d->pair_geom[2 * p + 1];
+      const int t1 = d->geom_type[g1], t2 = d->geom_type[g2];
+      const double mg = d->pair_margin[p];
+      int kind = 0;
+      if (t1 == GPLANE) kind = 1;
+      else if (t1 == GBOX && t2 == GBOX) kind = 2;
+      else if (t1 == GBOX) kind = 4;
+      else if (t2 == GBOX) kind = 8;
+      bpi[4 * p] = g1; bpi[4 * p + 1] = g2; bpi[4 * p + 2] = kind;
+      bpr[4 * p] = t1 == GPLANE ? d->geom_rbound[g2] + mg : d->geom_rbound[g1] + d->geom_rbound[g2] + mg;
+      bpr[4 * p + 1] = mg;
+      bpr[4 * p + 2] = kind == 4 ? d->geom_rbound[g2] : (kind == 8 ? d->geom_rbound[g1] : 0.0);
+    }
+    B.ints(bpi.data(), bpi.size(), &M.pair_bpi);
+    B.reals(bpr.data(), bpr.size(), &M.pair_bpr);
+  }
   B.reals(d->pair_gap, np, &M.pair_gap); B.reals(d->pair_solref, 2 * np, &M.pair_solref);
   B.reals(d->pair_solimp, 5 * np, &M.pair_solimp);
   B.ints(d->actuator_trnid, nu, &M.actuator_trnid); B.ints(d->actuator_ctrllimited, nu, &M.actuator_ctrllimited);

@@ -111,6 +111,13 @@ struct DevModel {
   const T *geom_size, *geom_pos, *geom_quat, *geom_rbound;
   // pairs
   const int *pair_geom, *pair_condim;
+  // broadphase records, one per candidate pair, so a round of 64 pairs is two vector loads with no
+  // dependent gathers (prefetched a round ahead): {g1, g2, kind, 0} — kind bit 0: g1 is a plane,
+  // bit 1: box-box, bit 2 / 3: g1 / g2 is a box and the other geom not — and {reach, margin,
+  // rbound of the non-box geom, 0}, reach = rbound[g1] + rbound[g2] + margin (plane: rbound[g2] +
+  // margin), the sums of the bounding-sphere tests
+  const int* pair_bpi;
+  const T* pair_bpr;
   const T *pair_friction, *pair_margin, *pair_gap, *pair_solref, *pair_solimp;
   // actuators
   const int *actuator_trnid, *actuator_ctrllimited, *actuator_forcelimited;

@@ -514,37 +514,50 @@ template <typename T>
 __device__ __forceinline__ void collision(const DevModel<T>& m, Env<T>& e) {
   int l = lane_id();
   const Layout& L = m.L;
-  // broadphase: bounding spheres (planes always pass); compact survivors in pair order
+  // broadphase: bounding spheres (planes: the half-space test); compact survivors in pair order.
+  // Each round reads its 64 pairs' records (DevModel.pair_bpi / pair_bpr) with the next round's
+  // already in flight, so only the LDS pose reads depend on a load.
   int nact = 0;
+  const int4* bpi = reinterpret_cast<const int4*>(m.pair_bpi);
+  int4 nr = l < m.npair ? bpi[l] : make_int4(0, 0, -1, 0);
+  T nreach = 0, nmargin = 0, nrbo = 0;
+  if (l < m.npair) { nreach = m.pair_bpr[4 * l]; nmargin = m.pair_bpr[4 * l + 1]; nrbo = m.pair_bpr[4 * l + 2]; }
   for (int base = 0; base < m.npair; base += 64) {
-    int p = base + l;
+    const int4 r = nr;
+    const T reach = nreach, margin = nmargin, rbo = nrbo;
+    const int pn = base + 64 + l;
+    if (pn < m.npair) {
+      nr = bpi[pn];
+      nreach = m.pair_bpr[4 * pn]; nmargin = m.pair_bpr[4 * pn + 1]; nrbo = m.pair_bpr[4 * pn + 2];
+    } else {
+      nr = make_int4(0, 0, -1, 0);
+    }
+    const int p = base + l;
     bool act = false;
-    if (p < m.npair) {
-      int g1 = m.pair_geom[2 * p], g2 = m.pair_geom[2 * p + 1];
-      T margin = m.pair_margin[p];
-      if (m.geom_type[g1] == GPLANE) {
+    if (r.z >= 0) {
+      const int g1 = r.x, g2 = r.y;
+      if (r.z & 1) {
         const T* pm = e.geom_xmat + 9 * g1;
         T n[3] = {pm[2], pm[5], pm[8]};
         T rel[3] = {e.geom_xpos[3 * g2] - e.geom_xpos[3 * g1], e.geom_xpos[3 * g2 + 1] - e.geom_xpos[3 * g1 + 1],
                     e.geom_xpos[3 * g2 + 2] - e.geom_xpos[3 * g1 + 2]};
-        act = dot3(rel, n) <= m.geom_rbound[g2] + margin;
+        act = dot3(rel, n) <= reach;
       } else {
         T dv[3] = {e.geom_xpos[3 * g2] - e.geom_xpos[3 * g1], e.geom_xpos[3 * g2 + 1] - e.geom_xpos[3 * g1 + 1],
                    e.geom_xpos[3 * g2 + 2] - e.geom_xpos[3 * g1 + 2]};
-        act = sqrt(dot3(dv, dv)) <= m.geom_rbound[g1] + m.geom_rbound[g2] + margin;
-        // many-pair scenes (bipedal 3,185 candidate pairs, assembly 803, construction 1,202): box
-        // pairs that pass the bounding spheres also pass a box test, so far fewer rounds of 64
-        // pairs reach the divergent narrowphase; conservative, the contact list is unchanged
-        if (act && L.tight_bp) {
-          const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        act = sqrt(dot3(dv, dv)) <= reach;
+        // many-pair scenes (bipedal 3,185 candidate pairs, assembly 803, construction 1,202, soccer
+        // 251): box pairs that pass the bounding spheres also pass a box test, so far fewer pairs
+        // reach the divergent narrowphase; conservative, the contact list is unchanged
+        if (act && L.tight_bp && (r.z & 14)) {
           const T tol = sizeof(T) == 8 ? (T)1e-9 : (T)1e-4;
-          if (t1 == GBOX && t2 == GBOX) {
+          if (r.z & 2) {
             act = !box_box_separated(e.geom_xpos + 3 * g1, e.geom_xmat + 9 * g1, m.geom_size + 3 * g1,
                                      e.geom_xpos + 3 * g2, e.geom_xmat + 9 * g2, m.geom_size + 3 * g2, margin, tol);
-          } else if (t1 == GBOX || t2 == GBOX) {
-            const int gb = t1 == GBOX ? g1 : g2, go = t1 == GBOX ? g2 : g1;
-            act = !sphere_box_separated(e.geom_xpos + 3 * go, m.geom_rbound[go], e.geom_xpos + 3 * gb,
-                                        e.geom_xmat + 9 * gb, m.geom_size + 3 * gb, margin, tol);
+          } else {
+            const int gb = (r.z & 4) ? g1 : g2, go = (r.z & 4) ? g2 : g1;
+            act = !sphere_box_separated(e.geom_xpos + 3 * go, rbo, e.geom_xpos + 3 * gb, e.geom_xmat + 9 * gb,
+                                        m.geom_size + 3 * gb, margin, tol);
           }
         }
       }
