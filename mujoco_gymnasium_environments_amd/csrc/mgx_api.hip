@@ -511,18 +511,28 @@ int build_model(const mgx_model_desc* d, int device, mgx_model* out, DevModel<T>
       const int g1 = d->pair_geom[2 * p], g2 = d->pair_geom[2 * p + 1];
       const int t1 = d->geom_type[g1], t2 = d->geom_type[g2];
       const double mg = d->pair_margin[p];
+      auto boxed = [](int t) { return t == GBOX || t == GCAPSULE || t == GCYLINDER; };
       int kind = 0;
       if (t1 == GPLANE) kind = 1;
-      else if (t1 == GBOX && t2 == GBOX) kind = 2;
-      else if (t1 == GBOX) kind = 4;
-      else if (t2 == GBOX) kind = 8;
+      else if (boxed(t1) && boxed(t2)) kind = 2;
+      else if (t1 == GSPHERE && boxed(t2)) kind = 4;
+      else if (t2 == GSPHERE && boxed(t1)) kind = 8;
       bpi[4 * p] = g1; bpi[4 * p + 1] = g2; bpi[4 * p + 2] = kind;
       bpr[4 * p] = t1 == GPLANE ? d->geom_rbound[g2] + mg : d->geom_rbound[g1] + d->geom_rbound[g2] + mg;
       bpr[4 * p + 1] = mg;
-      bpr[4 * p + 2] = kind == 4 ? d->geom_rbound[g2] : (kind == 8 ? d->geom_rbound[g1] : 0.0);
+      bpr[4 * p + 2] = kind == 4 ? d->geom_rbound[g1] : (kind == 8 ? d->geom_rbound[g2] : 0.0);
     }
     B.ints(bpi.data(), bpi.size(), &M.pair_bpi);
     B.reals(bpr.data(), bpr.size(), &M.pair_bpr);
+    std::vector<double> obb(3 * (size_t)ng, 0.0);
+    for (int g = 0; g < ng; g++) {
+      const double* sz = d->geom_size + 3 * g;
+      const int t = d->geom_type[g];
+      if (t == GBOX) { obb[3 * g] = sz[0]; obb[3 * g + 1] = sz[1]; obb[3 * g + 2] = sz[2]; }
+      if (t == GCAPSULE) { obb[3 * g] = sz[0]; obb[3 * g + 1] = sz[0]; obb[3 * g + 2] = sz[1] + sz[0]; }
+      if (t == GCYLINDER) { obb[3 * g] = sz[0]; obb[3 * g + 1] = sz[0]; obb[3 * g + 2] = sz[1]; }
+    }
+    B.reals(obb.data(), obb.size(), &M.geom_obb);
   }
   B.reals(d->pair_gap, np, &M.pair_gap); B.reals(d->pair_solref, 2 * np, &M.pair_solref);
   B.reals(d->pair_solimp, 5 * np, &M.pair_solimp);

@@ -15,7 +15,10 @@
 #define MGX_MAX_NBODY 64
 #define MGX_MAX_DEPTH 16      // longest dof chain (root..dof), soccer: 13
 #define MGX_MAX_CONPAIR 8     // contacts per geom pair (box-box)
-#define MGX_TIGHT_BROADPHASE_PAIRS 64  // more candidate pairs: box prefilters after the spheres (default)
+// more candidate pairs than this: bounding-box prefilters after the spheres (default; soccer 251,
+// martial arts 294, assembly 803, construction 1,202, bipedal 3,185 — not dancing's 106, where the
+// filters cost more than the narrowphase they save, nor parkour's 48)
+#define MGX_TIGHT_BROADPHASE_PAIRS 200
 #define MGX_EFC_SLOTS 6       // staged soccer step: max_nefc <= 64 * MGX_EFC_SLOTS = 384
 
 namespace mgx {
@@ -113,11 +116,13 @@ struct DevModel {
   const int *pair_geom, *pair_condim;
   // broadphase records, one per candidate pair, so a round of 64 pairs is two vector loads with no
   // dependent gathers (prefetched a round ahead): {g1, g2, kind, 0} — kind bit 0: g1 is a plane,
-  // bit 1: box-box, bit 2 / 3: g1 / g2 is a box and the other geom not — and {reach, margin,
-  // rbound of the non-box geom, 0}, reach = rbound[g1] + rbound[g2] + margin (plane: rbound[g2] +
-  // margin), the sums of the bounding-sphere tests
+  // bit 1: both geoms have a bounding box (box, capsule, cylinder; geom_obb), bit 2 / 3: g1 / g2 is
+  // a sphere and the other has a bounding box — and {reach, margin, the sphere's radius, 0}, reach =
+  // rbound[g1] + rbound[g2] + margin (plane: rbound[g2] + margin), the bounding-sphere tests' sums
   const int* pair_bpi;
   const T* pair_bpr;
+  const T* geom_obb;  // the geom's bounding box half-sizes in its frame: box (sx, sy, sz), capsule
+                      // (r, r, half-length + r), cylinder (r, r, half-height); 0 otherwise
   const T *pair_friction, *pair_margin, *pair_gap, *pair_solref, *pair_solimp;
   // actuators
   const int *actuator_trnid, *actuator_ctrllimited, *actuator_forcelimited;

@@ -547,17 +547,19 @@ __device__ __forceinline__ void collision(const DevModel<T>& m, Env<T>& e) {
                    e.geom_xpos[3 * g2 + 2] - e.geom_xpos[3 * g1 + 2]};
         act = sqrt(dot3(dv, dv)) <= reach;
         // many-pair scenes (bipedal 3,185 candidate pairs, assembly 803, construction 1,202, soccer
-        // 251): box pairs that pass the bounding spheres also pass a box test, so far fewer pairs
+        // 251): a pair that passes the bounding spheres must also pass a bounding-box test — the
+        // two geoms' boxes (box, capsule, cylinder: DevModel.geom_obb) not separated along their
+        // face axes, or a sphere within the margin of the other geom's box — so far fewer pairs
         // reach the divergent narrowphase; conservative, the contact list is unchanged
         if (act && L.tight_bp && (r.z & 14)) {
           const T tol = sizeof(T) == 8 ? (T)1e-9 : (T)1e-4;
           if (r.z & 2) {
-            act = !box_box_separated(e.geom_xpos + 3 * g1, e.geom_xmat + 9 * g1, m.geom_size + 3 * g1,
-                                     e.geom_xpos + 3 * g2, e.geom_xmat + 9 * g2, m.geom_size + 3 * g2, margin, tol);
+            act = !box_box_separated(e.geom_xpos + 3 * g1, e.geom_xmat + 9 * g1, m.geom_obb + 3 * g1,
+                                     e.geom_xpos + 3 * g2, e.geom_xmat + 9 * g2, m.geom_obb + 3 * g2, margin, tol);
           } else {
-            const int gb = (r.z & 4) ? g1 : g2, go = (r.z & 4) ? g2 : g1;
-            act = !sphere_box_separated(e.geom_xpos + 3 * go, rbo, e.geom_xpos + 3 * gb, e.geom_xmat + 9 * gb,
-                                        m.geom_size + 3 * gb, margin, tol);
+            const int gs = (r.z & 4) ? g1 : g2, gb = (r.z & 4) ? g2 : g1;
+            act = !sphere_box_separated(e.geom_xpos + 3 * gs, rbo, e.geom_xpos + 3 * gb, e.geom_xmat + 9 * gb,
+                                        m.geom_obb + 3 * gb, margin, tol);
           }
         }
       }

@@ -1,6 +1,7 @@
-"""CPU: the device broadphase's box prefilters are conservative (mgx_collide.h box_box_separated /
-sphere_box_separated, applied in collision() when a model has more than 64 candidate pairs: every
-task but parkour).
+"""CPU: the device broadphase's bounding-box prefilters are conservative (mgx_collide.h
+box_box_separated / sphere_box_separated on the geoms' bounding boxes — box, capsule (r, r, hl + r),
+cylinder (r, r, h) — applied in collision() when a model has more than 200 candidate pairs:
+soccer, martial arts, assembly, construction, bipedal).
 
 A pair the prefilters reject must have no contact: the test restates both filters in numpy (same
 formulas, same slack) and runs them on the oracle's own states at bench-condition actions —
@@ -13,7 +14,7 @@ sphere-test survivors they remove (the point of the filters: fewer narrowphase r
 import numpy as np
 import pytest
 
-GBOX, GPLANE = 6, 0
+GPLANE, GSPHERE, GCAPSULE, GCYLINDER, GBOX = 0, 2, 3, 5, 6
 TOL = 1e-9
 
 
@@ -36,13 +37,29 @@ def sphere_box_separated(c, r, pb, Rb, hb, margin, tol=TOL):
     return float(o @ o) > lim * lim
 
 
+def geom_obb(m):
+    """bounding-box half-sizes in the geom frame (DevModel.geom_obb): box, capsule, cylinder"""
+    gt = np.asarray(m.geom_type)
+    size = np.asarray(m.geom_size).reshape(-1, 3)
+    obb = np.zeros_like(size)
+    for g, t in enumerate(gt):
+        if t == GBOX:
+            obb[g] = size[g]
+        elif t == GCAPSULE:
+            obb[g] = (size[g][0], size[g][0], size[g][1] + size[g][0])
+        elif t == GCYLINDER:
+            obb[g] = (size[g][0], size[g][0], size[g][1])
+    return obb
+
+
 def survivors(m, xpos, xmat):
-    """pairs passing the bounding-sphere test, and which of them the box prefilters reject"""
+    """pairs passing the bounding-sphere test, and which of them the bounding-box prefilters reject"""
     gt = np.asarray(m.geom_type)
     pg = np.asarray(m.pair_geom).reshape(-1, 2)
     rb = np.asarray(m.geom_rbound)
     mg = np.asarray(m.pair_margin)
-    size = np.asarray(m.geom_size).reshape(-1, 3)
+    obb = geom_obb(m)
+    boxed = lambda t: t in (GBOX, GCAPSULE, GCYLINDER)  # noqa: E731
     passed, rejected = [], set()
     for p, (g1, g2) in enumerate(pg):
         if gt[g1] == GPLANE:
@@ -50,11 +67,11 @@ def survivors(m, xpos, xmat):
         if np.linalg.norm(xpos[g2] - xpos[g1]) > rb[g1] + rb[g2] + mg[p]:
             continue
         passed.append(p)
-        if gt[g1] == GBOX and gt[g2] == GBOX:
-            rej = box_box_separated(xpos[g1], xmat[g1], size[g1], xpos[g2], xmat[g2], size[g2], mg[p])
-        elif gt[g1] == GBOX or gt[g2] == GBOX:
-            gb, go = (g1, g2) if gt[g1] == GBOX else (g2, g1)
-            rej = sphere_box_separated(xpos[go], rb[go], xpos[gb], xmat[gb], size[gb], mg[p])
+        if boxed(gt[g1]) and boxed(gt[g2]):
+            rej = box_box_separated(xpos[g1], xmat[g1], obb[g1], xpos[g2], xmat[g2], obb[g2], mg[p])
+        elif (gt[g1] == GSPHERE and boxed(gt[g2])) or (gt[g2] == GSPHERE and boxed(gt[g1])):
+            gs, gb = (g1, g2) if gt[g1] == GSPHERE else (g2, g1)
+            rej = sphere_box_separated(xpos[gs], rb[gs], xpos[gb], xmat[gb], obb[gb], mg[p])
         else:
             rej = False
         if rej:

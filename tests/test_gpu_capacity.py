@@ -210,8 +210,8 @@ def test_solver_occupancy_hook_bit_identical(soccer_model, wpc):
 
 
 def test_broadphase_prefilters_bit_identical():
-    """The broadphase's box prefilters (Layout.tight_bp, on by default for models with more than 64
-    candidate pairs) only drop pairs the narrowphase would return no contact for: soccer (staged,
+    """The broadphase's bounding-box prefilters (Layout.tight_bp, on by default for models with more
+    than 200 candidate pairs) only drop pairs the narrowphase would return no contact for: soccer (staged,
     fp64) and bipedal (staged RK4, fp64) step bit-identically with them off (MGX_TIGHT_BROADPHASE=0)
     at bench actions (tests/test_broadphase_prefilter.py checks the same on the oracle's states)."""
     from mujoco_gymnasium_environments_amd.envs.bipedal import BipedalVectorEnv
