@@ -50,12 +50,12 @@ METRIC = "env steps/sec (whole node), humanoid_soccer 4096 envs/GPU at 1/2/4/8 M
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X_MICROARCH.md: FP32 vector peak; FP64 vector = 1/2
 # latest tools/profile_round.sh summaries of the soccer step (HBM traffic per step), per precision
-PMC_PROFILE = {"f64": "r06_final_head_pmc.json", "f32": "r03_f32_pmc.json"}
-PMC_PROFILE_BIPEDAL = "r06_bipedal_pmc.json"
+PMC_PROFILE = {"f64": "r06_final2_head_pmc.json", "f32": "r03_f32_pmc.json"}
+PMC_PROFILE_BIPEDAL = "r06_final_bipedal_pmc.json"
 PMC_PROFILE_ASSEMBLY = "r05_assembly_pmc.json"
 PMC_PROFILE_PARKOUR = "r06_parkour_pmc.json"
 PMC_PROFILE_CONSTRUCTION = "r05_construction_pmc.json"
-PMC_PROFILE_MIXED = "r06_mixed_pmc.json"
+PMC_PROFILE_MIXED = "r06_final_mixed_pmc.json"
 # algorithmic HBM bytes per env step: r/w qpos 41 + qvel 40 +
 # qacc_warmstart 40 (fp32), read action 33, r/w goalkeeper qfrc 1 + ball xfrc 2, r/w 11 task
 # scalars, write obs 80 (fp32), reward (fp64), terminated + truncated (u8)
