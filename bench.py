@@ -618,7 +618,8 @@ def main():
     ap.add_argument("--streams", type=int, default=None,
                     help="soccer / parkour / bipedal: split the rank's envs into this many stream shards, each "
                          "its own staged pipeline on its own HIP stream (envs/sharded.py); default 4 for "
-                         "parkour (145.9k -> 159.6k env-steps/s, profiles/r06_stream_shards_ab.json), else 1")
+                         "parkour (145.9k -> 159.6k env-steps/s), 2 for bipedal (206.6k -> 243.4k; "
+                         "profiles/r06_stream_shards_ab.json), else 1")
     ap.add_argument("--sub-batches", type=int, default=1,
                     help="parkour / bipedal: step the rank's envs as this many sub-batches one after another "
                          "on one stream (envs/sharded.py serial shards: one sub-batch's B live in the "
@@ -633,7 +634,7 @@ def main():
                                                           "construction"])
     args = ap.parse_args()
     if args.streams is None:
-        args.streams = 4 if args.task == "parkour" and args.sub_batches <= 1 else 1
+        args.streams = {"parkour": 4, "bipedal": 2}.get(args.task, 1) if args.sub_batches <= 1 else 1
     from mujoco_gymnasium_environments_amd.distributed import env_offset, reduce_rollout, world_from_env
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # no outer launcher: one child process per GPU, started before any GPU call
