@@ -342,7 +342,9 @@ def mixed_streams(tasks, mix_streams: int, mix_priority: int, dev):
     # beside bipedal and soccer, two A/B pairs on one box)
     # MGX_MIX_PRIO_GROUPS (A/B hook): which groups run at high priority; 0 / 0,1 / 1 measured
     # within noise of each other (75.3k - 75.9k, profiles/r04_mixed_priority_ab.json)
-    hi = {int(x) for x in os.environ.get("MGX_MIX_PRIO_GROUPS", "0").split(",") if x} if mix_priority else set()
+    # round 6: construction's group and parkour's stream at high priority (130.1k -> 132.0k
+    # env-steps/s mean of two interleaved pairs, profiles/r06_mixed_priority_ab.json)
+    hi = {int(x) for x in os.environ.get("MGX_MIX_PRIO_GROUPS", "0,3").split(",") if x} if mix_priority else set()
     gs = [torch.cuda.Stream(device=dev, priority=-1 if i in hi else 0) for i in range(len(MIXED_GROUPS))]
     return {k: gs[i] for i, grp in enumerate(MIXED_GROUPS) for k in grp if k in tasks}
 
