@@ -317,6 +317,28 @@ def sharded(args, N, dev, make):
     return StreamShardedEnv(make, N, args.streams, device=str(dev))
 
 
+def _with_hooks(kv: dict, make):
+    """make() with the MGX_* hooks in kv set in the environment (libmgx reads them when a model is
+    created), the previous values restored after"""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update(kv)
+    try:
+        return make()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def mix_parkour_hooks() -> dict:
+    """A/B hook MGX_MIX_PK_PRIO_ROWS: in the mixed run, parkour's solver waves raise their wave
+    priority above this many rows (MGX_PGS_PRIO_ROWS for the parkour model only)"""
+    v = os.environ.get("MGX_MIX_PK_PRIO_ROWS")
+    return {"MGX_PGS_PRIO_ROWS": v} if v else {}
+
+
 def mixed_side_streams(n_tasks: int, mix_streams: int) -> None:
     """The grouped layout runs without the staged tasks' side streams (MGX_SIDE_STREAM=0, a hook
     libmgx reads when a model is created: call this before the envs are built)."""
@@ -373,8 +395,9 @@ def bench_mixed(args, dev, world, rank, dist):
         "humanoid_soccer": (SoccerVectorEnv(N, device=str(dev), precision=args.precision, seed=11, env_offset=off,
                                             banks=args.banks), lambda: torch.rand(N, 33, device=dev, generator=g) * 300 - 150,
                             ALG_BYTES_PER_ENV_STEP_F64 if f64 else ALG_BYTES_PER_ENV_STEP),
-        "quadruped_parkour": (ParkourVectorEnv(N, device=str(dev), precision=args.precision, seed=12, env_offset=off,
-                                               staged=bool(args.mix_staged)),
+        "quadruped_parkour": (_with_hooks(mix_parkour_hooks(), lambda: ParkourVectorEnv(
+                                  N, device=str(dev), precision=args.precision, seed=12, env_offset=off,
+                                  staged=bool(args.mix_staged))),
                               lambda: (torch.rand(N, 16, device=dev, generator=g) * 2 - 1) * plim,
                               PARKOUR_ALG_BYTES_F64 if f64 else PARKOUR_ALG_BYTES),
         "bipedal_rescue": (BipedalVectorEnv(N, device=str(dev), precision=args.precision, seed=13, env_offset=off,
